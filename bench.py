@@ -1,0 +1,340 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident FEC encode+decode throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2c3|c4]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N ...
+
+Workload (one "step" = one pass of the hot path over one batch):
+  c2c3 (default; BASELINE.json configs[1] + configs[2]): per GPU 1,000,000 groups of
+       k=10 data packets x 1200 B (12.0 GB resident in HBM).  A step encodes every group
+       (r=3 parity rows) and then rebuilds, in place, every group with 2 erased shards
+       (positions uniform over the 13 shards, seeded).  value = payload GiB (k*P*G, all
+       ranks) / step time: the rate at which data goes through encode AND decode.
+  c4   (configs[3]): per GPU 1,000,000 groups of k=20 x 1200 B, r=5 encode only.
+
+Multi-GPU: one process per GPU, each with its own contiguous range of the global group
+stream; no data-path collective (groups are independent), a barrier and a MAX
+all-reduce of the elapsed time only.  scaling = "weak".
+
+Prints ONE JSON line on rank 0.  Extra keys: per-kernel timings ("kernels"), the HBM
+roofline of the dominant kernel ("roofline") and the CPU baseline ("cpu_baseline",
+rank 0 at N=1 only; the oracle restatement timed on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "quic-test_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+SEED = 0x5EED0000
+
+CONFIGS = {
+    "c2c3": dict(k=10, r=3, P=1200, groups=1_000_000, erasures=2, decode=True,
+                 workload="C2 encode + C3 decode: k=10 r=3, 1200 B packets, 1M groups/GPU, 2 erasures/group"),
+    "c4": dict(k=20, r=5, P=1200, groups=1_000_000, erasures=0, decode=False,
+               workload="C4 encode: k=20 r=5, 1200 B packets, 1M groups/GPU (8M over 8 GPUs)"),
+}
+
+
+# ----------------------------------------------------------------------------- helpers
+def shard_range(total_groups: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous [g0, g1) slice of the global group stream owned by `rank`."""
+    g0 = total_groups * rank // world
+    g1 = total_groups * (rank + 1) // world
+    return g0, g1
+
+
+def reduce_max(x: float) -> float:
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def reduce_sum(x: float) -> float:
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def barrier() -> None:
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+
+
+def erasure_masks(G: int, n_shards: int, erasures: int, seed: int):
+    """Exactly `erasures` distinct shards lost per group, uniform over n_shards."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    out = np.zeros(G, dtype=np.uint64)
+    chunk = 1 << 18
+    for c0 in range(0, G, chunk):
+        c1 = min(G, c0 + chunk)
+        pos = np.argsort(rng.random((c1 - c0, n_shards)), axis=1)[:, :erasures].astype(np.uint64)
+        out[c0:c1] = np.left_shift(np.uint64(1), pos).sum(axis=1, dtype=np.uint64)
+    return out
+
+
+def decode_algorithmic_bytes(masks, k: int, r: int, P: int) -> int:
+    """Sum over groups with lost data shards of (k + e) * P (read k survivors, write e)."""
+    import numpy as np
+    m = masks & np.uint64((1 << k) - 1)
+    e = np.zeros(len(m), dtype=np.int64)
+    mm = m.copy()
+    while mm.any():
+        e += (mm & np.uint64(1)).astype(np.int64)
+        mm >>= np.uint64(1)
+    pm = (masks >> np.uint64(k)) & np.uint64((1 << r) - 1)
+    alive = np.full(len(m), r, dtype=np.int64)
+    pp = pm.copy()
+    while pp.any():
+        alive -= (pp & np.uint64(1)).astype(np.int64)
+        pp >>= np.uint64(1)
+    ok = (e > 0) & (e <= alive)
+    return int(((k + e[ok]) * P).sum())
+
+
+def cpu_baseline(cfg: dict, seconds: float = 8.0) -> dict:
+    """The oracle restatement (oracle/, test infrastructure) timed on this host: the same
+    workload (encode + 2-erasure decode at k, r, P) on a bounded sample of groups."""
+    import numpy as np
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle
+    k, r, P = cfg["k"], cfg["r"], cfg["P"]
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    G = 20_000
+    data = oracle.splitmix_bytes(G * k * P, SEED + 2)
+    masks = erasure_masks(G, k + r, cfg["erasures"], SEED + 3) if cfg["decode"] else None
+    done, t_total = 0, 0.0
+    while t_total < seconds and done < 2_000_000:
+        t0 = time.perf_counter()
+        par = oracle.rs_encode(data, G, k, r, P, nthreads=threads)
+        if cfg["decode"]:
+            oracle.rs_decode(data, par, masks, G, k, r, P, nthreads=threads)
+        t_total += time.perf_counter() - t0
+        done += G
+    value = done * k * P / t_total / 2**30
+    # The reference's own computation (XOR row only, AVX2 restatement) on the same host.
+    reps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 2.0:
+        oracle.xor_encode_contig(data, G, k, P, nthreads=1)
+        reps += 1
+    xor1 = reps * G * k * P / (time.perf_counter() - t0) / 2**30
+    reps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 2.0:
+        oracle.xor_encode_contig(data, G, k, P, nthreads=threads)
+        reps += 1
+    xorn = reps * G * k * P / (time.perf_counter() - t0) / 2**30
+    # The reference library itself (oracle/_ref: /root/reference's fec_xor_simd.cpp compiled
+    # in this repo's build container), fec_encode_batch, single thread as it is written.
+    ref_gib_s = None
+    ref = oracle.ref_lib()
+    if ref is not None:
+        import numpy as np
+        offs = (np.arange(G * 10, dtype=np.uint32) * P).astype(np.uint32)
+        rep = np.zeros(G * P, dtype=np.uint8)
+        h = ref.fec_encoder_new(0.10, 1024)
+        reps = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 2.0:
+            ref.fec_encode_batch(h, data.ctypes.data, offs.ctypes.data, G * k // 10, P, rep.ctypes.data)
+            reps += 1
+        ref_gib_s = round(reps * G * k * P / (time.perf_counter() - t0) / 2**30, 3)
+        ref.fec_encoder_free(h)
+    cpu_model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                cpu_model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(value, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "sample": f"{done} groups ({G} per pass) of k={k} r={r} P={P}: oracle rs_encode"
+                  + (f" + rs_decode ({cfg['erasures']} erasures/group)" if cfg["decode"] else "")
+                  + f", {threads} threads, {t_total:.1f} s",
+        "cpu_model": cpu_model,
+        "xor_avx2_row0_gib_s": {"threads_1": round(xor1, 3), f"threads_{threads}": round(xorn, 3),
+                                "note": "reference computation only (XOR parity row 0, AVX2 restatement "
+                                        "bit-identical to fec_xor_simd.cpp:74-204)"},
+        "reference_fec_encode_batch_gib_s": ref_gib_s,
+    }
+
+
+def load_pmc_traffic(config: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/pmc_<config>.json),
+    if one exists for this build; else None."""
+    p = REPO / "profiles" / f"pmc_{config}.json"
+    if not p.exists():
+        return None
+    try:
+        return json.loads(p.read_text())
+    except (OSError, ValueError):
+        return None
+
+
+# ----------------------------------------------------------------------------- main
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2c3", choices=sorted(CONFIGS))
+    ap.add_argument("--groups", type=int, default=0, help="groups per GPU (default: the config's)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import quicfec
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    cfg = dict(CONFIGS[args.config])
+    k, r, P = cfg["k"], cfg["r"], cfg["P"]
+    G = args.groups or cfg["groups"]
+    g0, _ = shard_range(G * world, rank, world)
+
+    ctx = quicfec.Context(device=local)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    data = torch.empty(G * k * P, dtype=torch.uint8, device="cuda")
+    parity = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
+    # this rank's slice of one global synthetic stream
+    ctx.fill_random_dev(data, data.numel(), SEED + 2, byte_offset=g0 * k * P, stream=sp)
+    dec_bytes = 0
+    if cfg["decode"]:
+        masks_h = erasure_masks(G, k + r, cfg["erasures"], SEED + 3 + rank)
+        dec_bytes = decode_algorithmic_bytes(masks_h, k, r, P)
+        masks = torch.from_numpy(masks_h.view(np.int64)).to("cuda")
+        ctx.decode_prepare(k, r)
+    torch.cuda.synchronize()
+
+    verified = None
+    if not args.no_verify:
+        # correctness of this exact configuration before timing: encode, poison the erased
+        # data shards, rebuild, compare with the untouched copy; sampled groups vs oracle
+        # parity are covered by tests/test_gpu_parity.py.
+        orig = data.clone()
+        ctx.encode_dev(data, G, k, r, P, parity, stream=sp)
+        if cfg["decode"]:
+            bits = torch.arange(k, device="cuda", dtype=torch.int64)
+            lost = ((masks.view(G, 1) >> bits.view(1, k)) & 1).bool()
+            data.view(G, k, P)[lost] = 0xEE
+            st = torch.zeros(G, dtype=torch.uint8, device="cuda")
+            ctx.decode_dev(data, parity, masks, G, k, r, P, st, stream=sp)
+            torch.cuda.synchronize()
+            verified = bool(torch.equal(data, orig)) and int(st.sum().item()) == 0
+        else:
+            torch.cuda.synchronize()
+            verified = True
+        del orig
+        torch.cuda.empty_cache()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        ctx.encode_dev(data, G, k, r, P, parity, stream=sp)
+        if ev is not None:
+            ev[1].record(stream)
+        if cfg["decode"]:
+            ctx.decode_dev(data, parity, masks, G, k, r, P, None, stream=sp)
+            if ev is not None:
+                ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    dec_ms = (sum(e[1].elapsed_time(e[2]) for e in events) / args.steps) if cfg["decode"] else 0.0
+
+    elapsed_max = reduce_max(elapsed)
+    total_groups = reduce_sum(float(G))
+    payload = total_groups * k * P * args.steps
+    value = payload / elapsed_max / 2**30
+    ms_per_step = elapsed_max / args.steps * 1e3
+
+    enc_bytes = (k + r) * P * G
+    enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
+    kernels = {"encode": {"ms": round(enc_ms, 4), "algorithmic_bytes": enc_bytes,
+                          "achieved_GBps": round(enc_gbs, 1),
+                          "payload_GiBps": round(k * P * G / (enc_ms * 1e-3) / 2**30, 2)}}
+    if cfg["decode"]:
+        dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
+        kernels["decode"] = {"ms": round(dec_ms, 4), "algorithmic_bytes": dec_bytes,
+                             "achieved_GBps": round(dec_gbs, 1),
+                             "payload_GiBps": round(k * P * G / (dec_ms * 1e-3) / 2**30, 2)}
+    dom = max(kernels, key=lambda n: kernels[n]["ms"])
+    pmc = load_pmc_traffic(args.config) or {}
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["achieved_GBps"],
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(kernels[dom]["achieved_GBps"] / HBM_PEAK_GBS, 4),
+                "traffic": pmc.get(dom, {}).get("hbm_bytes_per_launch"),
+                "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes"],
+                "timing": "torch.cuda.Event on the launch stream, averaged over the timed steps"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg)
+
+    if rank == 0:
+        out = {
+            "metric": "FEC encode+decode GiB/s (device-resident), k=10 r=3 1200B pkts, 1/2/4/8 GPU",
+            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (counter-based splitmix64 bytes generated in HBM; seeded erasure masks)",
+            "config": {"workload": cfg["workload"], "k": k, "r": r, "packet_bytes": P,
+                       "groups_per_gpu": G, "erasures_per_group": cfg["erasures"],
+                       "parallelism": f"group-sharded x{world} (no collective)"},
+            "verified": verified,
+            "kernels": kernels,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    ctx.close()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,105 @@
+/*
+ * fec_hip.h — batch GF(2^8) erasure-coding API of libfec_hip.so (new; the reference has
+ * no equivalent).  These are the entry points SURVEY.md §8(b) "New entry points" asks
+ * for: explicit k and r, 64-bit layout, device-pointer variants on a caller stream,
+ * device selection.  Plain C types only.
+ *
+ * Code: byte-wise GF(2^8), polynomial 0x11D, systematic generator
+ * [I_k ; M] with M an r x k Cauchy matrix normalised so that row 0 and column 0 are all
+ * ones.  Parity row 0 is therefore the reference XOR repair packet
+ * (fec_xor_simd.cpp:411-427) byte for byte.  MDS for k + r <= 256.
+ *
+ * Layout (contiguous form):
+ *   data   : G*k*P bytes, data shard (g,j) at (g*k + j)*P
+ *   parity : G*r*P bytes, parity row (g,i) at (g*r + i)*P
+ * Erasure mask of a group: bit s set (s < k+r) => shard s lost; s < k is data shard s,
+ * s >= k is parity row s-k.  Decode requires k + r <= 64.
+ *
+ * Decode rule: erased data shards are rebuilt in place in `data` from every surviving
+ * data shard plus the lowest-indexed surviving parity rows (as many as there are erased
+ * data shards).  A single lost data shard with parity row 0 alive is therefore the
+ * reference XOR recovery (decoder.go:255-287).  Groups with more erased data shards than
+ * surviving parity rows are left untouched and reported unrecoverable.
+ */
+#ifndef FEC_HIP_H
+#define FEC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "fec_xor_simd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Return codes.  -1 keeps the reference's meaning (NULL argument, fec_xor_simd.cpp:564). */
+#define FEC_OK 0
+#define FEC_ERR_NULL (-1)      /* a required pointer is NULL                      */
+#define FEC_ERR_HIP (-2)       /* the HIP runtime reported an error               */
+#define FEC_ERR_RANGE (-3)     /* k, r, packet size or group count unsupported     */
+#define FEC_ERR_NODEV (-4)     /* no usable GPU                                   */
+#define FEC_ERR_NOMEM (-5)     /* device or pinned allocation failed              */
+
+/* Number of visible HIP devices (0 when none or the runtime is unusable). */
+int fec_hip_device_count(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char* fec_hip_last_error(void);
+
+/* fec_encoder_new on an explicit device ordinal (shards of a multi-GPU job). */
+FECEncoderCtx* fec_encoder_new_device(double redundancy, uint32_t max_groups, int device);
+
+/* Device ordinal a context is bound to, or -1 for NULL. */
+int fec_encoder_device(const FECEncoderCtx* ctx);
+
+/* Library build identifier (kernel ISA + version), for logs. */
+const char* fec_hip_version(void);
+
+/* The r x k parity matrix M, row-major (r*k bytes).  0, or FEC_ERR_RANGE. */
+int fec_parity_matrix(uint32_t k, uint32_t r, uint8_t* out);
+
+/* ---- synchronous API: host or device pointers (auto-detected) ----
+ * offsets: NULL for the contiguous layout, else k*num_groups u64 byte offsets into
+ * `data` (data shard (g,j) at data + offsets[g*k + j]); parity is always contiguous. */
+int fec_encode_batch_rs(FECEncoderCtx* ctx, const uint8_t* data, const uint64_t* offsets,
+                        uint64_t num_groups, uint32_t k, uint32_t r, uint32_t packet_size,
+                        uint8_t* parity_out);
+
+/* status_out (nullable): one byte per group, 0 = recovered or nothing lost,
+ * 1 = unrecoverable.  unrecoverable_out (nullable): count of status 1. */
+int fec_decode_batch_rs(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* parity,
+                        const uint64_t* erasure_masks, uint64_t num_groups, uint32_t k,
+                        uint32_t r, uint32_t packet_size, uint8_t* status_out,
+                        uint64_t* unrecoverable_out);
+
+/* ---- device-resident API: device pointers only, asynchronous on `stream`
+ * (a hipStream_t; NULL = the context's own stream).  Contiguous layout only. ---- */
+int fec_encode_batch_rs_dev(FECEncoderCtx* ctx, const uint8_t* d_data, uint64_t num_groups,
+                            uint32_t k, uint32_t r, uint32_t packet_size, uint8_t* d_parity,
+                            void* stream);
+
+/* d_status (nullable) as status_out above, written on the device. */
+int fec_decode_batch_rs_dev(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
+                            const uint64_t* d_erasure_masks, uint64_t num_groups, uint32_t k,
+                            uint32_t r, uint32_t packet_size, uint8_t* d_status, void* stream);
+
+/* Build (and upload) the decode codebook for (k, r) ahead of the first decode.  The
+ * codebook holds the recovery tables of every recoverable erasure pattern; its size is
+ * returned in *bytes_out (nullable).  0, FEC_ERR_RANGE if it would exceed the cap. */
+int fec_decode_prepare(FECEncoderCtx* ctx, uint32_t k, uint32_t r, uint64_t* bytes_out);
+
+/* ---- utilities for benchmarks and tests ---- */
+/* Fill d_dst with the counter-based splitmix64 stream (byte i of the stream at
+ * byte_offset + i), asynchronously on stream. */
+int fec_fill_random_dev(FECEncoderCtx* ctx, uint8_t* d_dst, uint64_t nbytes, uint64_t seed,
+                        uint64_t byte_offset, void* stream);
+
+/* Wait for the context's own stream. */
+int fec_synchronize(FECEncoderCtx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEC_HIP_H */

@@ -1,0 +1,550 @@
+// fec_kernels.hip — gfx950 (MI355X, CDNA4) kernels of libfec_hip.
+//
+// Hot path (SURVEY.md §8(a) a1/a4 and the new GF rows): batched systematic erasure
+// encode and decode of QUIC packet groups.  Byte-field arithmetic, HBM-bound: no MFMA.
+//
+//  * encode_v16<K,R,...>: one lane per 16-byte column of one group (flat over all groups,
+//    so a wave covers 64 consecutive columns and its loads are 1 KiB coalesced rows).
+//    A lane loads its column of all K data packets (K dwordx4 loads in flight), XORs them
+//    into parity row 0 (the reference XOR, fec_xor_simd.cpp:411-427) and multiplies them
+//    into rows 1..R-1 with v_perm_b32 table lookups (3 per dword per coefficient, tables
+//    in SGPRs via scalar loads), then stores R dwordx4.
+//  * classify: one lane per group, erasure mask -> codebook record (rank of the erased
+//    data set and of the parity rows used), status byte.
+//  * decode_v16<K,MAXE>: one wave per group, so the record (survivor list + tables) is
+//    wave-uniform and lives in SGPRs; lanes walk the group's 16-byte columns.
+//  * *_bytes: any packet size / alignment (one lane per byte), same tables.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "fec_kernels.hpp"
+
+namespace qfec {
+namespace {
+
+struct Tab {
+  uint32_t t0lo, t0hi, t1lo, t1hi, t2, coef, p0, p1;
+};
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Selector bytes for the three pieces of every byte of a dword.
+struct Sel {
+  uint32_t s0[4], s1[4], s2[4];
+};
+
+__device__ __forceinline__ void prep(const uint4& x, Sel& s) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    s.s0[q] = w[q] & 0x07070707u;
+    s.s1[q] = (w[q] >> 3) & 0x07070707u;
+    s.s2[q] = (w[q] >> 6) & 0x03030303u;
+  }
+}
+
+// GF(2^8) product of four bytes with the table's constant.
+__device__ __forceinline__ uint32_t gmul(uint32_t s0, uint32_t s1, uint32_t s2, const Tab& t) {
+  return xor3(__builtin_amdgcn_perm(t.t0hi, t.t0lo, s0), __builtin_amdgcn_perm(t.t1hi, t.t1lo, s1),
+              __builtin_amdgcn_perm(t.t2, t.t2, s2));
+}
+
+__device__ __forceinline__ void mac(uint4& acc, const Sel& s, const Tab& t) {
+  acc.x ^= gmul(s.s0[0], s.s1[0], s.s2[0], t);
+  acc.y ^= gmul(s.s0[1], s.s1[1], s.s2[1], t);
+  acc.z ^= gmul(s.s0[2], s.s1[2], s.s2[2], t);
+  acc.w ^= gmul(s.s0[3], s.s1[3], s.s2[3], t);
+}
+
+__device__ __forceinline__ void xor_into(uint4& acc, const uint4& x) {
+  acc.x ^= x.x;
+  acc.y ^= x.y;
+  acc.z ^= x.z;
+  acc.w ^= x.w;
+}
+
+__device__ __forceinline__ uint8_t gmul_byte(uint32_t x, const Tab& t) {
+  return static_cast<uint8_t>(gmul(x & 7u, (x >> 3) & 7u, (x >> 6) & 3u, t));
+}
+
+template <int OFF>
+__device__ __forceinline__ const uint8_t* packet_ptr(const uint8_t* data, const void* offsets,
+                                                     uint64_t g, uint32_t k, uint32_t j, uint32_t P) {
+  if constexpr (OFF == 0) {
+    return data + (g * k + j) * static_cast<uint64_t>(P);
+  } else if constexpr (OFF == 1) {
+    return data + static_cast<const uint32_t*>(offsets)[g * k + j];
+  } else {
+    return data + static_cast<const uint64_t*>(offsets)[g * k + j];
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Encode, 16-byte columns.  K > 0: compile-time group size, all K loads issued before
+// the arithmetic.  K == 0: runtime k, loop.  Rows [row0, row0 + R) of the parity; when
+// FIRST (row0 == 0) row 0 is the plain XOR.  Column 0 of every row is 1 by construction.
+// ---------------------------------------------------------------------------------
+template <int K, int R, int OFF, bool FIRST>
+__global__ __launch_bounds__(256) void encode_v16(const uint8_t* __restrict__ data,
+                                                  const void* __restrict__ offsets,
+                                                  uint8_t* __restrict__ parity, uint64_t g_first,
+                                                  uint32_t nthreads, uint32_t cpp, uint32_t P,
+                                                  uint32_t k_rt, uint32_t r_total, uint32_t row0,
+                                                  const Tab* __restrict__ tabs) {
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  if (t >= nthreads) return;
+  const uint32_t gl = t / cpp;
+  const uint32_t col = t - gl * cpp;
+  const uint64_t g = g_first + gl;
+  const uint32_t k = K > 0 ? static_cast<uint32_t>(K) : k_rt;
+  const size_t coff = static_cast<size_t>(col) * 16u;
+
+  uint4 acc[R];
+  if constexpr (K > 0) {
+    uint4 d[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      d[j] = *reinterpret_cast<const uint4*>(packet_ptr<OFF>(data, offsets, g, K, j, P) + coff);
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[i] = d[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+      if constexpr (FIRST && R == 1) {
+        xor_into(acc[0], d[j]);
+      } else {
+        Sel s;
+        prep(d[j], s);
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+          if (FIRST && i == 0) {
+            xor_into(acc[0], d[j]);
+          } else {
+            const uint32_t row = row0 + static_cast<uint32_t>(i);
+            mac(acc[i], s, tabs[(row - 1) * K + j]);
+          }
+        }
+      }
+    }
+  } else {
+    const uint4 d0 = *reinterpret_cast<const uint4*>(packet_ptr<OFF>(data, offsets, g, k, 0, P) + coff);
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[i] = d0;
+#pragma unroll 4
+    for (uint32_t j = 1; j < k; ++j) {
+      const uint4 x = *reinterpret_cast<const uint4*>(packet_ptr<OFF>(data, offsets, g, k, j, P) + coff);
+      Sel s;
+      prep(x, s);
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        if (FIRST && i == 0) {
+          xor_into(acc[0], x);
+        } else {
+          const uint32_t row = row0 + static_cast<uint32_t>(i);
+          mac(acc[i], s, tabs[(row - 1) * k + j]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    uint8_t* dst = parity + (g * r_total + row0 + static_cast<uint32_t>(i)) * static_cast<uint64_t>(P) + coff;
+    *reinterpret_cast<uint4*>(dst) = acc[i];
+  }
+}
+
+// Encode, one lane per byte (any size / alignment).  All r rows.
+template <int OFF>
+__global__ __launch_bounds__(256) void encode_bytes(const uint8_t* __restrict__ data,
+                                                    const void* __restrict__ offsets,
+                                                    uint8_t* __restrict__ parity, uint64_t g_first,
+                                                    uint32_t nthreads, uint32_t P, uint32_t k,
+                                                    uint32_t r, const Tab* __restrict__ tabs) {
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  if (t >= nthreads) return;
+  const uint32_t gl = t / P;
+  const uint32_t b = t - gl * P;
+  const uint64_t g = g_first + gl;
+  for (uint32_t i = 0; i < r; ++i) {
+    uint32_t acc = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+      const uint32_t x = packet_ptr<OFF>(data, offsets, g, k, j, P)[b];
+      acc ^= (i == 0 || j == 0) ? x : gmul_byte(x, tabs[(i - 1) * k + j]);
+    }
+    parity[(g * r + i) * static_cast<uint64_t>(P) + b] = static_cast<uint8_t>(acc);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Decode
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void classify(const uint64_t* __restrict__ masks, uint64_t groups,
+                                                uint32_t k, uint32_t r,
+                                                const uint64_t* __restrict__ binom, LevelMeta meta,
+                                                uint32_t* __restrict__ rec_off,
+                                                uint8_t* __restrict__ status) {
+  const uint64_t g = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  if (g >= groups) return;
+  const uint64_t m = masks[g];
+  const uint64_t kmask = k >= 64 ? ~0ull : ((1ull << k) - 1);
+  const uint64_t rmask = r >= 64 ? ~0ull : ((1ull << r) - 1);
+  uint64_t dm = m & kmask;
+  const uint64_t pm = (k >= 64) ? 0 : ((m >> k) & rmask);
+  const uint32_t e = __popcll(dm);
+  uint32_t rec = kRecNone;
+  uint8_t st = 0;
+  if (e > 0) {
+    const uint32_t alive = r - __popcll(pm);
+    if (e > alive) {
+      rec = kRecBad;
+      st = 1;
+    } else {
+      uint64_t rank_e = 0, rank_r = 0;
+      for (uint32_t t = 0; dm; ++t) {
+        const uint32_t j = __ffsll(static_cast<unsigned long long>(dm)) - 1;
+        rank_e += binom[j * 65 + t + 1];
+        dm &= dm - 1;
+      }
+      uint64_t sp = ~pm & rmask;
+      for (uint32_t t = 0; t < e; ++t) {
+        const uint32_t i = __ffsll(static_cast<unsigned long long>(sp)) - 1;
+        rank_r += binom[i * 65 + t + 1];
+        sp &= sp - 1;
+      }
+      const uint64_t idx = rank_e * meta.count_r[e] + rank_r;
+      rec = static_cast<uint32_t>((meta.base[e] + idx * meta.stride[e]) >> 5);
+    }
+  }
+  rec_off[g] = rec;
+  if (status) status[g] = st;
+}
+
+__device__ __forceinline__ uint32_t rec_byte(const uint32_t* __restrict__ w, uint32_t i) {
+  return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFu;
+}
+
+// One wave per group.  K > 0: compile-time k (survivor loads all issued first).
+// MAXE: rows rebuilt per pass (rows [m0, m0 + MAXE) of the record's e).
+template <int K, int MAXE>
+__global__ __launch_bounds__(256) void decode_v16(uint8_t* __restrict__ data,
+                                                  const uint8_t* __restrict__ parity,
+                                                  const uint32_t* __restrict__ rec_off,
+                                                  const uint8_t* __restrict__ codebook,
+                                                  uint64_t groups, uint32_t cpp, uint32_t P,
+                                                  uint32_t k_rt, uint32_t r, uint32_t m0) {
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * 4u +
+                      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+  if (gw >= groups) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t rec = __builtin_amdgcn_readfirstlane(rec_off[gw]);
+  if (rec >= kRecBad) return;
+  const uint32_t k = K > 0 ? static_cast<uint32_t>(K) : k_rt;
+  const uint8_t* recp = codebook + static_cast<uint64_t>(rec) * 32u;
+  const uint32_t* rw = reinterpret_cast<const uint32_t*>(recp);
+  const uint32_t e = rw[24] & 0xFFu;
+  const bool xor_only = ((rw[24] >> 8) & 0xFFu) != 0;
+  if (m0 >= e) return;
+  const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
+  uint8_t* dg = data + gw * k * static_cast<uint64_t>(P);
+  const uint8_t* pg = parity + gw * r * static_cast<uint64_t>(P);
+
+  for (uint32_t col = lane; col < cpp; col += 64u) {
+    const size_t coff = static_cast<size_t>(col) * 16u;
+    if (xor_only) {  // single data loss rebuilt from parity row 0: the reference XOR
+      uint4 acc = make_uint4(0, 0, 0, 0);
+      for (uint32_t s = 0; s < k; ++s) {
+        const uint32_t sid = rec_byte(rw, s);
+        const uint8_t* src = sid < k ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - k) * static_cast<uint64_t>(P);
+        xor_into(acc, *reinterpret_cast<const uint4*>(src + coff));
+      }
+      *reinterpret_cast<uint4*>(dg + rec_byte(rw, 64) * static_cast<uint64_t>(P) + coff) = acc;
+      continue;
+    }
+    uint4 acc[MAXE];
+#pragma unroll
+    for (int m = 0; m < MAXE; ++m) acc[m] = make_uint4(0, 0, 0, 0);
+    if constexpr (K > 0) {
+      uint4 x[K];
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        const uint32_t sid = rec_byte(rw, s);
+        const uint8_t* src = sid < k ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - k) * static_cast<uint64_t>(P);
+        x[s] = *reinterpret_cast<const uint4*>(src + coff);
+      }
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        Sel sl;
+        prep(x[s], sl);
+#pragma unroll
+        for (int m = 0; m < MAXE; ++m) {
+          if (m0 + m < e) {
+            const Tab& t = tabs[(m0 + m) * K + s];
+            if (t.coef == 1u) xor_into(acc[m], x[s]);
+            else if (t.coef != 0u) mac(acc[m], sl, t);
+          }
+        }
+      }
+    } else {
+#pragma unroll 2
+      for (uint32_t s = 0; s < k; ++s) {
+        const uint32_t sid = rec_byte(rw, s);
+        const uint8_t* src = sid < k ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - k) * static_cast<uint64_t>(P);
+        const uint4 xv = *reinterpret_cast<const uint4*>(src + coff);
+        Sel sl;
+        prep(xv, sl);
+#pragma unroll
+        for (int m = 0; m < MAXE; ++m) {
+          if (m0 + m < e) {
+            const Tab& t = tabs[(m0 + m) * k + s];
+            if (t.coef == 1u) xor_into(acc[m], xv);
+            else if (t.coef != 0u) mac(acc[m], sl, t);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MAXE; ++m) {
+      if (m0 + m < e) {
+        const uint32_t eid = rec_byte(rw, 64 + m0 + m);
+        *reinterpret_cast<uint4*>(dg + eid * static_cast<uint64_t>(P) + coff) = acc[m];
+      }
+    }
+  }
+}
+
+// Decode, one lane per byte (any size / alignment).
+__global__ __launch_bounds__(256) void decode_bytes(uint8_t* __restrict__ data,
+                                                    const uint8_t* __restrict__ parity,
+                                                    const uint32_t* __restrict__ rec_off,
+                                                    const uint8_t* __restrict__ codebook,
+                                                    uint64_t g_first, uint32_t nthreads, uint32_t P,
+                                                    uint32_t k, uint32_t r) {
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  if (t >= nthreads) return;
+  const uint32_t gl = t / P;
+  const uint32_t b = t - gl * P;
+  const uint64_t g = g_first + gl;
+  const uint32_t rec = rec_off[g];
+  if (rec >= kRecBad) return;
+  const uint8_t* recp = codebook + static_cast<uint64_t>(rec) * 32u;
+  const uint32_t e = recp[96];
+  const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
+  uint8_t* dg = data + g * k * static_cast<uint64_t>(P);
+  const uint8_t* pg = parity + g * r * static_cast<uint64_t>(P);
+  for (uint32_t m = 0; m < e; ++m) {
+    uint32_t acc = 0;
+    for (uint32_t s = 0; s < k; ++s) {
+      const uint32_t sid = recp[s];
+      const uint32_t x = sid < k ? dg[sid * static_cast<uint64_t>(P) + b] : pg[(sid - k) * static_cast<uint64_t>(P) + b];
+      acc ^= gmul_byte(x, tabs[m * k + s]);
+    }
+    // Erased shards are never survivors, so writing here cannot feed a later read.
+    dg[recp[64 + m] * static_cast<uint64_t>(P) + b] = static_cast<uint8_t>(acc);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Synthetic data: counter-based splitmix64 (oracle_fill_splitmix restates it on the CPU).
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void fill_words(uint8_t* __restrict__ dst, uint32_t n16,
+                                                  uint64_t seed, uint64_t word0) {
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  if (t >= n16) return;
+  const uint64_t w = word0 + 2ull * t;
+  const uint64_t a = mix64(seed + (w + 1) * 0x9E3779B97F4A7C15ull);
+  const uint64_t b = mix64(seed + (w + 2) * 0x9E3779B97F4A7C15ull);
+  reinterpret_cast<uint4*>(dst)[t] =
+      make_uint4(static_cast<uint32_t>(a), static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b),
+                 static_cast<uint32_t>(b >> 32));
+}
+
+__global__ __launch_bounds__(256) void fill_bytes(uint8_t* __restrict__ dst, uint32_t n, uint64_t seed,
+                                                  uint64_t pos0) {
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  if (t >= n) return;
+  const uint64_t pos = pos0 + t;
+  const uint64_t w = mix64(seed + (pos / 8 + 1) * 0x9E3779B97F4A7C15ull);
+  dst[t] = static_cast<uint8_t>(w >> (8 * (pos % 8)));
+}
+
+constexpr uint32_t kMaxThreadsPerLaunch = 1u << 30;
+
+inline uint32_t blocks_for(uint64_t n) { return static_cast<uint32_t>((n + 255) / 256); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------------
+namespace {
+
+template <int K, int R, int OFF, bool FIRST>
+hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
+  const uint32_t cpp = a.P / 16u;
+  const uint64_t gchunk = kMaxThreadsPerLaunch / cpp;
+  for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
+    const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
+    const uint32_t n = static_cast<uint32_t>(gn * cpp);
+    hipLaunchKernelGGL((encode_v16<K, R, OFF, FIRST>), dim3(blocks_for(n)), dim3(256), 0, s, a.data,
+                       a.offsets, a.parity, g0, n, cpp, a.P, a.k, a.r, row0,
+                       static_cast<const Tab*>(a.tables));
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+template <int OFF>
+hipError_t run_encode_generic(const EncodeLaunch& a, hipStream_t s) {
+  if (!a.vec16) {
+    const uint64_t gchunk = kMaxThreadsPerLaunch / a.P;
+    for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
+      const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
+      const uint32_t n = static_cast<uint32_t>(gn * a.P);
+      hipLaunchKernelGGL(encode_bytes<OFF>, dim3(blocks_for(n)), dim3(256), 0, s, a.data, a.offsets,
+                         a.parity, g0, n, a.P, a.k, a.r, static_cast<const Tab*>(a.tables));
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  // Runtime k: passes of up to 8 parity rows; the first pass owns the XOR row.
+  for (uint32_t row0 = 0; row0 < a.r; row0 += 8) {
+    const uint32_t rows = (a.r - row0 < 8) ? a.r - row0 : 8;
+    hipError_t e = hipSuccess;
+#define QFEC_PASS(RR)                                                            \
+  case RR:                                                                       \
+    e = row0 == 0 ? run_encode_v16<0, RR, OFF, true>(a, row0, s)                 \
+                  : run_encode_v16<0, RR, OFF, false>(a, row0, s);               \
+    break;
+    switch (rows) {
+      QFEC_PASS(1)
+      QFEC_PASS(2)
+      QFEC_PASS(3)
+      QFEC_PASS(4)
+      QFEC_PASS(5)
+      QFEC_PASS(6)
+      QFEC_PASS(7)
+      QFEC_PASS(8)
+      default:
+        return hipErrorInvalidValue;
+    }
+#undef QFEC_PASS
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
+  if (a.groups == 0) return hipSuccess;
+  if (a.vec16) {
+    if (a.off_kind == OffsetKind::kNone) {
+      if (a.k == 10 && a.r == 3) return run_encode_v16<10, 3, 0, true>(a, 0, s);
+      if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 0, true>(a, 0, s);
+      if (a.k == 20 && a.r == 5) return run_encode_v16<20, 5, 0, true>(a, 0, s);
+      if (a.k == 4 && a.r == 2) return run_encode_v16<4, 2, 0, true>(a, 0, s);
+    } else if (a.off_kind == OffsetKind::kU32) {
+      if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 1, true>(a, 0, s);
+    }
+  }
+  switch (a.off_kind) {
+    case OffsetKind::kNone:
+      return run_encode_generic<0>(a, s);
+    case OffsetKind::kU32:
+      return run_encode_generic<1>(a, s);
+    default:
+      return run_encode_generic<2>(a, s);
+  }
+}
+
+namespace {
+
+template <int K, int MAXE>
+hipError_t run_decode_v16(const DecodeLaunch& a, hipStream_t s) {
+  const uint32_t cpp = a.P / 16u;
+  const uint32_t passes = (a.r + MAXE - 1) / MAXE;  // e <= r
+  for (uint32_t p = 0; p < passes; ++p) {
+    const uint32_t m0 = p * MAXE;
+    const uint64_t blocks = (a.groups + 3) / 4;
+    for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 24)) {
+      const uint64_t bn = (blocks - b0 < (1u << 24)) ? blocks - b0 : (1u << 24);
+      const uint64_t g0 = b0 * 4;
+      const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
+      hipLaunchKernelGGL((decode_v16<K, MAXE>), dim3(static_cast<uint32_t>(bn)), dim3(256), 0, s,
+                         a.data + g0 * a.k * static_cast<uint64_t>(a.P),
+                         a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook,
+                         gn, cpp, a.P, a.k, a.r, m0);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
+  if (a.groups == 0) return hipSuccess;
+  for (uint64_t g0 = 0; g0 < a.groups; g0 += kMaxThreadsPerLaunch) {
+    const uint64_t gn = (a.groups - g0 < kMaxThreadsPerLaunch) ? a.groups - g0 : kMaxThreadsPerLaunch;
+    hipLaunchKernelGGL(classify, dim3(blocks_for(gn)), dim3(256), 0, s, a.masks + g0, gn, a.k, a.r,
+                       a.binom, a.meta, a.rec_off + g0, a.status ? a.status + g0 : nullptr);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (!a.vec16) {
+    const uint64_t gchunk = kMaxThreadsPerLaunch / a.P;
+    for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
+      const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
+      const uint32_t n = static_cast<uint32_t>(gn * a.P);
+      hipLaunchKernelGGL(decode_bytes, dim3(blocks_for(n)), dim3(256), 0, s, a.data, a.parity,
+                         a.rec_off, a.codebook, g0, n, a.P, a.k, a.r);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  if (a.k == 10 && a.r == 3) return run_decode_v16<10, 3>(a, s);
+  if (a.k == 10 && a.r == 1) return run_decode_v16<10, 1>(a, s);
+  if (a.k == 20 && a.r == 5) return run_decode_v16<20, 5>(a, s);
+  if (a.k == 4 && a.r == 2) return run_decode_v16<4, 2>(a, s);
+  return run_decode_v16<0, 8>(a, s);
+}
+
+hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
+                                hipStream_t s) {
+  if (nbytes == 0) return hipSuccess;
+  const bool fast = (byte_offset % 8 == 0) && (reinterpret_cast<uintptr_t>(dst) % 16 == 0);
+  uint64_t done = 0;
+  if (fast) {
+    const uint64_t n16 = nbytes / 16;
+    for (uint64_t c0 = 0; c0 < n16; c0 += kMaxThreadsPerLaunch) {
+      const uint64_t cn = (n16 - c0 < kMaxThreadsPerLaunch) ? n16 - c0 : kMaxThreadsPerLaunch;
+      hipLaunchKernelGGL(fill_words, dim3(blocks_for(cn)), dim3(256), 0, s, dst + c0 * 16,
+                         static_cast<uint32_t>(cn), seed, (byte_offset / 8) + 2 * c0);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    done = n16 * 16;
+  }
+  for (uint64_t c0 = done; c0 < nbytes; c0 += kMaxThreadsPerLaunch) {
+    const uint64_t cn = (nbytes - c0 < kMaxThreadsPerLaunch) ? nbytes - c0 : kMaxThreadsPerLaunch;
+    hipLaunchKernelGGL(fill_bytes, dim3(blocks_for(cn)), dim3(256), 0, s, dst + c0,
+                       static_cast<uint32_t>(cn), seed, byte_offset + c0);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace qfec

@@ -1,0 +1,54 @@
+// fec_kernels.hpp — launch interface between the C-ABI shim (fec_shim.cpp) and the
+// gfx950 kernels (fec_kernels.hip).  Internal to libfec_hip.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace qfec {
+
+// Byte offsets of packets, when the data shards are not contiguous.
+enum class OffsetKind : int { kNone = 0, kU32 = 1, kU64 = 2 };
+
+struct EncodeLaunch {
+  const uint8_t* data;       // base of the data shards (device address)
+  const void* offsets;       // device u32/u64 offsets (k per group) or nullptr
+  OffsetKind off_kind;
+  uint8_t* parity;           // parity row (g, i) at (g * r + i) * P
+  uint64_t groups;
+  uint32_t k, r, P;
+  const void* tables;        // (r-1) x k CoefEntry (rows 1..r-1), device
+  bool vec16;                // P % 16 == 0 and every packet 16-byte aligned
+};
+
+struct LevelMeta {           // codebook levels e = 1..32 (see gf256.hpp)
+  uint64_t base[33];
+  uint64_t stride[33];
+  uint64_t count_r[33];      // C(r, e)
+};
+
+struct DecodeLaunch {
+  uint8_t* data;
+  const uint8_t* parity;
+  const uint64_t* masks;
+  uint32_t* rec_off;         // workspace, one u32 per group
+  uint8_t* status;           // nullable
+  const uint8_t* codebook;   // device
+  const uint64_t* binom;     // device, 65 x 65
+  LevelMeta meta;
+  uint64_t groups;
+  uint32_t k, r, P;
+  bool vec16;
+};
+
+hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s);
+hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s);
+hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
+                                hipStream_t s);
+
+// Records marking "nothing to do" / "unrecoverable" in rec_off.
+constexpr uint32_t kRecNone = 0xFFFFFFFFu;
+constexpr uint32_t kRecBad = 0xFFFFFFFEu;
+
+}  // namespace qfec

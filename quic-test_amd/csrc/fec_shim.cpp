@@ -1,0 +1,728 @@
+// fec_shim.cpp — C-ABI of libfec_hip.so (include/fec_xor_simd.h, include/fec_hip.h).
+//
+// Replaces the reference's native library internal/fec/fec_xor_simd.cpp behind the
+// same eleven symbols, and adds the batch GF(2^8) encode/decode API.  All arithmetic
+// runs in the gfx950 kernels of fec_kernels.hip; this file owns contexts, device
+// buffers, host<->device staging, per-(k,r) plans and error reporting.
+//
+// Threading (SURVEY.md §8(b) "Threading"): one context per caller stream of work; every
+// entry point locks its context and binds the context's device for the duration of the
+// call (Go goroutines migrate between OS threads and the HIP current device is
+// thread-local), restoring the caller's device afterwards.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "fec_hip.h"
+#include "fec_kernels.hpp"
+#include "gf256.hpp"
+
+#define QFEC_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+thread_local std::string g_last_error;
+
+void set_error(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  set_error("%s: %s", what, hipGetErrorString(e));
+  return FEC_ERR_HIP;
+}
+
+#define QFEC_HIP(call)                                 \
+  do {                                                 \
+    const hipError_t qfec_e_ = (call);                 \
+    if (qfec_e_ != hipSuccess) return hip_fail(qfec_e_, #call); \
+  } while (0)
+
+// Binds a device for the scope, restores the caller's device on exit.
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+    if (!ok) (void)hipGetLastError();
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// Grow-only device buffer.
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (ptr) {
+      (void)hipFree(ptr);
+      ptr = nullptr;
+      cap = 0;
+    }
+    size_t want = bytes < 256 ? 256 : bytes;
+    hipError_t e = hipMalloc(&ptr, want);
+    if (e != hipSuccess) {
+      ptr = nullptr;
+      return e;
+    }
+    cap = want;
+    return hipSuccess;
+  }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(ptr); }
+};
+
+struct EncodePlan {
+  DevBuf tables;  // (r-1) * k CoefEntry
+};
+
+struct DecodePlan {
+  qfec::CodebookLayout layout;
+  DevBuf codebook;
+};
+
+constexpr uint64_t kCodebookCap = 2ull << 30;  // 2 GiB of recovery tables per (k, r)
+
+enum class Mem { kHost, kPinned, kDevice };
+
+Mem classify_ptr(const void* p) {
+  if (!p) return Mem::kHost;
+  hipPointerAttribute_t attr;
+  std::memset(&attr, 0, sizeof(attr));
+  const hipError_t e = hipPointerGetAttributes(&attr, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return Mem::kHost;
+  }
+  if (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) return Mem::kDevice;
+  if (attr.type == hipMemoryTypeHost) return Mem::kPinned;
+  return Mem::kHost;
+}
+
+}  // namespace
+
+struct FECEncoderCtx {
+  double redundancy = 0.10;
+  uint32_t max_groups = 1024;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  // staging / workspace buffers
+  DevBuf d_in, d_off, d_out, d_mask, d_status, d_rec, d_binom;
+  std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<EncodePlan>> enc_plans;
+  std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<DecodePlan>> dec_plans;
+
+  ~FECEncoderCtx() {
+    DeviceGuard g(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    d_in.release();
+    d_off.release();
+    d_out.release();
+    d_mask.release();
+    d_status.release();
+    d_rec.release();
+    d_binom.release();
+    enc_plans.clear();
+    for (auto& kv : dec_plans) kv.second->codebook.release();
+    dec_plans.clear();
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+FECEncoderCtx* make_ctx(double redundancy, uint32_t max_groups, int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    set_error("fec_encoder_new: no HIP device available");
+    return nullptr;
+  }
+  if (device < 0) {
+    if (hipGetDevice(&device) != hipSuccess) device = 0;
+  }
+  if (device >= n) {
+    set_error("fec_encoder_new: device %d out of range (%d devices)", device, n);
+    return nullptr;
+  }
+  DeviceGuard g(device);
+  if (!g.ok) {
+    set_error("fec_encoder_new: hipSetDevice(%d) failed", device);
+    return nullptr;
+  }
+  auto* ctx = new FECEncoderCtx();
+  // fec_xor_simd.cpp:540-541 defaults
+  ctx->redundancy = (redundancy > 0 && redundancy <= 1.0) ? redundancy : 0.10;
+  ctx->max_groups = max_groups > 0 ? max_groups : 1024;
+  ctx->device = device;
+  const hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    set_error("fec_encoder_new: hipStreamCreate: %s", hipGetErrorString(e));
+    ctx->stream = nullptr;
+    delete ctx;
+    return nullptr;
+  }
+  return ctx;
+}
+
+int get_encode_plan(FECEncoderCtx* ctx, uint32_t k, uint32_t r, const void** tables) {
+  auto key = std::make_pair(k, r);
+  auto it = ctx->enc_plans.find(key);
+  if (it == ctx->enc_plans.end()) {
+    std::vector<uint8_t> M;
+    if (!qfec::parity_matrix(k, r, M)) {
+      set_error("encode: unsupported k=%u r=%u (need k>0, r>0, k+r<=256)", k, r);
+      return FEC_ERR_RANGE;
+    }
+    auto plan = std::make_unique<EncodePlan>();
+    if (r > 1) {
+      std::vector<qfec::CoefEntry> tab(size_t(r - 1) * k);
+      for (uint32_t i = 1; i < r; ++i)
+        for (uint32_t j = 0; j < k; ++j) tab[(i - 1) * k + j] = qfec::make_entry(M[i * k + j]);
+      QFEC_HIP(plan->tables.ensure(tab.size() * sizeof(qfec::CoefEntry)));
+      QFEC_HIP(hipMemcpy(plan->tables.ptr, tab.data(), tab.size() * sizeof(qfec::CoefEntry),
+                         hipMemcpyHostToDevice));
+    }
+    it = ctx->enc_plans.emplace(key, std::move(plan)).first;
+  }
+  *tables = it->second->tables.ptr;
+  return FEC_OK;
+}
+
+int get_decode_plan(FECEncoderCtx* ctx, uint32_t k, uint32_t r, DecodePlan** out) {
+  auto key = std::make_pair(k, r);
+  auto it = ctx->dec_plans.find(key);
+  if (it == ctx->dec_plans.end()) {
+    auto plan = std::make_unique<DecodePlan>();
+    if (!qfec::codebook_layout(k, r, kCodebookCap, plan->layout)) {
+      set_error("decode: unsupported k=%u r=%u (need k+r<=64 and a codebook <= %llu bytes)", k, r,
+                (unsigned long long)kCodebookCap);
+      return FEC_ERR_RANGE;
+    }
+    std::vector<uint8_t> M, book;
+    qfec::parity_matrix(k, r, M);
+    if (!qfec::build_codebook(plan->layout, M, book)) {
+      set_error("decode: singular recovery submatrix for k=%u r=%u", k, r);
+      return FEC_ERR_RANGE;
+    }
+    QFEC_HIP(plan->codebook.ensure(book.size()));
+    QFEC_HIP(hipMemcpy(plan->codebook.ptr, book.data(), book.size(), hipMemcpyHostToDevice));
+    if (!ctx->d_binom.ptr) {
+      QFEC_HIP(ctx->d_binom.ensure(sizeof(qfec::binom().c)));
+      QFEC_HIP(hipMemcpy(ctx->d_binom.ptr, qfec::binom().c, sizeof(qfec::binom().c),
+                         hipMemcpyHostToDevice));
+    }
+    it = ctx->dec_plans.emplace(key, std::move(plan)).first;
+  }
+  *out = it->second.get();
+  return FEC_OK;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+hipStream_t pick_stream(FECEncoderCtx* ctx, void* stream) {
+  return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+// Device-resident encode, contiguous layout.  Caller holds ctx->mu and the device.
+int encode_dev_locked(FECEncoderCtx* ctx, const uint8_t* d_data, const void* d_offsets,
+                      qfec::OffsetKind ok, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
+                      uint8_t* d_parity, bool vec16, hipStream_t s) {
+  const void* tables = nullptr;
+  int rc = get_encode_plan(ctx, k, r, &tables);
+  if (rc != FEC_OK) return rc;
+  qfec::EncodeLaunch a;
+  a.data = d_data;
+  a.offsets = d_offsets;
+  a.off_kind = ok;
+  a.parity = d_parity;
+  a.groups = G;
+  a.k = k;
+  a.r = r;
+  a.P = P;
+  a.tables = tables;
+  a.vec16 = vec16;
+  QFEC_HIP(qfec::launch_encode(a, s));
+  return FEC_OK;
+}
+
+int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
+                      const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
+                      uint8_t* d_status, bool vec16, hipStream_t s) {
+  DecodePlan* plan = nullptr;
+  int rc = get_decode_plan(ctx, k, r, &plan);
+  if (rc != FEC_OK) return rc;
+  QFEC_HIP(ctx->d_rec.ensure(G * sizeof(uint32_t)));
+  qfec::DecodeLaunch a;
+  a.data = d_data;
+  a.parity = d_parity;
+  a.masks = d_masks;
+  a.rec_off = ctx->d_rec.as<uint32_t>();
+  a.status = d_status;
+  a.codebook = plan->codebook.as<uint8_t>();
+  a.binom = ctx->d_binom.as<uint64_t>();
+  std::memset(&a.meta, 0, sizeof(a.meta));
+  for (uint32_t e = 1; e <= 32; ++e) {
+    a.meta.base[e] = plan->layout.level_base[e];
+    a.meta.stride[e] = plan->layout.level_stride[e];
+    a.meta.count_r[e] = qfec::binom().c[r][e];
+  }
+  a.groups = G;
+  a.k = k;
+  a.r = r;
+  a.P = P;
+  a.vec16 = vec16;
+  QFEC_HIP(qfec::launch_decode(a, s));
+  return FEC_OK;
+}
+
+// Process-wide context used by the context-free xor_packets_* entry points.
+FECEncoderCtx* default_ctx() {
+  static std::once_flag once;
+  static FECEncoderCtx* ctx = nullptr;
+  std::call_once(once, [] { ctx = make_ctx(0.10, 1024, -1); });
+  return ctx;
+}
+
+void xor_packets_gpu(const uint8_t* packets[], size_t n, size_t packet_size, uint8_t* repair) {
+  if (n == 0 || packet_size == 0) return;  // fec_xor_simd.cpp:417-419
+  if (!packets || !repair) {
+    set_error("xor_packets: NULL argument");
+    return;
+  }
+  if (packet_size > 0xFFFFFFFFull || n > 0xFFFFFFFFull) {
+    set_error("xor_packets: size out of range");
+    return;
+  }
+  FECEncoderCtx* ctx = default_ctx();
+  if (!ctx) return;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  const uint32_t P = static_cast<uint32_t>(packet_size);
+  // Stage the packets contiguously (k = n, one group, r = 1).
+  if (ctx->d_in.ensure(n * packet_size) != hipSuccess || ctx->d_out.ensure(packet_size) != hipSuccess) {
+    set_error("xor_packets: device allocation failed");
+    return;
+  }
+  for (size_t p = 0; p < n; ++p) {
+    if (hipMemcpyAsync(ctx->d_in.as<uint8_t>() + p * packet_size, packets[p], packet_size,
+                       hipMemcpyDefault, ctx->stream) != hipSuccess) {
+      set_error("xor_packets: H2D copy failed");
+      return;
+    }
+  }
+  const bool vec16 = (P % 16u) == 0;
+  if (encode_dev_locked(ctx, ctx->d_in.as<uint8_t>(), nullptr, qfec::OffsetKind::kNone, 1,
+                        static_cast<uint32_t>(n), 1, P, ctx->d_out.as<uint8_t>(), vec16,
+                        ctx->stream) != FEC_OK)
+    return;
+  if (hipMemcpyAsync(repair, ctx->d_out.ptr, packet_size, hipMemcpyDefault, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    set_error("xor_packets: D2H copy failed");
+  }
+}
+
+}  // namespace
+
+// =====================================================================================
+// Reference ABI (include/fec_xor_simd.h)
+// =====================================================================================
+
+QFEC_EXPORT FECEncoderCtx* fec_encoder_new(double redundancy, uint32_t max_groups) {
+  return make_ctx(redundancy, max_groups, -1);
+}
+
+QFEC_EXPORT void fec_encoder_free(FECEncoderCtx* ctx) { delete ctx; }
+
+QFEC_EXPORT void* fec_alloc_slab(size_t size) {
+  const size_t aligned = (size + 63) & ~size_t(63);  // fec_xor_simd.cpp:471
+  void* p = nullptr;
+  const hipError_t e = hipHostMalloc(&p, aligned == 0 ? 64 : aligned, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("fec_alloc_slab(%zu): %s", size, hipGetErrorString(e));
+    return nullptr;
+  }
+  return p;
+}
+
+QFEC_EXPORT void* fec_alloc_slab_numa(size_t size, int numa_node) {
+  (void)numa_node;  // placement of pinned pages is left to the HIP runtime
+  return fec_alloc_slab(size);
+}
+
+QFEC_EXPORT void* fec_alloc_repair_buffer(size_t size) { return fec_alloc_slab(size); }
+
+QFEC_EXPORT void fec_free_slab(void* ptr) {
+  if (ptr) (void)hipHostFree(ptr);
+}
+
+QFEC_EXPORT void fec_free_repair_buffer(void* ptr) { fec_free_slab(ptr); }
+
+QFEC_EXPORT int fec_encode_batch(FECEncoderCtx* ctx, const uint8_t* slab, const uint32_t* offsets,
+                                 uint32_t num_groups, uint32_t packet_size, uint8_t* repair_out) {
+  // fec_xor_simd.cpp:564-570, same order
+  if (ctx == nullptr || slab == nullptr || offsets == nullptr || repair_out == nullptr) return -1;
+  if (num_groups == 0 || packet_size == 0) return 0;
+  constexpr uint32_t kPackets = 10;  // fec_xor_simd.cpp:580
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) {
+    set_error("fec_encode_batch: cannot bind device %d", ctx->device);
+    return FEC_ERR_NODEV;
+  }
+  const uint64_t noff = uint64_t(num_groups) * kPackets;
+  const uint64_t P = packet_size;
+  const Mem slab_mem = classify_ptr(slab);
+  const Mem off_mem = classify_ptr(offsets);
+  const Mem out_mem = classify_ptr(repair_out);
+  hipStream_t s = ctx->stream;
+
+  const uint8_t* d_slab = slab;
+  const uint32_t* d_offsets = offsets;
+  bool vec16 = (P % 16u) == 0;
+  if (slab_mem != Mem::kDevice || off_mem != Mem::kDevice) {
+    // Host offsets: read them here to size the slab window and check alignment.
+    std::vector<uint32_t> host_off;
+    const uint32_t* hoff = offsets;
+    if (off_mem == Mem::kDevice) {
+      host_off.resize(noff);
+      QFEC_HIP(hipMemcpy(host_off.data(), offsets, noff * 4, hipMemcpyDeviceToHost));
+      hoff = host_off.data();
+    }
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    for (uint64_t i = 0; i < noff; ++i) {
+      lo = hoff[i] < lo ? hoff[i] : lo;
+      hi = hoff[i] > hi ? hoff[i] : hi;
+    }
+    if (slab_mem == Mem::kDevice) {
+      for (uint64_t i = 0; i < noff && vec16; ++i) vec16 = aligned16(slab + hoff[i]);
+      if (off_mem != Mem::kDevice) {
+        QFEC_HIP(ctx->d_off.ensure(noff * 4));
+        QFEC_HIP(hipMemcpyAsync(ctx->d_off.ptr, hoff, noff * 4, hipMemcpyHostToDevice, s));
+        d_offsets = ctx->d_off.as<uint32_t>();
+      }
+    } else {
+      // Copy the window [lo, hi + P) of the host slab; rebase offsets to it.
+      const uint64_t span = uint64_t(hi) + P - lo;
+      std::vector<uint32_t> rebased(noff);
+      for (uint64_t i = 0; i < noff; ++i) {
+        rebased[i] = hoff[i] - lo;
+        vec16 = vec16 && (rebased[i] % 16u) == 0;
+      }
+      QFEC_HIP(ctx->d_in.ensure(span));
+      QFEC_HIP(ctx->d_off.ensure(noff * 4));
+      QFEC_HIP(hipMemcpyAsync(ctx->d_in.ptr, slab + lo, span, hipMemcpyHostToDevice, s));
+      QFEC_HIP(hipMemcpyAsync(ctx->d_off.ptr, rebased.data(), noff * 4, hipMemcpyHostToDevice, s));
+      QFEC_HIP(hipStreamSynchronize(s));  // `rebased` dies at scope end
+      d_slab = ctx->d_in.as<uint8_t>();
+      d_offsets = ctx->d_off.as<uint32_t>();
+    }
+  } else {
+    // Both on the device: alignment of the packets is unknown without reading offsets.
+    std::vector<uint32_t> host_off(noff);
+    QFEC_HIP(hipMemcpy(host_off.data(), offsets, noff * 4, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < noff && vec16; ++i) vec16 = aligned16(slab + host_off[i]);
+  }
+  uint8_t* d_repair = repair_out;
+  if (out_mem != Mem::kDevice) {
+    QFEC_HIP(ctx->d_out.ensure(uint64_t(num_groups) * P));
+    d_repair = ctx->d_out.as<uint8_t>();
+  }
+  const int rc = encode_dev_locked(ctx, d_slab, d_offsets, qfec::OffsetKind::kU32, num_groups,
+                                   kPackets, 1, packet_size, d_repair, vec16, s);
+  if (rc != FEC_OK) return rc;
+  if (out_mem != Mem::kDevice)
+    QFEC_HIP(hipMemcpyAsync(repair_out, d_repair, uint64_t(num_groups) * P, hipMemcpyDeviceToHost, s));
+  QFEC_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+QFEC_EXPORT xor_impl_fn fec_select_xor_impl(void) { return xor_packets_gpu; }
+
+QFEC_EXPORT void xor_packets_scalar(const uint8_t* packets[], size_t n, size_t packet_size,
+                                    uint8_t* repair) {
+  xor_packets_gpu(packets, n, packet_size, repair);
+}
+QFEC_EXPORT void xor_packets_avx2(const uint8_t* packets[], size_t n, size_t packet_size,
+                                  uint8_t* repair) {
+  xor_packets_gpu(packets, n, packet_size, repair);
+}
+QFEC_EXPORT void xor_packets_avx512(const uint8_t* packets[], size_t n, size_t packet_size,
+                                    uint8_t* repair) {
+  xor_packets_gpu(packets, n, packet_size, repair);
+}
+QFEC_EXPORT void xor_packets_neon(const uint8_t* packets[], size_t n, size_t packet_size,
+                                  uint8_t* repair) {
+  xor_packets_gpu(packets, n, packet_size, repair);
+}
+
+// =====================================================================================
+// Batch GF(2^8) API (include/fec_hip.h)
+// =====================================================================================
+
+QFEC_EXPORT int fec_hip_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+QFEC_EXPORT const char* fec_hip_last_error(void) { return g_last_error.c_str(); }
+
+QFEC_EXPORT FECEncoderCtx* fec_encoder_new_device(double redundancy, uint32_t max_groups, int device) {
+  if (device < 0) {
+    set_error("fec_encoder_new_device: negative device");
+    return nullptr;
+  }
+  return make_ctx(redundancy, max_groups, device);
+}
+
+QFEC_EXPORT int fec_encoder_device(const FECEncoderCtx* ctx) { return ctx ? ctx->device : -1; }
+
+QFEC_EXPORT const char* fec_hip_version(void) { return "libfec_hip 0.1 gfx950"; }
+
+QFEC_EXPORT int fec_parity_matrix(uint32_t k, uint32_t r, uint8_t* out) {
+  if (!out) return FEC_ERR_NULL;
+  std::vector<uint8_t> M;
+  if (!qfec::parity_matrix(k, r, M)) return FEC_ERR_RANGE;
+  std::memcpy(out, M.data(), M.size());
+  return FEC_OK;
+}
+
+namespace {
+
+int check_shape(uint64_t G, uint32_t k, uint32_t r, uint32_t P, bool decode) {
+  if (k == 0 || r == 0 || k + r > (decode ? qfec::kMaxDecodeShards : 256u)) {
+    set_error("unsupported k=%u r=%u", k, r);
+    return FEC_ERR_RANGE;
+  }
+  if (P == 0 && G != 0) {
+    set_error("packet_size must be > 0");
+    return FEC_ERR_RANGE;
+  }
+  return FEC_OK;
+}
+
+}  // namespace
+
+QFEC_EXPORT int fec_encode_batch_rs(FECEncoderCtx* ctx, const uint8_t* data, const uint64_t* offsets,
+                                    uint64_t G, uint32_t k, uint32_t r, uint32_t P, uint8_t* parity_out) {
+  if (!ctx || !data || !parity_out) return FEC_ERR_NULL;
+  int rc = check_shape(G, k, r, P, false);
+  if (rc != FEC_OK) return rc;
+  if (G == 0) return FEC_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return FEC_ERR_NODEV;
+  hipStream_t s = ctx->stream;
+  const uint64_t nin = G * k;
+  const uint64_t out_bytes = G * r * uint64_t(P);
+  const Mem dmem = classify_ptr(data);
+  const Mem omem = classify_ptr(parity_out);
+  const uint8_t* d_data = data;
+  const void* d_off = nullptr;
+  qfec::OffsetKind ok = qfec::OffsetKind::kNone;
+  bool vec16 = (P % 16u) == 0;
+  std::vector<uint64_t> rebased;
+  if (offsets) {
+    ok = qfec::OffsetKind::kU64;
+    const Mem offmem = classify_ptr(offsets);
+    std::vector<uint64_t> host_off;
+    const uint64_t* hoff = offsets;
+    if (offmem == Mem::kDevice) {
+      host_off.resize(nin);
+      QFEC_HIP(hipMemcpy(host_off.data(), offsets, nin * 8, hipMemcpyDeviceToHost));
+      hoff = host_off.data();
+    }
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint64_t i = 0; i < nin; ++i) {
+      lo = hoff[i] < lo ? hoff[i] : lo;
+      hi = hoff[i] > hi ? hoff[i] : hi;
+    }
+    if (dmem == Mem::kDevice) {
+      for (uint64_t i = 0; i < nin && vec16; ++i) vec16 = aligned16(data + hoff[i]);
+      if (offmem != Mem::kDevice) {
+        QFEC_HIP(ctx->d_off.ensure(nin * 8));
+        QFEC_HIP(hipMemcpyAsync(ctx->d_off.ptr, hoff, nin * 8, hipMemcpyHostToDevice, s));
+        QFEC_HIP(hipStreamSynchronize(s));
+        d_off = ctx->d_off.ptr;
+      } else {
+        d_off = offsets;
+      }
+    } else {
+      const uint64_t span = hi + P - lo;
+      rebased.resize(nin);
+      for (uint64_t i = 0; i < nin; ++i) {
+        rebased[i] = hoff[i] - lo;
+        vec16 = vec16 && (rebased[i] % 16u) == 0;
+      }
+      QFEC_HIP(ctx->d_in.ensure(span));
+      QFEC_HIP(ctx->d_off.ensure(nin * 8));
+      QFEC_HIP(hipMemcpyAsync(ctx->d_in.ptr, data + lo, span, hipMemcpyHostToDevice, s));
+      QFEC_HIP(hipMemcpyAsync(ctx->d_off.ptr, rebased.data(), nin * 8, hipMemcpyHostToDevice, s));
+      d_data = ctx->d_in.as<uint8_t>();
+      d_off = ctx->d_off.ptr;
+    }
+  } else {
+    if (dmem != Mem::kDevice) {
+      QFEC_HIP(ctx->d_in.ensure(nin * P));
+      QFEC_HIP(hipMemcpyAsync(ctx->d_in.ptr, data, nin * P, hipMemcpyHostToDevice, s));
+      d_data = ctx->d_in.as<uint8_t>();
+    } else {
+      vec16 = vec16 && aligned16(data);
+    }
+  }
+  uint8_t* d_par = parity_out;
+  if (omem != Mem::kDevice) {
+    QFEC_HIP(ctx->d_out.ensure(out_bytes));
+    d_par = ctx->d_out.as<uint8_t>();
+  } else {
+    vec16 = vec16 && aligned16(parity_out);
+  }
+  rc = encode_dev_locked(ctx, d_data, d_off, ok, G, k, r, P, d_par, vec16, s);
+  if (rc != FEC_OK) return rc;
+  if (omem != Mem::kDevice)
+    QFEC_HIP(hipMemcpyAsync(parity_out, d_par, out_bytes, hipMemcpyDeviceToHost, s));
+  QFEC_HIP(hipStreamSynchronize(s));
+  return FEC_OK;
+}
+
+QFEC_EXPORT int fec_decode_batch_rs(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* parity,
+                                    const uint64_t* masks, uint64_t G, uint32_t k, uint32_t r,
+                                    uint32_t P, uint8_t* status_out, uint64_t* unrecoverable_out) {
+  if (!ctx || !data || !parity || !masks) return FEC_ERR_NULL;
+  int rc = check_shape(G, k, r, P, true);
+  if (rc != FEC_OK) return rc;
+  if (unrecoverable_out) *unrecoverable_out = 0;
+  if (G == 0) return FEC_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return FEC_ERR_NODEV;
+  hipStream_t s = ctx->stream;
+  const uint64_t data_bytes = G * k * uint64_t(P);
+  const uint64_t par_bytes = G * r * uint64_t(P);
+  const Mem dmem = classify_ptr(data), pmem = classify_ptr(parity), mmem = classify_ptr(masks);
+  uint8_t* d_data = data;
+  const uint8_t* d_par = parity;
+  const uint64_t* d_masks = masks;
+  bool vec16 = (P % 16u) == 0;
+  if (dmem != Mem::kDevice) {
+    QFEC_HIP(ctx->d_in.ensure(data_bytes));
+    QFEC_HIP(hipMemcpyAsync(ctx->d_in.ptr, data, data_bytes, hipMemcpyHostToDevice, s));
+    d_data = ctx->d_in.as<uint8_t>();
+  } else {
+    vec16 = vec16 && aligned16(data);
+  }
+  if (pmem != Mem::kDevice) {
+    QFEC_HIP(ctx->d_out.ensure(par_bytes));
+    QFEC_HIP(hipMemcpyAsync(ctx->d_out.ptr, parity, par_bytes, hipMemcpyHostToDevice, s));
+    d_par = ctx->d_out.as<uint8_t>();
+  } else {
+    vec16 = vec16 && aligned16(parity);
+  }
+  if (mmem != Mem::kDevice) {
+    QFEC_HIP(ctx->d_mask.ensure(G * 8));
+    QFEC_HIP(hipMemcpyAsync(ctx->d_mask.ptr, masks, G * 8, hipMemcpyHostToDevice, s));
+    d_masks = ctx->d_mask.as<uint64_t>();
+  }
+  QFEC_HIP(ctx->d_status.ensure(G));
+  rc = decode_dev_locked(ctx, d_data, d_par, d_masks, G, k, r, P, ctx->d_status.as<uint8_t>(), vec16, s);
+  if (rc != FEC_OK) return rc;
+  if (dmem != Mem::kDevice)
+    QFEC_HIP(hipMemcpyAsync(data, d_data, data_bytes, hipMemcpyDeviceToHost, s));
+  std::vector<uint8_t> st(G);
+  QFEC_HIP(hipMemcpyAsync(st.data(), ctx->d_status.ptr, G, hipMemcpyDeviceToHost, s));
+  QFEC_HIP(hipStreamSynchronize(s));
+  uint64_t bad = 0;
+  for (uint64_t g = 0; g < G; ++g) bad += st[g] != 0;
+  if (status_out) std::memcpy(status_out, st.data(), G);
+  if (unrecoverable_out) *unrecoverable_out = bad;
+  return FEC_OK;
+}
+
+QFEC_EXPORT int fec_encode_batch_rs_dev(FECEncoderCtx* ctx, const uint8_t* d_data, uint64_t G,
+                                        uint32_t k, uint32_t r, uint32_t P, uint8_t* d_parity,
+                                        void* stream) {
+  if (!ctx || !d_data || !d_parity) return FEC_ERR_NULL;
+  int rc = check_shape(G, k, r, P, false);
+  if (rc != FEC_OK) return rc;
+  if (G == 0) return FEC_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return FEC_ERR_NODEV;
+  const bool vec16 = (P % 16u) == 0 && aligned16(d_data) && aligned16(d_parity);
+  return encode_dev_locked(ctx, d_data, nullptr, qfec::OffsetKind::kNone, G, k, r, P, d_parity, vec16,
+                           pick_stream(ctx, stream));
+}
+
+QFEC_EXPORT int fec_decode_batch_rs_dev(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
+                                        const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r,
+                                        uint32_t P, uint8_t* d_status, void* stream) {
+  if (!ctx || !d_data || !d_parity || !d_masks) return FEC_ERR_NULL;
+  int rc = check_shape(G, k, r, P, true);
+  if (rc != FEC_OK) return rc;
+  if (G == 0) return FEC_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return FEC_ERR_NODEV;
+  const bool vec16 = (P % 16u) == 0 && aligned16(d_data) && aligned16(d_parity);
+  return decode_dev_locked(ctx, d_data, d_parity, d_masks, G, k, r, P, d_status, vec16,
+                           pick_stream(ctx, stream));
+}
+
+QFEC_EXPORT int fec_decode_prepare(FECEncoderCtx* ctx, uint32_t k, uint32_t r, uint64_t* bytes_out) {
+  if (!ctx) return FEC_ERR_NULL;
+  int rc = check_shape(1, k, r, 1, true);
+  if (rc != FEC_OK) return rc;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return FEC_ERR_NODEV;
+  DecodePlan* plan = nullptr;
+  rc = get_decode_plan(ctx, k, r, &plan);
+  if (rc != FEC_OK) return rc;
+  if (bytes_out) *bytes_out = plan->layout.total_bytes;
+  return FEC_OK;
+}
+
+QFEC_EXPORT int fec_fill_random_dev(FECEncoderCtx* ctx, uint8_t* d_dst, uint64_t nbytes, uint64_t seed,
+                                    uint64_t byte_offset, void* stream) {
+  if (!ctx || !d_dst) return FEC_ERR_NULL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return FEC_ERR_NODEV;
+  QFEC_HIP(qfec::launch_fill_splitmix(d_dst, nbytes, seed, byte_offset, pick_stream(ctx, stream)));
+  return FEC_OK;
+}
+
+QFEC_EXPORT int fec_synchronize(FECEncoderCtx* ctx) {
+  if (!ctx) return FEC_ERR_NULL;
+  DeviceGuard dg(ctx->device);
+  QFEC_HIP(hipStreamSynchronize(ctx->stream));
+  return FEC_OK;
+}

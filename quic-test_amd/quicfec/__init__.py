@@ -1,0 +1,246 @@
+"""quicfec — Python binding of libfec_hip.so (the MI355X FEC engine) over its C-ABI.
+
+This is the host-side mirror the tests and ``bench.py`` drive.  It binds exactly the
+symbols declared in ``include/fec_xor_simd.h`` (the reference cgo surface,
+internal/fec/fec_xor_simd.h:22-137) and ``include/fec_hip.h`` (batch GF(2^8) API).
+
+There is no fallback: if ``libfec_hip.so`` is missing, :func:`load_library` raises, and
+if no GPU is usable, :class:`Context` raises :class:`FecError` (the C library returns
+NULL from ``fec_encoder_new``, which is what lets the Go hybrid encoder fall back to Go,
+encoder_hybrid.go:44-52).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+from typing import Optional
+
+import numpy as np
+
+PKG_ROOT = Path(__file__).resolve().parent.parent          # quic-test_amd/
+REPO_ROOT = PKG_ROOT.parent
+LIB_PATH = PKG_ROOT / "lib" / "libfec_hip.so"
+INCLUDE_DIR = REPO_ROOT / "include"
+
+FEC_OK = 0
+FEC_ERR_NULL = -1
+FEC_ERR_HIP = -2
+FEC_ERR_RANGE = -3
+FEC_ERR_NODEV = -4
+FEC_ERR_NOMEM = -5
+
+# Every function the headers declare (tests check the library exports all of them).
+REFERENCE_SYMBOLS = (
+    "fec_encoder_new", "fec_alloc_slab", "fec_alloc_slab_numa", "fec_alloc_repair_buffer",
+    "fec_free_repair_buffer", "fec_encode_batch", "fec_encoder_free", "fec_free_slab",
+    "fec_select_xor_impl", "xor_packets_scalar", "xor_packets_avx2", "xor_packets_avx512",
+    "xor_packets_neon",
+)
+HIP_SYMBOLS = (
+    "fec_hip_device_count", "fec_hip_last_error", "fec_encoder_new_device", "fec_encoder_device",
+    "fec_hip_version", "fec_parity_matrix", "fec_encode_batch_rs", "fec_decode_batch_rs",
+    "fec_encode_batch_rs_dev", "fec_decode_batch_rs_dev", "fec_decode_prepare",
+    "fec_fill_random_dev", "fec_synchronize",
+)
+
+
+class FecError(RuntimeError):
+    def __init__(self, what: str, code: int, detail: str = ""):
+        super().__init__(f"{what} failed with code {code}" + (f": {detail}" if detail else ""))
+        self.code = code
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+_u32, _u64, _int, _dbl, _sz = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_size_t
+XOR_IMPL_FN = ctypes.CFUNCTYPE(None, ctypes.POINTER(_vp), _sz, _sz, _vp)
+
+
+def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
+    """Load libfec_hip.so (built by ``__graft_entry__.build()``); raise if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else Path(os.environ.get("QUICFEC_LIB", LIB_PATH))
+    if not p.exists():
+        raise FileNotFoundError(
+            f"libfec_hip.so not found at {p}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(str(p))
+    sig = {
+        "fec_encoder_new": (_vp, [_dbl, _u32]),
+        "fec_encoder_new_device": (_vp, [_dbl, _u32, _int]),
+        "fec_encoder_free": (None, [_vp]),
+        "fec_encoder_device": (_int, [_vp]),
+        "fec_alloc_slab": (_vp, [_sz]),
+        "fec_alloc_slab_numa": (_vp, [_sz, _int]),
+        "fec_alloc_repair_buffer": (_vp, [_sz]),
+        "fec_free_slab": (None, [_vp]),
+        "fec_free_repair_buffer": (None, [_vp]),
+        "fec_encode_batch": (_int, [_vp, _vp, _vp, _u32, _u32, _vp]),
+        "fec_select_xor_impl": (_vp, []),
+        "xor_packets_scalar": (None, [ctypes.POINTER(_vp), _sz, _sz, _vp]),
+        "xor_packets_avx2": (None, [ctypes.POINTER(_vp), _sz, _sz, _vp]),
+        "xor_packets_avx512": (None, [ctypes.POINTER(_vp), _sz, _sz, _vp]),
+        "xor_packets_neon": (None, [ctypes.POINTER(_vp), _sz, _sz, _vp]),
+        "fec_hip_device_count": (_int, []),
+        "fec_hip_last_error": (ctypes.c_char_p, []),
+        "fec_hip_version": (ctypes.c_char_p, []),
+        "fec_parity_matrix": (_int, [_u32, _u32, _vp]),
+        "fec_encode_batch_rs": (_int, [_vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp]),
+        "fec_decode_batch_rs": (_int, [_vp, _vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp]),
+        "fec_encode_batch_rs_dev": (_int, [_vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp]),
+        "fec_decode_batch_rs_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp]),
+        "fec_decode_prepare": (_int, [_vp, _u32, _u32, ctypes.POINTER(_u64)]),
+        "fec_fill_random_dev": (_int, [_vp, _vp, _u64, _u64, _u64, _vp]),
+        "fec_synchronize": (_int, [_vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return (load_library().fec_hip_last_error() or b"").decode(errors="replace")
+
+
+def device_count() -> int:
+    return int(load_library().fec_hip_device_count())
+
+
+def parity_matrix(k: int, r: int) -> np.ndarray:
+    out = np.zeros((r, k), dtype=np.uint8)
+    rc = load_library().fec_parity_matrix(k, r, out.ctypes.data)
+    if rc != FEC_OK:
+        raise FecError("fec_parity_matrix", rc)
+    return out
+
+
+def _ptr(a) -> int:
+    """Address of a numpy array or torch tensor (device or host)."""
+    if isinstance(a, np.ndarray):
+        if not a.flags["C_CONTIGUOUS"]:
+            raise ValueError("array must be C-contiguous")
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        if hasattr(a, "is_contiguous") and not a.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return a.data_ptr()
+    if isinstance(a, int):
+        return a
+    raise TypeError(f"unsupported buffer type {type(a)!r}")
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != FEC_OK:
+        raise FecError(what, rc, last_error())
+
+
+class Context:
+    """An FECEncoderCtx (one per stream of work / per GPU)."""
+
+    def __init__(self, device: Optional[int] = None, redundancy: float = 0.10, max_groups: int = 1024):
+        self.lib = load_library()
+        if device is None:
+            h = self.lib.fec_encoder_new(redundancy, max_groups)
+        else:
+            h = self.lib.fec_encoder_new_device(redundancy, max_groups, device)
+        if not h:
+            raise FecError("fec_encoder_new", FEC_ERR_NODEV, last_error())
+        self.handle = h
+
+    @property
+    def device(self) -> int:
+        return int(self.lib.fec_encoder_device(self.handle))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self.lib.fec_encoder_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- reference ABI ----
+    def encode_batch_legacy(self, slab, offsets, num_groups: int, packet_size: int, repair_out) -> int:
+        """fec_encode_batch (k fixed to 10).  Returns the C return code."""
+        return int(self.lib.fec_encode_batch(self.handle, _ptr(slab) if slab is not None else None,
+                                             _ptr(offsets) if offsets is not None else None,
+                                             num_groups, packet_size,
+                                             _ptr(repair_out) if repair_out is not None else None))
+
+    # ---- batch GF(2^8) API, host or device buffers ----
+    def encode(self, data, k: int, r: int, packet_size: int, parity_out, num_groups: Optional[int] = None,
+               offsets=None) -> None:
+        G = num_groups if num_groups is not None else _nbytes(data) // (k * packet_size)
+        rc = self.lib.fec_encode_batch_rs(self.handle, _ptr(data), _ptr(offsets) if offsets is not None else None,
+                                          G, k, r, packet_size, _ptr(parity_out))
+        _check(rc, "fec_encode_batch_rs")
+
+    def decode(self, data, parity, masks, k: int, r: int, packet_size: int, status_out=None,
+               num_groups: Optional[int] = None) -> int:
+        G = num_groups if num_groups is not None else _nbytes(masks) // 8
+        bad = ctypes.c_uint64(0)
+        rc = self.lib.fec_decode_batch_rs(self.handle, _ptr(data), _ptr(parity), _ptr(masks), G, k, r,
+                                          packet_size, _ptr(status_out) if status_out is not None else None,
+                                          ctypes.byref(bad))
+        _check(rc, "fec_decode_batch_rs")
+        return int(bad.value)
+
+    # ---- device-resident API ----
+    def encode_dev(self, d_data, num_groups: int, k: int, r: int, packet_size: int, d_parity,
+                   stream: Optional[int] = None) -> None:
+        rc = self.lib.fec_encode_batch_rs_dev(self.handle, _ptr(d_data), num_groups, k, r, packet_size,
+                                              _ptr(d_parity), stream)
+        _check(rc, "fec_encode_batch_rs_dev")
+
+    def decode_dev(self, d_data, d_parity, d_masks, num_groups: int, k: int, r: int, packet_size: int,
+                   d_status=None, stream: Optional[int] = None) -> None:
+        rc = self.lib.fec_decode_batch_rs_dev(self.handle, _ptr(d_data), _ptr(d_parity), _ptr(d_masks),
+                                              num_groups, k, r, packet_size,
+                                              _ptr(d_status) if d_status is not None else None, stream)
+        _check(rc, "fec_decode_batch_rs_dev")
+
+    def decode_prepare(self, k: int, r: int) -> int:
+        n = ctypes.c_uint64(0)
+        _check(self.lib.fec_decode_prepare(self.handle, k, r, ctypes.byref(n)), "fec_decode_prepare")
+        return int(n.value)
+
+    def fill_random_dev(self, d_dst, nbytes: int, seed: int, byte_offset: int = 0,
+                        stream: Optional[int] = None) -> None:
+        _check(self.lib.fec_fill_random_dev(self.handle, _ptr(d_dst), nbytes, seed, byte_offset, stream),
+               "fec_fill_random_dev")
+
+    def synchronize(self) -> None:
+        _check(self.lib.fec_synchronize(self.handle), "fec_synchronize")
+
+
+def _nbytes(a) -> int:
+    if isinstance(a, np.ndarray):
+        return a.nbytes
+    if hasattr(a, "numel"):
+        return a.numel() * a.element_size()
+    raise TypeError("pass num_groups explicitly for raw pointers")
+
+
+def xor_packets(packets, packet_size: int, repair, variant: str = "avx2") -> None:
+    """Call one of the ABI-compat xor_packets_* entry points (GPU-backed)."""
+    lib = load_library()
+    arr = (_vp * max(1, len(packets)))(*[_ptr(p) for p in packets])
+    getattr(lib, f"xor_packets_{variant}")(arr, len(packets), packet_size, _ptr(repair))

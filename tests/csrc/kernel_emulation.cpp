@@ -1,0 +1,169 @@
+// kernel_emulation.cpp — CPU check of the GPU library's table arithmetic (tests only).
+//
+// Re-executes, on the CPU, exactly the per-dword arithmetic of fec_kernels.hip
+// (v_perm_b32 table lookups, the classify ranking, codebook-driven rebuild) using the
+// product's own host code (quic-test_amd/csrc/gf256.hpp), and compares the bytes with the
+// oracle restatement (oracle/liboracle.so).  Lets the CPU suite catch table / ranking /
+// codebook-layout bugs before a GPU run.  Prints "OK <cases>" or the first mismatch.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "gf256.hpp"
+
+extern "C" {
+int oracle_rs_encode(const uint8_t*, uint64_t, uint32_t, uint32_t, uint32_t, uint8_t*, int);
+int64_t oracle_rs_decode(uint8_t*, const uint8_t*, const uint64_t*, uint64_t, uint32_t, uint32_t, uint32_t,
+                         uint8_t*, int);
+void oracle_fill_splitmix(uint8_t*, uint64_t, uint64_t, uint64_t);
+}
+
+using qfec::CoefEntry;
+
+// v_perm_b32 (CDNA4 ISA): byte b of the result = byte sel_b of {S0:S1} for sel_b < 8.
+static uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+  const uint64_t d = (uint64_t(s0) << 32) | s1;
+  uint32_t out = 0;
+  for (int b = 0; b < 4; ++b) {
+    const uint32_t s = (sel >> (8 * b)) & 0xFF;
+    uint32_t v;
+    if (s < 8) v = (d >> (8 * s)) & 0xFF;
+    else if (s == 12) v = 0;
+    else if (s >= 13) v = 0xFF;
+    else v = ((d >> (16 * (s - 8) + 15)) & 1) ? 0xFF : 0;
+    out |= v << (8 * b);
+  }
+  return out;
+}
+
+static uint32_t gmul(uint32_t w, const CoefEntry& t) {
+  const uint32_t s0 = w & 0x07070707u, s1 = (w >> 3) & 0x07070707u, s2 = (w >> 6) & 0x03030303u;
+  return perm(t.t0hi, t.t0lo, s0) ^ perm(t.t1hi, t.t1lo, s1) ^ perm(t.t2, t.t2, s2);
+}
+
+static uint32_t ld32(const uint8_t* p) {
+  uint32_t v;
+  std::memcpy(&v, p, 4);
+  return v;
+}
+static void st32(uint8_t* p, uint32_t v) { std::memcpy(p, &v, 4); }
+
+static int fail(const char* what, int a, int b, int c) {
+  std::printf("MISMATCH %s (%d,%d,%d)\n", what, a, b, c);
+  return 1;
+}
+
+int main() {
+  std::mt19937_64 rng(12345);
+  int cases = 0;
+  // every product of the multiply tables against the field definition
+  for (int c = 0; c < 256; ++c) {
+    const CoefEntry e = qfec::make_entry(uint8_t(c));
+    for (int x = 0; x < 256; ++x) {
+      const uint32_t w = uint32_t(x) * 0x01010101u;
+      if (gmul(w, e) != uint32_t(qfec::gf().mul(uint8_t(c), uint8_t(x))) * 0x01010101u) return fail("gmul", c, x, 0);
+    }
+  }
+  const uint32_t shapes[][3] = {{4, 2, 256}, {10, 3, 1200}, {10, 1, 64}, {20, 5, 96}, {7, 4, 32}, {3, 8, 16}, {1, 1, 8}, {16, 16, 16}, {32, 8, 8}};
+  for (const auto& sh : shapes) {
+    const uint32_t k = sh[0], r = sh[1], P = sh[2];
+    const uint64_t G = 40;
+    std::vector<uint8_t> data(G * k * P), par(G * r * P), ref_par(G * r * P);
+    oracle_fill_splitmix(data.data(), data.size(), 0x1000 + k * 64 + r, 0);
+    std::vector<uint8_t> M;
+    qfec::parity_matrix(k, r, M);
+    std::vector<CoefEntry> tabs;
+    for (uint32_t i = 1; i < r; ++i)
+      for (uint32_t j = 0; j < k; ++j) tabs.push_back(qfec::make_entry(M[i * k + j]));
+    // encode_v16 arithmetic (row 0 and column 0 XOR, the rest table lookups)
+    for (uint64_t g = 0; g < G; ++g)
+      for (uint32_t b = 0; b < P; b += 4)
+        for (uint32_t i = 0; i < r; ++i) {
+          uint32_t acc = ld32(&data[(g * k + 0) * P + b]);
+          for (uint32_t j = 1; j < k; ++j) {
+            const uint32_t x = ld32(&data[(g * k + j) * P + b]);
+            acc ^= (i == 0) ? x : gmul(x, tabs[(i - 1) * k + j]);
+          }
+          st32(&par[(g * r + i) * P + b], acc);
+        }
+    oracle_rs_encode(data.data(), G, k, r, P, ref_par.data(), 1);
+    if (par != ref_par) return fail("encode", k, r, P);
+    ++cases;
+    if (k + r > 64) continue;
+    // decode: classify ranking + codebook records
+    qfec::CodebookLayout L;
+    if (!qfec::codebook_layout(k, r, 2ull << 30, L)) {
+      // dense codebook over the cap (e.g. 16+16, 32+8): not supported by this path
+      if (k + r <= 25) return fail("layout", k, r, P);
+      continue;
+    }
+    std::vector<uint8_t> book;
+    if (!qfec::build_codebook(L, M, book)) return fail("codebook", k, r, P);
+    for (int trial = 0; trial < 6; ++trial) {
+      std::vector<uint64_t> masks(G);
+      for (uint64_t g = 0; g < G; ++g) {
+        uint64_t m = 0;
+        const uint32_t ne = uint32_t(rng() % (r + 2));
+        for (uint32_t t = 0; t < ne; ++t) m |= 1ull << (rng() % (k + r));
+        masks[g] = m;
+      }
+      std::vector<uint8_t> mine = data, ref = data;
+      for (uint64_t g = 0; g < G; ++g)
+        for (uint32_t j = 0; j < k; ++j)
+          if ((masks[g] >> j) & 1) {
+            std::memset(&mine[(g * k + j) * P], 0xEE, P);
+            std::memset(&ref[(g * k + j) * P], 0xEE, P);
+          }
+      std::vector<uint8_t> st(G);
+      const int64_t bad_ref = oracle_rs_decode(ref.data(), ref_par.data(), masks.data(), G, k, r, P, st.data(), 1);
+      int64_t bad = 0;
+      for (uint64_t g = 0; g < G; ++g) {
+        // classify (fec_kernels.hip)
+        const uint64_t kmask = (1ull << k) - 1, rmask = (r >= 64) ? ~0ull : ((1ull << r) - 1);
+        uint64_t dm = masks[g] & kmask;
+        const uint64_t pm = (masks[g] >> k) & rmask;
+        const uint32_t e = __builtin_popcountll(dm);
+        if (e == 0) continue;
+        if (e > r - __builtin_popcountll(pm)) {
+          ++bad;
+          if (st[g] != 1) return fail("status", k, r, int(g));
+          continue;
+        }
+        uint64_t rank_e = 0, rank_r = 0;
+        for (uint32_t t = 0; dm; ++t) {
+          rank_e += qfec::binom().c[__builtin_ctzll(dm)][t + 1];
+          dm &= dm - 1;
+        }
+        uint64_t sp = ~pm & rmask;
+        for (uint32_t t = 0; t < e; ++t) {
+          rank_r += qfec::binom().c[__builtin_ctzll(sp)][t + 1];
+          sp &= sp - 1;
+        }
+        const uint64_t off = L.level_base[e] + (rank_e * qfec::binom().c[r][e] + rank_r) * L.level_stride[e];
+        if (off % 32) return fail("align", k, r, int(g));
+        const uint8_t* rec = &book[off];
+        if (rec[96] != e) return fail("record-e", k, r, int(g));
+        const CoefEntry* T = reinterpret_cast<const CoefEntry*>(rec + qfec::kRecordHeader);
+        for (uint32_t b = 0; b < P; b += 4)
+          for (uint32_t m = 0; m < e; ++m) {
+            uint32_t acc = 0;
+            for (uint32_t s = 0; s < k; ++s) {
+              const uint32_t sid = rec[s];
+              const uint32_t x = sid < k ? ld32(&data[(g * k + sid) * P + b]) : ld32(&ref_par[(g * r + sid - k) * P + b]);
+              if ((sid < k) && ((masks[g] >> sid) & 1)) return fail("survivor-erased", k, r, int(g));
+              const CoefEntry& t = T[m * k + s];
+              acc ^= (t.coef == 1) ? x : (t.coef == 0 ? 0 : gmul(x, t));
+            }
+            st32(&mine[(g * k + rec[64 + m]) * P + b], acc);
+          }
+      }
+      if (bad != bad_ref) return fail("bad-count", k, r, int(bad));
+      if (mine != ref) return fail("decode", k, r, trial);
+      ++cases;
+    }
+  }
+  std::printf("OK %d\n", cases);
+  return 0;
+}

@@ -1,0 +1,101 @@
+"""CPU-side checks of the product library (no GPU compute calls).
+
+- libfec_hip.so loads and exports every function include/*.h declares;
+- behaviour that needs no device (NULL handling, no-GPU context creation, the code's
+  parity matrix) matches the reference contract (fec_xor_simd.cpp:538-594);
+- the kernels' table arithmetic, classify ranking and decode codebook, re-executed on the
+  CPU from the product's own host code, match the oracle byte for byte.
+"""
+import json
+import re
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _declared_functions():
+    names = set()
+    for h in (REPO / "include").glob("*.h"):
+        text = h.read_text()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(\w+)\s*\(", text, flags=re.M):
+            name = m.group(1)
+            if name not in ("typedef",) and not text[m.start():m.end()].startswith("typedef"):
+                names.add(name)
+    return names
+
+
+def test_headers_declare_reference_surface():
+    names = _declared_functions()
+    # the eleven reference functions (internal/fec/fec_xor_simd.h:22-137, 4 ISA variants)
+    ref = {"fec_encoder_new", "fec_alloc_slab", "fec_alloc_slab_numa", "fec_alloc_repair_buffer",
+           "fec_free_repair_buffer", "fec_encode_batch", "fec_encoder_free", "fec_free_slab",
+           "fec_select_xor_impl", "xor_packets_scalar", "xor_packets_avx2", "xor_packets_avx512",
+           "xor_packets_neon"}
+    assert ref <= names
+
+
+def test_library_exports_every_declared_symbol(quicfec_mod):
+    lib_path = quicfec_mod.LIB_PATH
+    out = subprocess.run(["nm", "-D", "--defined-only", str(lib_path)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    missing = _declared_functions() - exported
+    assert not missing, missing
+    assert set(quicfec_mod.REFERENCE_SYMBOLS) | set(quicfec_mod.HIP_SYMBOLS) <= exported
+
+
+def test_library_is_gfx950_code_object(quicfec_mod):
+    blob = quicfec_mod.LIB_PATH.read_bytes()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_null_arguments_need_no_gpu(quicfec_mod):
+    lib = quicfec_mod.load_library()
+    buf = np.zeros(16, dtype=np.uint8)
+    off = np.zeros(10, dtype=np.uint32)
+    # fec_xor_simd.cpp:564-566: NULL ctx/slab/offsets/repair -> -1 (checked before anything else)
+    assert lib.fec_encode_batch(None, buf.ctypes.data, off.ctypes.data, 1, 8, buf.ctypes.data) == -1
+    assert lib.fec_encode_batch(None, None, None, 0, 0, None) == -1
+    assert lib.fec_encode_batch_rs(None, None, None, 0, 1, 1, 1, None) == quicfec_mod.FEC_ERR_NULL
+    assert lib.fec_decode_batch_rs(None, None, None, None, 0, 1, 1, 1, None, None) == quicfec_mod.FEC_ERR_NULL
+    lib.fec_encoder_free(None)
+    lib.fec_free_slab(None)
+    lib.fec_free_repair_buffer(None)
+    assert lib.fec_encoder_device(None) == -1
+
+
+def test_no_gpu_context_is_null_not_abort(quicfec_mod):
+    if quicfec_mod.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    lib = quicfec_mod.load_library()
+    assert not lib.fec_encoder_new(0.1, 1024)
+    assert "no HIP device" in quicfec_mod.last_error()
+    with pytest.raises(quicfec_mod.FecError):
+        quicfec_mod.Context()
+
+
+def test_parity_matrix_matches_oracle_and_fixture(quicfec_mod, oracle_mod, golden_dir):
+    mats = json.loads((golden_dir / "parity_matrices.json").read_text())
+    for key, M in mats.items():
+        k, r = map(int, key.split(","))
+        assert np.array_equal(quicfec_mod.parity_matrix(k, r), np.array(M, dtype=np.uint8))
+    for k, r in ((1, 255), (128, 128), (200, 56)):
+        assert np.array_equal(quicfec_mod.parity_matrix(k, r), oracle_mod.parity_matrix(k, r))
+    with pytest.raises(quicfec_mod.FecError):
+        quicfec_mod.parity_matrix(200, 57)
+    with pytest.raises(quicfec_mod.FecError):
+        quicfec_mod.parity_matrix(0, 3)
+
+
+def test_kernel_arithmetic_emulation(tmp_path, oracle_mod):
+    exe = tmp_path / "kernel_emulation"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", str(REPO / "quic-test_amd" / "csrc"),
+                    str(REPO / "tests" / "csrc" / "kernel_emulation.cpp"), str(oracle_mod.ORACLE_LIB),
+                    f"-Wl,-rpath,{oracle_mod.ORACLE_DIR}", "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.startswith("OK"), out.stdout + out.stderr

@@ -1,0 +1,306 @@
+"""GPU parity tests: libfec_hip.so (through its C-ABI) against the oracle and the
+reference-generated golden fixtures.  Bit-exact everywhere (byte arithmetic).
+
+Small cases compare every byte with the oracle; BASELINE.json's full sizes (1M groups,
+k=10 r=3 / k=20 r=5, 1200 B) are checked through sampled groups against the oracle and
+the size-independent encode -> erase -> decode round trip.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED0000
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _dev(torch, arr):
+    return torch.from_numpy(np.ascontiguousarray(arr)).cuda()
+
+
+# ---------------- reference ABI: fec_encode_batch, xor_packets_* ----------------
+
+def test_legacy_batch_golden_host_pinned_device(gpu_ctx, quicfec_mod, oracle_mod, xor_golden, manifest, torch_cuda):
+    c = next(c for c in manifest["cases"] if c["name"] == "batch_k10_p1200_g64")
+    G, P = c["G"], c["P"]
+    slab = oracle_mod.splitmix_bytes(G * 10 * P, c["seed"])
+    offs = (np.arange(G * 10, dtype=np.uint32) * P).astype(np.uint32)
+    exp = xor_golden["batch_k10_p1200_g64"]
+    # pageable host memory
+    rep = np.zeros(G * P, dtype=np.uint8)
+    assert gpu_ctx.encode_batch_legacy(slab, offs, G, P, rep) == 0
+    assert np.array_equal(rep, exp)
+    # pinned slab + repair from fec_alloc_slab / fec_alloc_repair_buffer (the Go wrapper's path)
+    lib = quicfec_mod.load_library()
+    ps = lib.fec_alloc_slab(slab.nbytes)
+    pr = lib.fec_alloc_repair_buffer(rep.nbytes)
+    assert ps and pr and ps % 64 == 0
+    import ctypes
+    ctypes.memmove(ps, slab.ctypes.data, slab.nbytes)
+    assert lib.fec_encode_batch(gpu_ctx.handle, ps, offs.ctypes.data, G, P, pr) == 0
+    got = np.ctypeslib.as_array((ctypes.c_uint8 * rep.nbytes).from_address(pr)).copy()
+    lib.fec_free_slab(ps)
+    lib.fec_free_repair_buffer(pr)
+    assert np.array_equal(got, exp)
+    # device pointers
+    ds, do, dr = _dev(torch_cuda, slab), _dev(torch_cuda, offs.view(np.int32)), torch_cuda.zeros(G * P, dtype=torch_cuda.uint8, device="cuda")
+    assert gpu_ctx.encode_batch_legacy(ds, do, G, P, dr) == 0
+    assert np.array_equal(dr.cpu().numpy(), exp)
+
+
+def test_legacy_batch_scattered_unaligned(gpu_ctx, oracle_mod, xor_golden, manifest):
+    c = next(c for c in manifest["cases"] if c["name"] == "batch_scattered_p100_g16")
+    slab = oracle_mod.splitmix_bytes(c["slab_bytes"], c["seed"])
+    offs = xor_golden["batch_scattered_p100_g16_offsets"]
+    rep = np.zeros(c["G"] * c["P"], dtype=np.uint8)
+    assert gpu_ctx.encode_batch_legacy(slab, offs, c["G"], c["P"], rep) == 0
+    assert np.array_equal(rep, xor_golden["batch_scattered_p100_g16"])
+
+
+def test_legacy_return_codes(gpu_ctx, manifest):
+    codes = manifest["legacy_return_codes"]
+    buf = np.zeros(64, dtype=np.uint8)
+    off = np.zeros(10, dtype=np.uint32)
+    rep = np.full(8, 0xAB, dtype=np.uint8)
+    assert gpu_ctx.encode_batch_legacy(None, off, 1, 8, rep) == codes["null_slab"]
+    assert gpu_ctx.encode_batch_legacy(buf, None, 1, 8, rep) == codes["null_offsets"]
+    assert gpu_ctx.encode_batch_legacy(buf, off, 1, 8, None) == codes["null_repair"]
+    assert gpu_ctx.encode_batch_legacy(buf, off, 0, 8, rep) == codes["zero_groups"]
+    assert gpu_ctx.encode_batch_legacy(buf, off, 1, 0, rep) == codes["zero_size"]
+    assert (rep == 0xAB).all()
+
+
+@pytest.mark.parametrize("variant", ["avx2", "scalar", "avx512", "neon"])
+def test_xor_packets_entry_points_golden(quicfec_mod, oracle_mod, xor_golden, manifest, variant):
+    n = 0
+    for c in manifest["cases"]:
+        if c["api"] != "xor_packets_avx2" or "G" not in c:
+            continue
+        data = oracle_mod.splitmix_bytes(c["G"] * c["k"] * c["P"], c["seed"])
+        got = []
+        for g in range(c["G"]):
+            pk = [data[(g * c["k"] + j) * c["P"]:(g * c["k"] + j + 1) * c["P"]] for j in range(c["k"])]
+            out = np.zeros(c["P"], dtype=np.uint8)
+            quicfec_mod.xor_packets(pk, c["P"], out, variant=variant)
+            got.append(out)
+        assert np.array_equal(np.concatenate(got), xor_golden[c["name"]]), (variant, c["name"])
+        n += 1
+    assert n >= 12
+    pk = [np.full(1200, i, dtype=np.uint8) for i in range(10)]
+    out = np.zeros(1200, dtype=np.uint8)
+    quicfec_mod.xor_packets(pk, 1200, out, variant=variant)
+    assert np.array_equal(out, xor_golden["kat_encoder_test"])
+    pre = np.full(16, 0x5A, dtype=np.uint8)
+    quicfec_mod.xor_packets([], 16, pre, variant=variant)
+    assert (pre == 0x5A).all()
+
+
+def test_select_xor_impl_is_callable(quicfec_mod, oracle_mod):
+    lib = quicfec_mod.load_library()
+    fn = quicfec_mod.XOR_IMPL_FN(lib.fec_select_xor_impl())
+    pk = [oracle_mod.splitmix_bytes(300, s) for s in range(5)]
+    import ctypes
+    arr = (ctypes.c_void_p * 5)(*[p.ctypes.data for p in pk])
+    out = np.zeros(300, dtype=np.uint8)
+    fn(arr, 5, 300, out.ctypes.data)
+    assert np.array_equal(out, oracle_mod.xor_packets(pk, 300))
+
+
+# ---------------- batch GF(2^8) API ----------------
+
+SHAPES = [(4, 2, 256), (10, 3, 1200), (20, 5, 1200), (10, 1, 1200), (7, 4, 48), (12, 9, 64),
+          (3, 1, 16), (10, 3, 100), (5, 3, 33), (1, 1, 7), (30, 20, 32)]
+
+
+@pytest.mark.parametrize("k,r,P", SHAPES)
+def test_rs_encode_matches_oracle(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
+    G = 97
+    data = oracle_mod.splitmix_bytes(G * k * P, SEED + k * 1000 + r * 10 + P)
+    exp = oracle_mod.rs_encode(data, G, k, r, P)
+    par = np.zeros(G * r * P, dtype=np.uint8)
+    gpu_ctx.encode(data, k, r, P, par, num_groups=G)
+    assert np.array_equal(par, exp)
+    dd = _dev(torch_cuda, data)
+    dp = torch_cuda.zeros(G * r * P, dtype=torch_cuda.uint8, device="cuda")
+    gpu_ctx.encode_dev(dd, G, k, r, P, dp)
+    gpu_ctx.synchronize()
+    assert np.array_equal(dp.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("aligned", [True, False])
+def test_rs_encode_gather_offsets(gpu_ctx, oracle_mod, aligned):
+    k, r, P, G = 10, 3, 1200 if aligned else 1201, 23
+    rng = np.random.default_rng(7)
+    slab = oracle_mod.splitmix_bytes(G * k * P * 2 + 64, 99)
+    slots = rng.permutation(G * k * 2)[:G * k]
+    offs = (slots.astype(np.uint64) * P).astype(np.uint64)
+    contig = np.concatenate([slab[int(o):int(o) + P] for o in offs])
+    exp = oracle_mod.rs_encode(contig, G, k, r, P)
+    par = np.zeros(G * r * P, dtype=np.uint8)
+    gpu_ctx.encode(slab, k, r, P, par, num_groups=G, offsets=offs)
+    assert np.array_equal(par, exp)
+
+
+def _random_masks(rng, G, k, r, max_lost):
+    masks = np.zeros(G, dtype=np.uint64)
+    for g in range(G):
+        ne = int(rng.integers(0, max_lost + 1))
+        pos = rng.choice(k + r, size=min(ne, k + r), replace=False)
+        masks[g] = np.uint64(sum(1 << int(p) for p in pos))
+    return masks
+
+
+def _poison(data, masks, G, k, P):
+    d = data.copy().reshape(G, k, P)
+    for g in range(G):
+        for j in range(k):
+            if (int(masks[g]) >> j) & 1:
+                d[g, j, :] = 0xEE
+    return d.reshape(-1)
+
+
+@pytest.mark.parametrize("k,r,P", [s for s in SHAPES if s[0] + s[1] <= 25])
+def test_rs_decode_matches_oracle(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
+    G = 211
+    rng = np.random.default_rng(k * 131 + r * 7 + P)
+    data = oracle_mod.splitmix_bytes(G * k * P, SEED + 77 + k + r + P)
+    par = oracle_mod.rs_encode(data, G, k, r, P)
+    masks = _random_masks(rng, G, k, r, r + 1)
+    broken = _poison(data, masks, G, k, P)
+    exp = broken.copy()
+    bad_exp, st_exp = oracle_mod.rs_decode(exp, par, masks, G, k, r, P)
+    got = broken.copy()
+    st = np.zeros(G, dtype=np.uint8)
+    bad = gpu_ctx.decode(got, par, masks, k, r, P, status_out=st)
+    assert bad == bad_exp
+    assert np.array_equal(st, st_exp)
+    assert np.array_equal(got, exp)
+    # device-resident API
+    dd, dpar, dm = _dev(torch_cuda, broken), _dev(torch_cuda, par), _dev(torch_cuda, masks.view(np.int64))
+    dst = torch_cuda.zeros(G, dtype=torch_cuda.uint8, device="cuda")
+    gpu_ctx.decode_dev(dd, dpar, dm, G, k, r, P, dst)
+    gpu_ctx.synchronize()
+    assert np.array_equal(dd.cpu().numpy(), exp)
+    assert np.array_equal(dst.cpu().numpy(), st_exp)
+
+
+def test_gf_golden_fixtures(gpu_ctx, oracle_mod, manifest, gf_golden):
+    for c in manifest["cases"]:
+        if not c["name"].startswith("rs_"):
+            continue
+        G, k, r, P = c["G"], c["k"], c["r"], c["P"]
+        data = oracle_mod.splitmix_bytes(G * k * P, c["seed"])
+        par = np.zeros(G * r * P, dtype=np.uint8)
+        gpu_ctx.encode(data, k, r, P, par, num_groups=G)
+        assert np.array_equal(par, gf_golden[c["name"] + "_parity"]), c["name"]
+        masks = gf_golden[c["name"] + "_masks"]
+        broken = _poison(data, masks, G, k, P)
+        st = np.zeros(G, dtype=np.uint8)
+        bad = gpu_ctx.decode(broken, par, masks, k, r, P, status_out=st)
+        assert bad == c["unrecoverable"]
+        assert np.array_equal(broken, gf_golden[c["name"] + "_decoded"]), c["name"]
+
+
+def test_single_loss_is_reference_xor_recovery(gpu_ctx, oracle_mod):
+    """1 lost data shard + parity row 0 alive == FECDecoder.recoverSingle (decoder.go:255-287)."""
+    k, r, P, G = 10, 3, 1200, 50
+    data = oracle_mod.splitmix_bytes(G * k * P, 4242)
+    par = oracle_mod.rs_encode(data, G, k, r, P)
+    rng = np.random.default_rng(3)
+    lost = rng.integers(0, k, size=G)
+    masks = np.array([1 << int(j) for j in lost], dtype=np.uint64)
+    got = _poison(data, masks, G, k, P)
+    assert gpu_ctx.decode(got, par, masks, k, r, P) == 0
+    for g in range(G):
+        pk = [None if j == lost[g] else data[(g * k + j) * P:(g * k + j + 1) * P] for j in range(k)]
+        mid, rec = oracle_mod.go_recover_single(pk, par[g * r * P:g * r * P + P], P)
+        assert mid == lost[g]
+        assert np.array_equal(got[(g * k + mid) * P:(g * k + mid + 1) * P], rec)
+
+
+def test_fill_random_matches_oracle(gpu_ctx, oracle_mod, torch_cuda):
+    for n, off in ((4096, 0), (1000, 8), (777, 3)):
+        d = torch_cuda.zeros(n + 16, dtype=torch_cuda.uint8, device="cuda")
+        gpu_ctx.fill_random_dev(d, n, 0x1234, off)
+        gpu_ctx.synchronize()
+        assert np.array_equal(d.cpu().numpy()[:n], oracle_mod.splitmix_bytes(n, 0x1234, off))
+
+
+def test_decode_prepare_sizes(gpu_ctx):
+    assert gpu_ctx.decode_prepare(10, 3) > 0
+    assert gpu_ctx.decode_prepare(20, 5) > 0
+    import quicfec
+    with pytest.raises(quicfec.FecError):
+        gpu_ctx.decode_prepare(40, 30)
+
+
+# ---------------- BASELINE.json full sizes (size-independent properties) ----------------
+
+def _sample_check(torch, gpu_ctx, oracle_mod, d_data, d_par, G, k, r, P, n=48, seed=1):
+    rng = np.random.default_rng(seed)
+    gs = np.unique(np.concatenate([[0, G - 1], rng.integers(0, G, size=n)]))
+    for g in gs:
+        g = int(g)
+        blk = d_data[g * k * P:(g + 1) * k * P].cpu().numpy()
+        exp = oracle_mod.rs_encode(blk, 1, k, r, P)
+        assert np.array_equal(d_par[g * r * P:(g + 1) * r * P].cpu().numpy(), exp), g
+
+
+@pytest.mark.slow
+def test_full_size_c2_c3_round_trip(gpu_ctx, oracle_mod, torch_cuda):
+    torch = torch_cuda
+    k, r, P, G = 10, 3, 1200, 1_000_000
+    data = torch.empty(G * k * P, dtype=torch.uint8, device="cuda")
+    par = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_random_dev(data, data.numel(), SEED + 2)
+    gpu_ctx.encode_dev(data, G, k, r, P, par)
+    gpu_ctx.synchronize()
+    _sample_check(torch, gpu_ctx, oracle_mod, data, par, G, k, r, P)
+    # C3: exactly 2 erasures per group, uniform over the 13 shards
+    rng = np.random.default_rng(SEED + 3)
+    keys = rng.random((G, k + r))
+    pos = np.argsort(keys, axis=1)[:, :2]
+    masks = (np.left_shift(np.uint64(1), pos.astype(np.uint64))).sum(axis=1, dtype=np.uint64)
+    orig = data.clone()
+    dm = torch.from_numpy(masks.view(np.int64)).cuda()
+    lost = torch.zeros((G, k), dtype=torch.bool, device="cuda")
+    bits = torch.arange(k, device="cuda", dtype=torch.int64)
+    lost = ((dm.view(G, 1) >> bits.view(1, k)) & 1).bool()
+    data.view(G, k, P)[lost] = 0xEE
+    st = torch.zeros(G, dtype=torch.uint8, device="cuda")
+    gpu_ctx.decode_dev(data, par, dm, G, k, r, P, st)
+    gpu_ctx.synchronize()
+    assert int(st.sum().item()) == 0
+    assert torch.equal(data, orig)
+
+
+@pytest.mark.slow
+def test_full_size_c4_shard_encode(gpu_ctx, oracle_mod, torch_cuda):
+    torch = torch_cuda
+    k, r, P, G = 20, 5, 1200, 1_000_000      # one GPU's shard of C4 (8M groups / 8)
+    data = torch.empty(G * k * P, dtype=torch.uint8, device="cuda")
+    par = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_random_dev(data, data.numel(), SEED + 4)
+    gpu_ctx.encode_dev(data, G, k, r, P, par)
+    gpu_ctx.synchronize()
+    _sample_check(torch, gpu_ctx, oracle_mod, data, par, G, k, r, P, n=24)
+    # erase r shards in a slice of groups and rebuild
+    Gs = 50_000
+    rng = np.random.default_rng(5)
+    pos = np.argsort(rng.random((Gs, k + r)), axis=1)[:, :r]
+    masks = (np.left_shift(np.uint64(1), pos.astype(np.uint64))).sum(axis=1, dtype=np.uint64)
+    dm = torch.from_numpy(masks.view(np.int64)).cuda()
+    sub = data[:Gs * k * P]
+    orig = sub.clone()
+    bits = torch.arange(k, device="cuda", dtype=torch.int64)
+    lost = ((dm.view(Gs, 1) >> bits.view(1, k)) & 1).bool()
+    sub.view(Gs, k, P)[lost] = 0x11
+    gpu_ctx.decode_dev(sub, par[:Gs * r * P], dm, Gs, k, r, P)
+    gpu_ctx.synchronize()
+    assert torch.equal(sub, orig)
