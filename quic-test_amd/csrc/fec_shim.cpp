@@ -178,7 +178,7 @@ FECEncoderCtx* make_ctx(double redundancy, uint32_t max_groups, int device) {
   ctx->redundancy = (redundancy > 0 && redundancy <= 1.0) ? redundancy : 0.10;
   ctx->max_groups = max_groups > 0 ? max_groups : 1024;
   ctx->device = device;
-  const hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  const hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault);
   if (e != hipSuccess) {
     set_error("fec_encoder_new: hipStreamCreate: %s", hipGetErrorString(e));
     ctx->stream = nullptr;

@@ -65,6 +65,14 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
     if _lib is not None and path is None:
         return _lib
     p = Path(path) if path else Path(os.environ.get("QUICFEC_LIB", LIB_PATH))
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7.  If torch is
+    # importable, load it first so libfec_hip.so binds to the same (already loaded)
+    # runtime by SONAME instead of pulling /opt/rocm's copy next to it.
+    if os.environ.get("QUICFEC_NO_TORCH", "0") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     if not p.exists():
         raise FileNotFoundError(
             f"libfec_hip.so not found at {p}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"

@@ -1,0 +1,19 @@
+#!/usr/bin/env bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel trace.
+# Every GPU step has its own time limit; the first failure ends the script.
+set -euo pipefail
+ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
+OUT="$ROOT/gpurun_out"
+mkdir -p "$OUT"
+cd "$ROOT"
+echo "== pytest -m gpu"; timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1 || { tail -50 "$OUT/pytest_gpu.log"; exit 1; }
+tail -3 "$OUT/pytest_gpu.log"
+echo "== smoke"; timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; tail -2 "$OUT/smoke.log"
+echo "== bench"; timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err"; cat "$OUT/bench.json"
+if [ "${PROFILE:-1}" = "1" ]; then
+  echo "== rocprofv3"
+  export TMPDIR=/tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-verify > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+  find "$OUT/prof" -name "*kernel_stats.csv" -exec cat {} \;
+fi

@@ -274,8 +274,8 @@ def test_full_size_c2_c3_round_trip(gpu_ctx, oracle_mod, torch_cuda):
     lost = ((dm.view(G, 1) >> bits.view(1, k)) & 1).bool()
     data.view(G, k, P)[lost] = 0xEE
     st = torch.zeros(G, dtype=torch.uint8, device="cuda")
-    gpu_ctx.decode_dev(data, par, dm, G, k, r, P, st)
-    gpu_ctx.synchronize()
+    gpu_ctx.decode_dev(data, par, dm, G, k, r, P, st, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
     assert int(st.sum().item()) == 0
     assert torch.equal(data, orig)
 
@@ -301,6 +301,6 @@ def test_full_size_c4_shard_encode(gpu_ctx, oracle_mod, torch_cuda):
     bits = torch.arange(k, device="cuda", dtype=torch.int64)
     lost = ((dm.view(Gs, 1) >> bits.view(1, k)) & 1).bool()
     sub.view(Gs, k, P)[lost] = 0x11
-    gpu_ctx.decode_dev(sub, par[:Gs * r * P], dm, Gs, k, r, P)
-    gpu_ctx.synchronize()
+    gpu_ctx.decode_dev(sub, par[:Gs * r * P], dm, Gs, k, r, P, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
     assert torch.equal(sub, orig)
