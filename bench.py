@@ -182,6 +182,50 @@ def cpu_baseline(cfg: dict, seconds: float = 8.0) -> dict:
     }
 
 
+def e2e_pinned(ctx, d_data, d_parity, d_masks, G: int, cfg: dict, reps: int = 3) -> dict:
+    """The path as the QUIC client/server sees it: packets start and end in host memory.
+    Page-locked host buffers (the same allocator kind as fec_alloc_slab) go through the
+    synchronous API, which pipelines ~64 MB chunks H2D -> kernel -> D2H on 3 streams."""
+    import torch
+    k, r, P = cfg["k"], cfg["r"], cfg["P"]
+    h_data = torch.empty(d_data.numel(), dtype=torch.uint8, pin_memory=True)
+    h_par = torch.empty(d_parity.numel(), dtype=torch.uint8, pin_memory=True)
+    h_data.copy_(d_data)
+    torch.cuda.synchronize()
+    out = {}
+    # raw copy rates on this box for reference
+    t0 = time.perf_counter()
+    d_data.copy_(h_data, non_blocking=True)
+    torch.cuda.synchronize()
+    out["h2d_GBps"] = round(h_data.numel() / (time.perf_counter() - t0) / 1e9, 2)
+    t0 = time.perf_counter()
+    h_data.copy_(d_data, non_blocking=True)
+    torch.cuda.synchronize()
+    out["d2h_GBps"] = round(h_data.numel() / (time.perf_counter() - t0) / 1e9, 2)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ctx.encode(h_data, k, r, P, h_par, num_groups=G)
+        ts.append(time.perf_counter() - t0)
+    te = min(ts)
+    out["encode_GiBps"] = round(k * P * G / te / 2**30, 2)
+    out["encode_ms"] = round(te * 1e3, 2)
+    if d_masks is not None:
+        h_masks = d_masks.cpu().numpy().view("uint64")
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ctx.decode(h_data, h_par, h_masks, k, r, P, num_groups=G)
+            ts.append(time.perf_counter() - t0)
+        td = min(ts)
+        out["decode_GiBps"] = round(k * P * G / td / 2**30, 2)
+        out["decode_ms"] = round(td * 1e3, 2)
+        out["roundtrip_GiBps"] = round(k * P * G / (te + td) / 2**30, 2)
+    out["note"] = "payload k*P*G per second, host page-locked in/out, best of %d" % reps
+    del h_data, h_par
+    return out
+
+
 def load_pmc_traffic(config: str):
     """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/pmc_<config>.json),
     if one exists for this build; else None."""
@@ -204,6 +248,8 @@ def main() -> int:
     ap.add_argument("--groups", type=int, default=0, help="groups per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also time the host-resident path (pinned buffers, H2D -> kernel -> D2H)")
     args = ap.parse_args()
 
     import numpy as np
@@ -310,6 +356,10 @@ def main() -> int:
                 "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes"],
                 "timing": "torch.cuda.Event on the launch stream, averaged over the timed steps"}
 
+    e2e = None
+    if args.e2e:
+        e2e = e2e_pinned(ctx, data, parity, masks if cfg["decode"] else None, G, cfg)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)
@@ -329,6 +379,8 @@ def main() -> int:
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if e2e is not None:
+            out["e2e_pinned"] = e2e
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

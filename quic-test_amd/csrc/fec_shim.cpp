@@ -66,10 +66,14 @@ struct DeviceGuard {
   }
 };
 
-// Grow-only device buffer.
+// Grow-only device buffer (freed with its owner).
 struct DevBuf {
   void* ptr = nullptr;
   size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     if (ptr) {
@@ -124,6 +128,14 @@ Mem classify_ptr(const void* p) {
 
 }  // namespace
 
+// One stage of the host<->device pipeline: its own stream and device buffers.
+struct PipeSlot {
+  hipStream_t s = nullptr;
+  DevBuf in, par, mask, status, rec;
+};
+constexpr int kPipeSlots = 3;
+constexpr uint64_t kPipeChunkBytes = 64ull << 20;  // data bytes per pipelined chunk
+
 struct FECEncoderCtx {
   double redundancy = 0.10;
   uint32_t max_groups = 1024;
@@ -132,12 +144,15 @@ struct FECEncoderCtx {
   std::mutex mu;
   // staging / workspace buffers
   DevBuf d_in, d_off, d_out, d_mask, d_status, d_rec, d_binom;
+  PipeSlot pipe[kPipeSlots];
   std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<EncodePlan>> enc_plans;
   std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<DecodePlan>> dec_plans;
 
   ~FECEncoderCtx() {
     DeviceGuard g(device);
     if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& p : pipe)
+      if (p.s) (void)hipStreamSynchronize(p.s);
     d_in.release();
     d_off.release();
     d_out.release();
@@ -145,8 +160,15 @@ struct FECEncoderCtx {
     d_status.release();
     d_rec.release();
     d_binom.release();
+    for (auto& p : pipe) {
+      p.in.release();
+      p.par.release();
+      p.mask.release();
+      p.status.release();
+      p.rec.release();
+      if (p.s) (void)hipStreamDestroy(p.s);
+    }
     enc_plans.clear();
-    for (auto& kv : dec_plans) kv.second->codebook.release();
     dec_plans.clear();
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -271,16 +293,17 @@ int encode_dev_locked(FECEncoderCtx* ctx, const uint8_t* d_data, const void* d_o
 
 int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
                       const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
-                      uint8_t* d_status, bool vec16, hipStream_t s) {
+                      uint8_t* d_status, bool vec16, hipStream_t s, DevBuf* rec = nullptr) {
   DecodePlan* plan = nullptr;
   int rc = get_decode_plan(ctx, k, r, &plan);
   if (rc != FEC_OK) return rc;
-  QFEC_HIP(ctx->d_rec.ensure(G * sizeof(uint32_t)));
+  DevBuf& ws = rec ? *rec : ctx->d_rec;
+  QFEC_HIP(ws.ensure(G * sizeof(uint32_t)));
   qfec::DecodeLaunch a;
   a.data = d_data;
   a.parity = d_parity;
   a.masks = d_masks;
-  a.rec_off = ctx->d_rec.as<uint32_t>();
+  a.rec_off = ws.as<uint32_t>();
   a.status = d_status;
   a.codebook = plan->codebook.as<uint8_t>();
   a.binom = ctx->d_binom.as<uint64_t>();
@@ -296,6 +319,73 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   a.P = P;
   a.vec16 = vec16;
   QFEC_HIP(qfec::launch_decode(a, s));
+  return FEC_OK;
+}
+
+int ensure_pipe(FECEncoderCtx* ctx) {
+  for (auto& p : ctx->pipe)
+    if (!p.s) QFEC_HIP(hipStreamCreateWithFlags(&p.s, hipStreamNonBlocking));
+  return FEC_OK;
+}
+
+// Host-resident batches: chunks of ~64 MB of data flow H2D -> kernel -> D2H, chunk c on
+// pipeline slot c % 3, so the copy engines (H2D and D2H run on separate DMA engines) and
+// the kernels of neighbouring chunks overlap.  Page-locked host buffers (fec_alloc_slab)
+// make the copies asynchronous; pageable ones still work, with less overlap.
+int encode_host_pipelined(FECEncoderCtx* ctx, const uint8_t* data, uint64_t G, uint32_t k, uint32_t r,
+                          uint32_t P, uint8_t* parity_out) {
+  int rc = ensure_pipe(ctx);
+  if (rc != FEC_OK) return rc;
+  const uint64_t in_g = uint64_t(k) * P, out_g = uint64_t(r) * P;
+  uint64_t cg = kPipeChunkBytes / in_g;
+  cg = cg == 0 ? 1 : (cg > G ? G : cg);
+  for (auto& p : ctx->pipe) {
+    QFEC_HIP(p.in.ensure(cg * in_g));
+    QFEC_HIP(p.par.ensure(cg * out_g));
+  }
+  const bool vec16 = (P % 16u) == 0;
+  uint64_t c = 0;
+  for (uint64_t g0 = 0; g0 < G; g0 += cg, ++c) {
+    PipeSlot& sl = ctx->pipe[c % kPipeSlots];
+    const uint64_t n = (G - g0 < cg) ? G - g0 : cg;
+    QFEC_HIP(hipMemcpyAsync(sl.in.ptr, data + g0 * in_g, n * in_g, hipMemcpyHostToDevice, sl.s));
+    rc = encode_dev_locked(ctx, sl.in.as<uint8_t>(), nullptr, qfec::OffsetKind::kNone, n, k, r, P,
+                           sl.par.as<uint8_t>(), vec16, sl.s);
+    if (rc != FEC_OK) return rc;
+    QFEC_HIP(hipMemcpyAsync(parity_out + g0 * out_g, sl.par.ptr, n * out_g, hipMemcpyDeviceToHost, sl.s));
+  }
+  for (auto& p : ctx->pipe) QFEC_HIP(hipStreamSynchronize(p.s));
+  return FEC_OK;
+}
+
+int decode_host_pipelined(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* parity, const uint64_t* masks,
+                          uint64_t G, uint32_t k, uint32_t r, uint32_t P, uint8_t* status_out) {
+  int rc = ensure_pipe(ctx);
+  if (rc != FEC_OK) return rc;
+  const uint64_t in_g = uint64_t(k) * P, par_g = uint64_t(r) * P;
+  uint64_t cg = kPipeChunkBytes / in_g;
+  cg = cg == 0 ? 1 : (cg > G ? G : cg);
+  for (auto& p : ctx->pipe) {
+    QFEC_HIP(p.in.ensure(cg * in_g));
+    QFEC_HIP(p.par.ensure(cg * par_g));
+    QFEC_HIP(p.mask.ensure(cg * 8));
+    QFEC_HIP(p.status.ensure(cg));
+  }
+  const bool vec16 = (P % 16u) == 0;
+  uint64_t c = 0;
+  for (uint64_t g0 = 0; g0 < G; g0 += cg, ++c) {
+    PipeSlot& sl = ctx->pipe[c % kPipeSlots];
+    const uint64_t n = (G - g0 < cg) ? G - g0 : cg;
+    QFEC_HIP(hipMemcpyAsync(sl.in.ptr, data + g0 * in_g, n * in_g, hipMemcpyHostToDevice, sl.s));
+    QFEC_HIP(hipMemcpyAsync(sl.par.ptr, parity + g0 * par_g, n * par_g, hipMemcpyHostToDevice, sl.s));
+    QFEC_HIP(hipMemcpyAsync(sl.mask.ptr, masks + g0, n * 8, hipMemcpyHostToDevice, sl.s));
+    rc = decode_dev_locked(ctx, sl.in.as<uint8_t>(), sl.par.as<uint8_t>(), sl.mask.as<uint64_t>(), n, k, r, P,
+                           sl.status.as<uint8_t>(), vec16, sl.s, &sl.rec);
+    if (rc != FEC_OK) return rc;
+    QFEC_HIP(hipMemcpyAsync(data + g0 * in_g, sl.in.ptr, n * in_g, hipMemcpyDeviceToHost, sl.s));
+    QFEC_HIP(hipMemcpyAsync(status_out + g0, sl.status.ptr, n, hipMemcpyDeviceToHost, sl.s));
+  }
+  for (auto& p : ctx->pipe) QFEC_HIP(hipStreamSynchronize(p.s));
   return FEC_OK;
 }
 
@@ -545,6 +635,8 @@ QFEC_EXPORT int fec_encode_batch_rs(FECEncoderCtx* ctx, const uint8_t* data, con
   const uint64_t out_bytes = G * r * uint64_t(P);
   const Mem dmem = classify_ptr(data);
   const Mem omem = classify_ptr(parity_out);
+  if (!offsets && dmem != Mem::kDevice && omem != Mem::kDevice)
+    return encode_host_pipelined(ctx, data, G, k, r, P, parity_out);
   const uint8_t* d_data = data;
   const void* d_off = nullptr;
   qfec::OffsetKind ok = qfec::OffsetKind::kNone;
@@ -628,6 +720,23 @@ QFEC_EXPORT int fec_decode_batch_rs(FECEncoderCtx* ctx, uint8_t* data, const uin
   const uint64_t data_bytes = G * k * uint64_t(P);
   const uint64_t par_bytes = G * r * uint64_t(P);
   const Mem dmem = classify_ptr(data), pmem = classify_ptr(parity), mmem = classify_ptr(masks);
+  if (dmem != Mem::kDevice && pmem != Mem::kDevice && mmem != Mem::kDevice &&
+      (!status_out || classify_ptr(status_out) != Mem::kDevice)) {
+    std::vector<uint8_t> st_local;
+    uint8_t* st = status_out;
+    if (!st) {
+      st_local.resize(G);
+      st = st_local.data();
+    }
+    rc = decode_host_pipelined(ctx, data, parity, masks, G, k, r, P, st);
+    if (rc != FEC_OK) return rc;
+    if (unrecoverable_out) {
+      uint64_t bad = 0;
+      for (uint64_t g = 0; g < G; ++g) bad += st[g] != 0;
+      *unrecoverable_out = bad;
+    }
+    return FEC_OK;
+  }
   uint8_t* d_data = data;
   const uint8_t* d_par = parity;
   const uint64_t* d_masks = masks;

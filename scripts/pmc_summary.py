@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-launch HBM bytes.
+
+    python scripts/pmc_summary.py <fetch_dir> <write_dir> <config> [out.json]
+
+Corrections (MI355X_MICROARCH.md §HBM and cdna_hip_programming.md §7):
+  * FETCH_SIZE / WRITE_SIZE are in KiB;
+  * on gfx950 FETCH_SIZE reports exactly half of the bytes of a wide coalesced streaming
+    read (16 B/lane global loads), so it is doubled;
+  * WRITE_SIZE reads the bytes exactly for 16-B-per-lane streaming stores.
+The kernels of this library only issue 16-B-per-lane streaming loads/stores on the hot
+path, so both corrections apply as stated.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+
+def collect(d: Path, counter: str):
+    vals = defaultdict(list)
+    for f in d.rglob("*counter_collection.csv"):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                name = row.get("Kernel_Name", "")
+                vals[name].append(float(row["Counter_Value"]))
+    return vals
+
+
+def short(name: str) -> str:
+    for key in ("encode_v16", "decode_v16", "classify", "fill_words", "encode_bytes", "decode_bytes"):
+        if key in name:
+            return key
+    return name[:40]
+
+
+def main():
+    fdir, wdir, config = Path(sys.argv[1]), Path(sys.argv[2]), sys.argv[3]
+    out = Path(sys.argv[4]) if len(sys.argv) > 4 else Path(__file__).resolve().parents[1] / "profiles" / f"pmc_{config}.json"
+    fetch = collect(fdir, "FETCH_SIZE")
+    write = collect(wdir, "WRITE_SIZE")
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes)",
+           "correction": "FETCH_SIZE x2 (gfx950 wide-stream read), KiB -> bytes"}
+    for name in set(fetch) | set(write):
+        s = short(name)
+        f = fetch.get(name, [])
+        w = write.get(name, [])
+        fk = sorted(f)[len(f) // 2] if f else None
+        wk = sorted(w)[len(w) // 2] if w else None
+        entry = {"kernel": name[:160], "dispatches": max(len(f), len(w)),
+                 "fetch_size_kib_median": fk, "write_size_kib_median": wk}
+        if fk is not None and wk is not None:
+            entry["hbm_read_bytes_per_launch"] = int(fk * 1024 * 2)
+            entry["hbm_write_bytes_per_launch"] = int(wk * 1024)
+            entry["hbm_bytes_per_launch"] = entry["hbm_read_bytes_per_launch"] + entry["hbm_write_bytes_per_launch"]
+        key = {"encode_v16": "encode", "decode_v16": "decode"}.get(s, s)
+        res[key] = entry
+    out.write_text(json.dumps(res, indent=1))
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -224,6 +224,38 @@ def test_single_loss_is_reference_xor_recovery(gpu_ctx, oracle_mod):
         assert np.array_equal(got[(g * k + mid) * P:(g * k + mid + 1) * P], rec)
 
 
+@pytest.mark.parametrize("pinned", [True, False])
+def test_host_pipeline_multi_chunk(gpu_ctx, oracle_mod, torch_cuda, pinned):
+    """Host-resident batches larger than one 64 MB pipeline chunk (5 chunks over 3 slots)."""
+    k, r, P, G = 10, 3, 1200, 27_000
+    data = oracle_mod.splitmix_bytes(G * k * P, SEED + 11)
+    exp = oracle_mod.rs_encode(data, G, k, r, P, nthreads=8)
+    if pinned:
+        h_data = torch_cuda.from_numpy(data).pin_memory()
+        h_par = torch_cuda.zeros(G * r * P, dtype=torch_cuda.uint8).pin_memory()
+    else:
+        h_data, h_par = data.copy(), np.zeros(G * r * P, dtype=np.uint8)
+    gpu_ctx.encode(h_data, k, r, P, h_par, num_groups=G)
+    got = h_par.numpy() if pinned else h_par
+    assert np.array_equal(got, exp)
+    rng = np.random.default_rng(12)
+    masks = _random_masks(rng, G, k, r, r + 1)
+    broken = _poison(data, masks, G, k, P)
+    ref = broken.copy()
+    bad_exp, st_exp = oracle_mod.rs_decode(ref, exp, masks, G, k, r, P, nthreads=8)
+    if pinned:
+        hb = torch_cuda.from_numpy(broken).pin_memory()
+        st = torch_cuda.zeros(G, dtype=torch_cuda.uint8).pin_memory()
+        bad = gpu_ctx.decode(hb, h_par, masks, k, r, P, status_out=st, num_groups=G)
+        hb, st = hb.numpy(), st.numpy()
+    else:
+        hb, st = broken, np.zeros(G, dtype=np.uint8)
+        bad = gpu_ctx.decode(hb, exp, masks, k, r, P, status_out=st)
+    assert bad == bad_exp
+    assert np.array_equal(st, st_exp)
+    assert np.array_equal(hb, ref)
+
+
 def test_fill_random_matches_oracle(gpu_ctx, oracle_mod, torch_cuda):
     for n, off in ((4096, 0), (1000, 8), (777, 3)):
         d = torch_cuda.zeros(n + 16, dtype=torch_cuda.uint8, device="cuda")
