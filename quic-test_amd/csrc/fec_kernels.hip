@@ -30,8 +30,9 @@ struct Tab {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Memory policy bits of the streaming kernels.
-constexpr int kNtLoad = 1;   // non-temporal loads (data read once)
-constexpr int kNtStore = 2;  // non-temporal stores
+constexpr int kNtLoad = 1;        // non-temporal loads (data read once)
+constexpr int kNtStore = 2;       // non-temporal stores
+constexpr int kNoCoefBranch = 4;  // decode: multiply by every coefficient, no 0/1 branches
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
@@ -255,6 +256,145 @@ __device__ __forceinline__ uint32_t rec_byte(const uint32_t* __restrict__ w, uin
   return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFu;
 }
 
+// NW-dword (NW = 4: 16 B, NW = 1: 4 B) load/store of one lane's piece.
+template <int NW, int POL>
+__device__ __forceinline__ void ldw(const uint8_t* p, uint32_t (&v)[NW]) {
+  if constexpr (NW == 4) {
+    const u32x4 t = ld16<POL>(p);
+    v[0] = t.x;
+    v[1] = t.y;
+    v[2] = t.z;
+    v[3] = t.w;
+  } else {
+    v[0] = *reinterpret_cast<const uint32_t*>(p);
+  }
+}
+
+template <int NW, int POL>
+__device__ __forceinline__ void stw(uint8_t* p, const uint32_t (&v)[NW]) {
+  if constexpr (NW == 4) {
+    st16<POL>(p, u32x4{v[0], v[1], v[2], v[3]});
+  } else {
+    if constexpr ((POL & kNtStore) != 0) __builtin_nontemporal_store(v[0], reinterpret_cast<uint32_t*>(p));
+    else *reinterpret_cast<uint32_t*>(p) = v[0];
+  }
+}
+
+// Rebuild rows [m0, m0 + MAXE) of one group's record at byte offset `off` of every
+// packet, NW dwords per lane.  The record (survivors, tables) is wave-uniform: SGPRs.
+template <int K, int MAXE, int POL, int NW>
+__device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, const Tab* __restrict__ tabs,
+                                             uint8_t* __restrict__ dg, const uint8_t* __restrict__ pg,
+                                             uint32_t k, uint32_t P, uint32_t off, uint32_t e, uint32_t m0,
+                                             bool xor_only) {
+  if (xor_only) {  // single data loss rebuilt from parity row 0: the reference XOR
+    uint32_t acc[NW] = {};
+    for (uint32_t s = 0; s < k; ++s) {
+      const uint32_t sid = rec_byte(rw, s);
+      const uint8_t* src = sid < k ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - k) * static_cast<uint64_t>(P);
+      uint32_t v[NW];
+      ldw<NW, POL>(src + off, v);
+#pragma unroll
+      for (int q = 0; q < NW; ++q) acc[q] ^= v[q];
+    }
+    stw<NW, POL>(dg + rec_byte(rw, 64) * static_cast<uint64_t>(P) + off, acc);
+    return;
+  }
+  uint32_t acc[MAXE][NW];
+#pragma unroll
+  for (int m = 0; m < MAXE; ++m)
+#pragma unroll
+    for (int q = 0; q < NW; ++q) acc[m][q] = 0;
+  auto consume = [&](const uint32_t (&v)[NW], uint32_t s, uint32_t kk) {
+    uint32_t s0[NW], s1[NW], s2[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      s0[q] = v[q] & 0x07070707u;
+      s1[q] = (v[q] >> 3) & 0x07070707u;
+      s2[q] = (v[q] >> 6) & 0x03030303u;
+    }
+#pragma unroll
+    for (int m = 0; m < MAXE; ++m) {
+      if (m0 + m < e) {
+        const Tab& t = tabs[(m0 + m) * kk + s];
+        if constexpr ((POL & kNoCoefBranch) != 0) {
+          // coefficient 0 / 1 tables are the zero / identity maps: no branch on the value
+#pragma unroll
+          for (int q = 0; q < NW; ++q) acc[m][q] ^= gmul(s0[q], s1[q], s2[q], t);
+        } else if (t.coef == 1u) {
+#pragma unroll
+          for (int q = 0; q < NW; ++q) acc[m][q] ^= v[q];
+        } else if (t.coef != 0u) {
+#pragma unroll
+          for (int q = 0; q < NW; ++q) acc[m][q] ^= gmul(s0[q], s1[q], s2[q], t);
+        }
+      }
+    }
+  };
+  if constexpr (K > 0) {
+    uint32_t x[K][NW];
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      const uint32_t sid = rec_byte(rw, s);
+      const uint8_t* src = sid < K ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - K) * static_cast<uint64_t>(P);
+      ldw<NW, POL>(src + off, x[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < K; ++s) consume(x[s], s, K);
+  } else {
+#pragma unroll 2
+    for (uint32_t s = 0; s < k; ++s) {
+      const uint32_t sid = rec_byte(rw, s);
+      const uint8_t* src = sid < k ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - k) * static_cast<uint64_t>(P);
+      uint32_t v[NW];
+      ldw<NW, POL>(src + off, v);
+      consume(v, s, k);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MAXE; ++m) {
+    if (m0 + m < e) {
+      const uint32_t eid = rec_byte(rw, 64 + m0 + m);
+      stw<NW, POL>(dg + eid * static_cast<uint64_t>(P) + off, acc[m]);
+    }
+  }
+}
+
+// One wave per group, so the record is wave-uniform (SGPRs).  A packet is covered by
+// whole 1 KiB passes of 16 B per lane, then the remainder (< 1 KiB) by 256 B passes of
+// 4 B per lane: at 1200 B that is 64 + 44 busy lanes instead of 64 + 11 lanes doing
+// 16-B work, i.e. 5 instead of 8 dword slots of VALU per lane and survivor.
+template <int K, int MAXE, int POL = 0>
+__global__ __launch_bounds__(256) void decode_wave(uint8_t* __restrict__ data,
+                                                   const uint8_t* __restrict__ parity,
+                                                   const uint32_t* __restrict__ rec_off,
+                                                   const uint8_t* __restrict__ codebook,
+                                                   uint64_t groups, uint32_t P, uint32_t k_rt, uint32_t r,
+                                                   uint32_t m0) {
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * 4u +
+                      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+  if (gw >= groups) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t rec = __builtin_amdgcn_readfirstlane(rec_off[gw]);
+  if (rec >= kRecBad) return;
+  const uint32_t k = K > 0 ? static_cast<uint32_t>(K) : k_rt;
+  const uint8_t* recp = codebook + static_cast<uint64_t>(rec) * 32u;
+  const uint32_t* rw = reinterpret_cast<const uint32_t*>(recp);
+  const uint32_t e = rw[24] & 0xFFu;
+  const bool xor_only = ((rw[24] >> 8) & 0xFFu) != 0;
+  if (m0 >= e) return;
+  const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
+  uint8_t* dg = data + gw * k * static_cast<uint64_t>(P);
+  const uint8_t* pg = parity + gw * r * static_cast<uint64_t>(P);
+  const uint32_t main_end = P & ~1023u;
+  for (uint32_t base = 0; base < main_end; base += 1024u)
+    decode_piece<K, MAXE, POL, 4>(rw, tabs, dg, pg, k, P, base + lane * 16u, e, m0, xor_only);
+  for (uint32_t base = main_end; base < P; base += 256u) {
+    const uint32_t off = base + lane * 4u;
+    if (off < P) decode_piece<K, MAXE, POL, 1>(rw, tabs, dg, pg, k, P, off, e, m0, xor_only);
+  }
+}
+
 // One wave per group.  K > 0: compile-time k (survivor loads all issued first).
 // MAXE: rows rebuilt per pass (rows [m0, m0 + MAXE) of the record's e).
 template <int K, int MAXE, int POL = 0>
@@ -340,6 +480,67 @@ __global__ __launch_bounds__(256) void decode_v16(uint8_t* __restrict__ data,
         const uint32_t eid = rec_byte(rw, 64 + m0 + m);
         st16<POL>(dg + eid * static_cast<uint64_t>(P) + coff, acc[m]);
       }
+    }
+  }
+}
+
+// Tiled decode: a workgroup owns `tile` whole groups and one lane owns one 16-byte column
+// of one group (all lanes busy, like encode_v16's tiled form).  A wave may then hold two
+// groups with different erasure patterns, so each lane reads its own record (header and
+// tables through the vector cache; lanes of one group read the same lines) and runs the
+// multiply for every coefficient, 0 and 1 included (their tables are the zero / identity
+// maps): no lane-divergent branches except the row count e.
+template <int K, int MAXE, int POL = 0>
+__global__ __launch_bounds__(512) void decode_tiled(uint8_t* __restrict__ data,
+                                                    const uint8_t* __restrict__ parity,
+                                                    const uint32_t* __restrict__ rec_off,
+                                                    const uint8_t* __restrict__ codebook,
+                                                    uint64_t groups, uint32_t cpp, uint32_t P,
+                                                    uint32_t r, uint32_t tile) {
+  const uint32_t lane = threadIdx.x;
+  uint32_t gl = lane / cpp;
+  const uint32_t col = lane - gl * cpp;
+  if (gl >= tile) return;
+  gl += blockIdx.x * tile;
+  if (gl >= groups) return;
+  const uint64_t g = gl;
+  const uint32_t rec = rec_off[g];
+  if (rec >= kRecBad) return;
+  const uint8_t* recp = codebook + static_cast<uint64_t>(rec) * 32u;
+  const uint32_t* rw = reinterpret_cast<const uint32_t*>(recp);
+  const uint32_t e = rw[24] & 0xFFu;
+  const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
+  uint8_t* dg = data + g * K * static_cast<uint64_t>(P);
+  const uint8_t* pg = parity + g * r * static_cast<uint64_t>(P);
+  const size_t coff = static_cast<size_t>(col) * 16u;
+  uint32_t sw[(K + 3) / 4];
+#pragma unroll
+  for (int q = 0; q < (K + 3) / 4; ++q) sw[q] = rw[q];
+  u32x4 x[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    const uint32_t sid = (sw[s >> 2] >> (8 * (s & 3))) & 0xFFu;
+    const uint8_t* src = sid < K ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - K) * static_cast<uint64_t>(P);
+    x[s] = ld16<POL>(src + coff);
+  }
+  u32x4 acc[MAXE];
+#pragma unroll
+  for (int m = 0; m < MAXE; ++m) acc[m] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    Sel sl;
+    prep(x[s], sl);
+#pragma unroll
+    for (int m = 0; m < MAXE; ++m) {
+      if (static_cast<uint32_t>(m) < e) mac(acc[m], sl, tabs[m * K + s]);
+    }
+  }
+  const uint32_t ew = rw[16];  // erased ids E_0..E_3 (bytes 64..67)
+#pragma unroll
+  for (int m = 0; m < MAXE; ++m) {
+    if (static_cast<uint32_t>(m) < e) {
+      const uint32_t eid = m < 4 ? (ew >> (8 * m)) & 0xFFu : rec_byte(rw, 64 + m);
+      st16<POL>(dg + eid * static_cast<uint64_t>(P) + coff, acc[m]);
     }
   }
 }
@@ -552,6 +753,46 @@ hipError_t run_decode_v16(const DecodeLaunch& a, hipStream_t s) {
   return hipSuccess;
 }
 
+template <int K, int MAXE, int POL>
+hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
+  const uint32_t passes = (a.r + MAXE - 1) / MAXE;  // e <= r
+  for (uint32_t p = 0; p < passes; ++p) {
+    const uint32_t m0 = p * MAXE;
+    const uint64_t blocks = (a.groups + 3) / 4;
+    for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 24)) {
+      const uint64_t bn = (blocks - b0 < (1u << 24)) ? blocks - b0 : (1u << 24);
+      const uint64_t g0 = b0 * 4;
+      const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
+      hipLaunchKernelGGL((decode_wave<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(256), 0, s,
+                         a.data + g0 * a.k * static_cast<uint64_t>(a.P),
+                         a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
+                         a.k, a.r, m0);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
+template <int K, int MAXE, int POL>
+hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s) {
+  const uint32_t cpp = a.P / 16u;
+  const uint32_t bs = (tile * cpp + 63) / 64 * 64;
+  const uint64_t blocks = (a.groups + tile - 1) / tile;
+  for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 30)) {
+    const uint64_t bn = (blocks - b0 < (1u << 30)) ? blocks - b0 : (1u << 30);
+    const uint64_t g0 = b0 * tile;
+    const uint64_t gn = (a.groups - g0 < bn * tile) ? a.groups - g0 : bn * tile;
+    hipLaunchKernelGGL((decode_tiled<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(bs), 0, s,
+                       a.data + g0 * a.k * static_cast<uint64_t>(a.P),
+                       a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, cpp,
+                       a.P, a.r, tile);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 }  // namespace
 
 hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
@@ -574,6 +815,37 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
+  }
+  const uint32_t tile = pick_tile(a.P / 16u, a.k, a.P);
+  if (tile > 0 && (a.variant == kDecodeTiledPlain || a.variant == kDecodeTiledNt)) {
+    const bool nt = a.variant == kDecodeTiledNt;
+#define QFEC_TILED(KK, RR)                                                                   \
+  if (a.k == KK && a.r == RR)                                                                \
+    return nt ? run_decode_tiled<KK, RR, kNtStore>(a, tile, s) : run_decode_tiled<KK, RR, 0>(a, tile, s);
+    QFEC_TILED(10, 3)
+    QFEC_TILED(10, 1)
+    QFEC_TILED(20, 5)
+    QFEC_TILED(4, 2)
+#undef QFEC_TILED
+  }
+  if (a.variant == kDecodeWaveNoBranch) {
+#define QFEC_WAVE_NB(KK, RR) \
+  if (a.k == KK && a.r == RR) return run_decode_wave<KK, RR, kNtStore | kNoCoefBranch>(a, s);
+    QFEC_WAVE_NB(10, 3)
+    QFEC_WAVE_NB(20, 5)
+#undef QFEC_WAVE_NB
+  }
+  if (a.variant != kDecodeWavePerGroup) {
+    const bool nt = a.variant != kDecodeWavePlain;
+#define QFEC_WAVE(KK, RR)                                                                    \
+  if (a.k == KK && a.r == RR)                                                                \
+    return nt ? run_decode_wave<KK, RR, kNtStore>(a, s) : run_decode_wave<KK, RR, 0>(a, s);
+    QFEC_WAVE(10, 3)
+    QFEC_WAVE(10, 1)
+    QFEC_WAVE(20, 5)
+    QFEC_WAVE(4, 2)
+#undef QFEC_WAVE
+    return nt ? run_decode_wave<0, 8, kNtStore>(a, s) : run_decode_wave<0, 8, 0>(a, s);
   }
   if (a.k == 10 && a.r == 3) return run_decode_v16<10, 3>(a, s);
   if (a.k == 10 && a.r == 1) return run_decode_v16<10, 1>(a, s);

@@ -28,7 +28,17 @@ struct LevelMeta {           // codebook levels e = 1..32 (see gf256.hpp)
   uint64_t count_r[33];      // C(r, e)
 };
 
+// Decode kernel selection (tests / probes; the library uses kDecodeAuto).
+constexpr int kDecodeAuto = 0;           // the measured best of the forms below
+constexpr int kDecodeWavePerGroup = 1;   // one wave per group, 16-B lanes only
+constexpr int kDecodeTiledPlain = 2;     // workgroup = whole groups, per-lane records
+constexpr int kDecodeTiledNt = 3;        //   same, non-temporal stores
+constexpr int kDecodeWavePlain = 4;      // one wave per group, 16-B passes + 4-B tail
+constexpr int kDecodeWaveNt = 5;         //   same, non-temporal stores (the default)
+constexpr int kDecodeWaveNoBranch = 6;   //   same, no branch on coefficient 0 / 1
+
 struct DecodeLaunch {
+  int variant = kDecodeAuto;
   uint8_t* data;
   const uint8_t* parity;
   const uint64_t* masks;

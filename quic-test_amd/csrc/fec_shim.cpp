@@ -398,6 +398,7 @@ FECEncoderCtx* default_ctx() {
 }
 
 void xor_packets_gpu(const uint8_t* packets[], size_t n, size_t packet_size, uint8_t* repair) {
+  g_last_error.clear();  // void return: callers read fec_hip_last_error() to detect failure
   if (n == 0 || packet_size == 0) return;  // fec_xor_simd.cpp:417-419
   if (!packets || !repair) {
     set_error("xor_packets: NULL argument");

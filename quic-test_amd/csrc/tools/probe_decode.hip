@@ -1,0 +1,149 @@
+// probe_decode.hip — development probe: decode kernel variants A/B in one process, each
+// verified to rebuild the poisoned shards exactly.  Not part of the library.
+#include "../fec_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../gf256.hpp"
+
+#define CK(x)                                                                          \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess) {                                                            \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      std::exit(2);                                                                    \
+    }                                                                                  \
+  } while (0)
+
+namespace qfec {
+namespace {
+__global__ void poison(uint8_t* data, const uint64_t* masks, uint64_t groups, uint32_t k, uint32_t P) {
+  const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  const uint64_t g = t / (uint64_t(k) * P);
+  if (g >= groups) return;
+  const uint32_t j = uint32_t((t / P) % k);
+  if ((masks[g] >> j) & 1) data[t] = 0xEE;
+}
+}  // namespace
+}  // namespace qfec
+
+using namespace qfec;
+
+int main(int argc, char** argv) {
+  const uint32_t k = argc > 3 ? std::atoi(argv[3]) : 10, r = argc > 4 ? std::atoi(argv[4]) : 3, P = 1200;
+  const uint32_t ners = argc > 5 ? std::atoi(argv[5]) : 2;
+  const uint64_t G = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1000000;
+  const int rounds = argc > 2 ? std::atoi(argv[2]) : 7;
+  const uint64_t nd = G * k * P, np = G * r * P;
+  uint8_t *data, *orig, *par;
+  uint64_t* masks;
+  uint32_t* rec;
+  CK(hipMalloc(&data, nd));
+  CK(hipMalloc(&orig, nd));
+  CK(hipMalloc(&par, np));
+  CK(hipMalloc(&masks, G * 8));
+  CK(hipMalloc(&rec, G * 4));
+  CK(launch_fill_splitmix(data, nd, 0x5EED0002, 0, nullptr));
+  std::vector<uint8_t> M;
+  parity_matrix(k, r, M);
+  std::vector<CoefEntry> tab;
+  for (uint32_t i = 1; i < r; ++i)
+    for (uint32_t j = 0; j < k; ++j) tab.push_back(make_entry(M[i * k + j]));
+  void* dtab = nullptr;
+  if (!tab.empty()) {
+    CK(hipMalloc(&dtab, tab.size() * 32));
+    CK(hipMemcpy(dtab, tab.data(), tab.size() * 32, hipMemcpyHostToDevice));
+  }
+  EncodeLaunch el{data, nullptr, OffsetKind::kNone, par, G, k, r, P, dtab, true};
+  CK(launch_encode(el, nullptr));
+  CK(hipMemcpy(orig, data, nd, hipMemcpyDeviceToDevice));
+  // exactly `ners` erasures per group, uniform over the k + r shards
+  std::vector<uint64_t> hm(G);
+  std::mt19937_64 rng(0x5EED0003);
+  uint64_t alg = 0;
+  for (uint64_t g = 0; g < G; ++g) {
+    uint64_t m = 0;
+    while (uint32_t(__builtin_popcountll(m)) < ners) m |= 1ull << (rng() % (k + r));
+    hm[g] = m;
+    const uint32_t e = __builtin_popcountll(m & ((1ull << k) - 1));
+    if (e) alg += uint64_t(k + e) * P;
+  }
+  CK(hipMemcpy(masks, hm.data(), G * 8, hipMemcpyHostToDevice));
+  CodebookLayout L;
+  codebook_layout(k, r, 2ull << 30, L);
+  std::vector<uint8_t> book;
+  build_codebook(L, M, book);
+  uint8_t* dbook;
+  uint64_t* dbin;
+  CK(hipMalloc(&dbook, book.size()));
+  CK(hipMemcpy(dbook, book.data(), book.size(), hipMemcpyHostToDevice));
+  CK(hipMalloc(&dbin, sizeof(binom().c)));
+  CK(hipMemcpy(dbin, binom().c, sizeof(binom().c), hipMemcpyHostToDevice));
+  DecodeLaunch dl;
+  dl.data = data;
+  dl.parity = par;
+  dl.masks = masks;
+  dl.rec_off = rec;
+  dl.status = nullptr;
+  dl.codebook = dbook;
+  dl.binom = dbin;
+  std::memset(&dl.meta, 0, sizeof(dl.meta));
+  for (uint32_t e = 1; e <= 32; ++e) {
+    dl.meta.base[e] = L.level_base[e];
+    dl.meta.stride[e] = L.level_stride[e];
+    dl.meta.count_r[e] = binom().c[r][e];
+  }
+  dl.groups = G;
+  dl.k = k;
+  dl.r = r;
+  dl.P = P;
+  dl.vec16 = true;
+  struct Var {
+    std::string name;
+    int variant;
+    std::vector<float> ms;
+  };
+  std::vector<Var> vars = {{"wave-per-group v16", kDecodeWavePerGroup, {}},
+                           {"tiled nt-store", kDecodeTiledNt, {}},
+                           {"wave 16B+4B plain", kDecodeWavePlain, {}},
+                           {"wave 16B+4B nt", kDecodeWaveNt, {}},
+                           {"wave nt no-branch", kDecodeWaveNoBranch, {}}};
+  for (auto& v : vars) {
+    dl.variant = v.variant;
+    poison<<<uint32_t((nd + 255) / 256), 256>>>(data, masks, G, k, P);
+    CK(launch_decode(dl, nullptr));
+    CK(hipDeviceSynchronize());
+    std::vector<uint8_t> a(nd), b(nd);
+    CK(hipMemcpy(a.data(), data, nd, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), orig, nd, hipMemcpyDeviceToHost));
+    std::printf("check %-18s %s\n", v.name.c_str(), a == b ? "OK" : "MISMATCH");
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int rd = 0; rd < rounds; ++rd)
+    for (auto& v : vars) {
+      dl.variant = v.variant;
+      CK(hipEventRecord(e0));
+      CK(launch_decode(dl, nullptr));
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      v.ms.push_back(ms);
+    }
+  std::printf("k=%u r=%u erasures=%u groups=%llu algorithmic bytes %.3f GB\n", k, r, ners, (unsigned long long)G, alg / 1e9);
+  std::printf("%-20s %10s %10s %10s\n", "variant", "med_ms", "min_ms", "GB/s(med)");
+  for (auto& v : vars) {
+    std::sort(v.ms.begin(), v.ms.end());
+    const float med = v.ms[v.ms.size() / 2];
+    std::printf("%-20s %10.4f %10.4f %10.1f\n", v.name.c_str(), med, v.ms[0], alg / (med * 1e-3) / 1e9);
+  }
+  return 0;
+}

@@ -1,0 +1,454 @@
+// fec.cpp — C++ mirror of internal/fec (see fec.hpp) on top of libfec_hip.so's C-ABI.
+#include "fec.hpp"
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "fec_hip.h"
+
+namespace quicfec {
+
+namespace {
+
+Error errorf(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+Error errorf(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  return Error{buf};
+}
+
+double clamp_redundancy(double r) { return (r <= 0 || r > 1) ? 0.10 : r; }  // encoder.go:30-32
+
+}  // namespace
+
+// ===================================================================== FECEncoderCXX
+std::unique_ptr<FECEncoderCXX> FECEncoderCXX::New(double redundancy, int maxGroups) {
+  redundancy = clamp_redundancy(redundancy);  // fec_cgo.go:44-46
+  if (maxGroups <= 0) maxGroups = 1024;       // fec_cgo.go:47-49
+  std::unique_ptr<FECEncoderCXX> enc(new FECEncoderCXX());
+  enc->maxGroups_ = maxGroups;
+  enc->ctx_ = fec_encoder_new(redundancy, static_cast<uint32_t>(maxGroups));
+  if (!enc->ctx_) return nullptr;
+  // slab: maxGroups * 10 packets * 1200 B (+ one zero packet, see EncodeBatch)
+  enc->slabSize_ = size_t(maxGroups) * 10 * 1200 + 1200;
+  enc->slab_ = static_cast<uint8_t*>(fec_alloc_slab(enc->slabSize_));
+  if (!enc->slab_) {
+    fec_encoder_free(enc->ctx_);
+    enc->ctx_ = nullptr;
+    return nullptr;
+  }
+  enc->offsets_.reserve(size_t(maxGroups) * 10);
+  enc->repairSize_ = size_t(maxGroups) * 1200;
+  enc->repair_ = static_cast<uint8_t*>(fec_alloc_repair_buffer(enc->repairSize_));
+  if (!enc->repair_) {
+    fec_free_slab(enc->slab_);
+    enc->slab_ = nullptr;
+    fec_encoder_free(enc->ctx_);
+    enc->ctx_ = nullptr;
+    return nullptr;
+  }
+  enc->initialized_ = true;
+  return enc;
+}
+
+FECEncoderCXX::~FECEncoderCXX() { Close(); }
+
+Error FECEncoderCXX::resizeSlab(size_t newSize) {
+  if (newSize <= slabSize_) return {};
+  auto* p = static_cast<uint8_t*>(fec_alloc_slab(newSize));
+  if (!p) return errorf("failed to allocate slab of size %zu", newSize);
+  std::memcpy(p, slab_, slabSize_);
+  fec_free_slab(slab_);
+  slab_ = p;
+  slabSize_ = newSize;
+  return {};
+}
+
+Error FECEncoderCXX::resizeRepairBuffer(size_t newSize) {
+  if (newSize <= repairSize_) return {};
+  auto* p = static_cast<uint8_t*>(fec_alloc_repair_buffer(newSize));
+  if (!p) return errorf("failed to allocate repair buffer of size %zu", newSize);
+  fec_free_repair_buffer(repair_);
+  repair_ = p;
+  repairSize_ = newSize;
+  return {};
+}
+
+Error FECEncoderCXX::EncodeBatch(const std::vector<FECBatchGroup>& groups, int packetSize,
+                                 std::vector<RepairPacket>* out) {
+  if (!initialized_) return errorf("encoder not initialized");  // fec_cgo.go:96-98
+  if (out) out->clear();
+  if (groups.empty()) return {};                                // :100-102
+  if (packetSize <= 0) return errorf("invalid packet size %d", packetSize);
+  std::lock_guard<std::mutex> lk(mu_);
+  const size_t P = static_cast<size_t>(packetSize);
+  // Slab layout: [zero packet][group 0 packet 0..9][group 1 ...], every packet padded to
+  // packetSize.  Slots a group does not fill point at the zero packet, so a partial group
+  // XORs exactly the packets it has (encoder.go:133-143).
+  const size_t need = P + groups.size() * 10 * P;
+  if (Error e = resizeSlab(need)) return errorf("failed to resize slab: %s", e.msg.c_str());
+  if (need > 0xFFFFFFFFull) return errorf("batch exceeds the 4 GiB u32-offset slab (fec_xor_simd.h:71)");
+  std::memset(slab_, 0, P);
+  offsets_.clear();
+  size_t off = P;
+  for (const auto& g : groups) {
+    if (g.Packets.size() > 10) return errorf("group of %zu packets: fec_encode_batch takes 10", g.Packets.size());
+    for (size_t p = 0; p < 10; ++p) {
+      if (p < g.Packets.size()) {
+        const Bytes& pkt = g.Packets[p];
+        const size_t n = std::min(pkt.size(), P);
+        std::memcpy(slab_ + off, pkt.data(), n);
+        if (n < P) std::memset(slab_ + off + n, 0, P - n);
+        offsets_.push_back(static_cast<uint32_t>(off));
+        off += P;
+      } else {
+        offsets_.push_back(0);
+      }
+    }
+  }
+  const size_t repairNeeded = groups.size() * P;
+  if (Error e = resizeRepairBuffer(repairNeeded)) return errorf("failed to resize repair buffer: %s", e.msg.c_str());
+  const int ret = fec_encode_batch(ctx_, slab_, offsets_.data(), static_cast<uint32_t>(groups.size()),
+                                   static_cast<uint32_t>(P), repair_);
+  if (ret != 0) return errorf("C++ encoding failed with code %d", ret);  // :147-149
+  if (out) {
+    out->resize(groups.size());
+    for (size_t i = 0; i < groups.size(); ++i) (*out)[i].assign(repair_ + i * P, repair_ + (i + 1) * P);
+  }
+  return {};
+}
+
+Error FECEncoderCXX::Close() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!initialized_) return {};
+  if (ctx_) fec_encoder_free(ctx_);
+  ctx_ = nullptr;
+  if (slab_) fec_free_slab(slab_);
+  slab_ = nullptr;
+  if (repair_) fec_free_repair_buffer(repair_);
+  repair_ = nullptr;
+  initialized_ = false;
+  return {};
+}
+
+// ===================================================================== HybridFECEncoder
+HybridFECEncoder::HybridFECEncoder(double redundancy) : redundancy_(clamp_redundancy(redundancy)) {
+  packets_.reserve(groupSize_);
+  packetIDs_.reserve(groupSize_);
+  cxx_ = FECEncoderCXX::New(redundancy_, 1024);  // encoder_hybrid.go:44
+  useCXX_ = cxx_ && cxx_->initialized();
+}
+
+AddPacketResult HybridFECEncoder::AddPacket(const uint8_t* packet, size_t len, uint64_t packetID) {
+  std::lock_guard<std::mutex> lk(mu_);
+  packets_.emplace_back(packet, packet + len);  // the packet is copied (:64-65)
+  packetIDs_.push_back(packetID);
+  if (static_cast<int>(packets_.size()) >= groupSize_) return generateRedundancy();
+  return {};
+}
+
+AddPacketResult HybridFECEncoder::generateRedundancy() {
+  AddPacketResult res;
+  if (!useCXX_) {
+    res.err = errorf("GPU FEC engine unavailable: %s", fec_hip_last_error());
+    return res;
+  }
+  if (packets_.empty()) {
+    res.err = errorf("no packets in group");
+    return res;
+  }
+  size_t maxSize = 0;
+  for (const auto& p : packets_) maxSize = std::max(maxSize, p.size());
+  if (maxSize == 0) {
+    res.err = errorf("empty packets");
+    return res;
+  }
+  FECBatchGroup group;
+  group.Packets = packets_;
+  for (const auto& p : packets_) group.Sizes.push_back(static_cast<uint32_t>(p.size()));
+  std::vector<RepairPacket> repairs;
+  if (Error e = cxx_->EncodeBatch({group}, static_cast<int>(maxSize), &repairs)) {
+    res.err = errorf("C++ encoding failed: %s", e.msg.c_str());
+    return res;
+  }
+  if (repairs.empty()) {
+    res.err = errorf("no repair packet generated");
+    return res;
+  }
+  res.redundancy = createFECPacket(repairs[0], static_cast<int>(packets_.size()));
+  packets_.clear();
+  packetIDs_.clear();
+  ++groupID_;
+  // metric updates exactly as encoder_hybrid.go:124-127 (PacketsEncoded counts groupSize)
+  metrics_.GroupsProcessed++;
+  metrics_.PacketsEncoded += groupSize_;
+  metrics_.RedundancyPackets++;
+  metrics_.RedundancyBytes += static_cast<int64_t>(res.redundancy.size());
+  res.needsRedundancy = true;
+  return res;
+}
+
+// encoder_hybrid.go:175-192: FE C0 | groupID u64 LE | count u8 | payload
+Bytes HybridFECEncoder::createFECPacket(const Bytes& repair, int packetCount) {
+  Bytes out(11 + repair.size());
+  out[0] = 0xFE;
+  out[1] = 0xC0;
+  for (int b = 0; b < 8; ++b) out[2 + b] = static_cast<uint8_t>(groupID_ >> (8 * b));
+  out[10] = static_cast<uint8_t>(packetCount);
+  std::memcpy(out.data() + 11, repair.data(), repair.size());
+  return out;
+}
+
+std::pair<Bytes, Error> HybridFECEncoder::Flush() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (packets_.empty()) return {{}, {}};
+  AddPacketResult r = generateRedundancy();
+  return {r.redundancy, r.err};
+}
+
+FECMetrics HybridFECEncoder::GetMetrics() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return metrics_;
+}
+
+void HybridFECEncoder::ResetMetrics() {
+  std::lock_guard<std::mutex> lk(mu_);
+  metrics_ = FECMetrics();
+}
+
+Error HybridFECEncoder::Close() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (cxx_) return cxx_->Close();
+  return {};
+}
+
+// ===================================================================== FECDecoder
+namespace {
+
+// decoder.go:62-69
+Bytes padTo(const uint8_t* data, size_t len, size_t n) {
+  Bytes out(n, 0);
+  std::memcpy(out.data(), data, std::min(len, n));
+  return out;
+}
+
+}  // namespace
+
+FECDecoder::FECDecoder() = default;
+
+bool FECDecoder::AddPacket(const uint8_t* packet, size_t len, uint64_t packetID, uint64_t groupID) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (groups_.find(groupID) == groups_.end() && groups_.size() >= kMaxActiveGroups) evictOldestGroup();
+  auto it = groups_.find(groupID);
+  if (it == groups_.end()) {
+    Group g;
+    g.groupID = groupID;
+    g.createdAt = std::chrono::steady_clock::now();
+    it = groups_.emplace(groupID, std::move(g)).first;
+    metrics_.GroupsActive = static_cast<int64_t>(groups_.size());
+  }
+  Group& g = it->second;
+  if (g.symbolLen == 0) g.symbolLen = static_cast<int>(std::min<size_t>(len, kMaxSymbolLen));
+  g.packets[packetID] = padTo(packet, len, static_cast<size_t>(g.symbolLen));
+  g.present[packetID] = true;
+  g.received++;
+  metrics_.PacketsReceived++;
+  if (g.hasRedundancy && g.received < g.packetCount) return tryRecover(g);
+  return false;
+}
+
+std::pair<bool, std::vector<Recovered>> FECDecoder::AddRedundancyPacket(const uint8_t* b, size_t len) {
+  std::lock_guard<std::mutex> lk(mu_);
+  // parseRedundancyHeader, decoder.go:72-85
+  if (len < 11 || b[0] != 0xFE || b[1] != 0xC0) return {false, {}};
+  uint64_t groupID = 0;
+  for (int i = 0; i < 8; ++i) groupID |= uint64_t(b[2 + i]) << (8 * i);
+  const int packetCount = b[10];
+  if (packetCount <= 0 || packetCount > kMaxPacketCount) return {false, {}};
+  const uint8_t* payload = b + 11;
+  const size_t plen = len - 11;
+
+  if (groups_.find(groupID) == groups_.end() && groups_.size() >= kMaxActiveGroups) evictOldestGroup();
+  auto it = groups_.find(groupID);
+  if (it == groups_.end()) {
+    Group g;
+    g.groupID = groupID;
+    g.createdAt = std::chrono::steady_clock::now();
+    g.packetCount = packetCount;
+    it = groups_.emplace(groupID, std::move(g)).first;
+    metrics_.GroupsActive = static_cast<int64_t>(groups_.size());
+  }
+  Group& g = it->second;
+  if (g.packetCount != 0 && g.packetCount != packetCount) {  // conflicting counts: drop the group
+    groups_.erase(it);
+    metrics_.GroupsActive = static_cast<int64_t>(groups_.size());
+    return {false, {}};
+  }
+  g.packetCount = packetCount;
+  if (g.symbolLen == 0) g.symbolLen = static_cast<int>(std::min<size_t>(plen, kMaxSymbolLen));
+  g.redundancy = padTo(payload, plen, static_cast<size_t>(g.symbolLen));
+  g.hasRedundancy = true;
+  metrics_.RepairPacketsReceived++;
+  if (g.received < g.packetCount) {
+    if (tryRecover(g)) {
+      // decoder.go:170-178 lists ids still marked absent; tryRecover has just marked the
+      // rebuilt one present, so — as in the reference — the list comes back empty.
+      std::vector<Recovered> list;
+      for (uint64_t id = 0; id < static_cast<uint64_t>(g.packetCount); ++id) {
+        auto p = g.present.find(id);
+        if ((p == g.present.end() || !p->second) && g.packets.count(id)) list.push_back({id, g.packets[id]});
+      }
+      return {true, list};
+    }
+  }
+  return {false, {}};
+}
+
+bool FECDecoder::tryRecover(Group& g) {  // decoder.go:216-248
+  if (!g.hasRedundancy) return false;
+  if (g.received >= g.packetCount) return false;
+  const int missing = g.packetCount - g.received;
+  if (missing == 1) {
+    uint64_t id = 0;
+    Bytes data;
+    if (recoverSingle(g, &id, &data)) {
+      g.packets[id] = std::move(data);
+      g.present[id] = true;
+      g.received++;
+      metrics_.RecoveryEvents++;
+      metrics_.PacketsRecovered++;
+      return true;
+    }
+    metrics_.FailedRecoveries++;
+  } else {
+    metrics_.FailedRecoveries++;  // multiple losses: XOR recovers one
+  }
+  return false;
+}
+
+// decoder.go:255-287: out = parity ^ every other packet, on the GPU.
+bool FECDecoder::recoverSingle(Group& g, uint64_t* id, Bytes* out) {
+  if (!g.hasRedundancy || g.symbolLen == 0) return false;
+  bool found = false;
+  for (uint64_t i = 0; i < static_cast<uint64_t>(g.packetCount); ++i) {
+    auto p = g.present.find(i);
+    if (p == g.present.end() || !p->second) {
+      *id = i;
+      found = true;
+      break;
+    }
+  }
+  if (!found) return false;
+  std::vector<const uint8_t*> srcs;
+  srcs.push_back(g.redundancy.data());
+  for (auto& kv : g.packets)
+    if (kv.first != *id) srcs.push_back(kv.second.data());  // every stored symbol is symbolLen long
+  out->assign(static_cast<size_t>(g.symbolLen), 0);
+  xor_impl_fn xor_gpu = fec_select_xor_impl();
+  xor_gpu(srcs.data(), srcs.size(), static_cast<size_t>(g.symbolLen), out->data());
+  // the xor entry points clear the thread's error text on entry and set it on failure
+  const char* err = fec_hip_last_error();
+  return !(err && err[0]);
+}
+
+void FECDecoder::evictOldestGroup() {  // decoder.go:306-325
+  if (groups_.empty()) return;
+  auto oldest = groups_.begin();
+  for (auto it = groups_.begin(); it != groups_.end(); ++it)
+    if (it->second.createdAt < oldest->second.createdAt) oldest = it;
+  groups_.erase(oldest);
+  metrics_.GroupsEvicted++;
+  metrics_.GroupsActive = static_cast<int64_t>(groups_.size());
+}
+
+void FECDecoder::CleanupGroups() {  // decoder.go:328-343
+  std::lock_guard<std::mutex> lk(mu_);
+  const auto now = std::chrono::steady_clock::now();
+  for (auto it = groups_.begin(); it != groups_.end();) {
+    if (now - it->second.createdAt > std::chrono::seconds(kGroupTTLSeconds)) {
+      it = groups_.erase(it);
+      metrics_.GroupsEvicted++;
+    } else {
+      ++it;
+    }
+  }
+  metrics_.GroupsActive = static_cast<int64_t>(groups_.size());
+}
+
+FECDecoderMetrics FECDecoder::GetMetrics() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return metrics_;
+}
+
+void FECDecoder::ResetMetrics() {
+  std::lock_guard<std::mutex> lk(mu_);
+  metrics_ = FECDecoderMetrics();
+}
+
+Bytes FECDecoder::GetPacket(uint64_t groupID, uint64_t packetID) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto g = groups_.find(groupID);
+  if (g == groups_.end()) return {};
+  auto p = g->second.packets.find(packetID);
+  return p == g->second.packets.end() ? Bytes{} : p->second;
+}
+
+void FECDecoder::AgeGroupsForTest(int seconds) {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto& kv : groups_) kv.second.createdAt -= std::chrono::seconds(seconds);
+}
+
+// ===================================================================== batch extension
+namespace {
+
+FECEncoderCtx* shared_ctx() {
+  static std::once_flag once;
+  static FECEncoderCtx* ctx = nullptr;
+  std::call_once(once, [] { ctx = fec_encoder_new(0.10, 1024); });
+  return ctx;
+}
+
+}  // namespace
+
+Error EncodeBatchRS(const Bytes& data, int k, int r, int packetSize, Bytes* parity) {
+  FECEncoderCtx* ctx = shared_ctx();
+  if (!ctx) return errorf("no usable GPU: %s", fec_hip_last_error());
+  if (k <= 0 || r <= 0 || packetSize <= 0 || data.size() % (size_t(k) * packetSize) != 0)
+    return errorf("data is not a whole number of %dx%d groups", k, packetSize);
+  const uint64_t G = data.size() / (size_t(k) * packetSize);
+  parity->assign(G * r * size_t(packetSize), 0);
+  if (G == 0) return {};
+  const int rc = fec_encode_batch_rs(ctx, data.data(), nullptr, G, k, r, packetSize, parity->data());
+  if (rc != 0) return errorf("fec_encode_batch_rs failed with code %d: %s", rc, fec_hip_last_error());
+  return {};
+}
+
+int64_t RecoverBatchRS(Bytes& data, const Bytes& parity, const std::vector<uint64_t>& erasures, int k, int r,
+                       int packetSize, Error* err) {
+  FECEncoderCtx* ctx = shared_ctx();
+  if (!ctx) {
+    if (err) *err = errorf("no usable GPU: %s", fec_hip_last_error());
+    return -1;
+  }
+  const uint64_t G = erasures.size();
+  if (data.size() < G * k * size_t(packetSize) || parity.size() < G * r * size_t(packetSize)) {
+    if (err) *err = errorf("buffers too small for %llu groups", (unsigned long long)G);
+    return -1;
+  }
+  if (G == 0) return 0;
+  uint64_t bad = 0;
+  const int rc = fec_decode_batch_rs(ctx, data.data(), parity.data(), erasures.data(), G, k, r, packetSize,
+                                     nullptr, &bad);
+  if (rc != 0) {
+    if (err) *err = errorf("fec_decode_batch_rs failed with code %d: %s", rc, fec_hip_last_error());
+    return -1;
+  }
+  return static_cast<int64_t>(bad);
+}
+
+}  // namespace quicfec

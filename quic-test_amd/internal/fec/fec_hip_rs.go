@@ -1,0 +1,129 @@
+//go:build cgo && fec_hip
+
+// Batch GF(2^8) erasure coding on the GPU (include/fec_hip.h).  New API next to the
+// reference's FECEncoderCXX (fec_cgo.go:25-247), which keeps working unchanged on top of
+// the same library (its fec_encode_batch call, fec_cgo.go:138, now runs on the GPU).
+//
+// Status: written against the C-ABI in include/; not compiled here (no Go toolchain in
+// the build image).  The same calls are exercised from Python (quicfec) and C++
+// (quic-test_amd/host) by the test suite.
+
+package fec
+
+/*
+#include <stdint.h>
+#include <stdlib.h>
+#include "fec_hip.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"runtime"
+	"sync"
+	"unsafe"
+)
+
+// RSCodec encodes k data packets into r parity packets per group and rebuilds up to r
+// lost packets, for whole batches of groups per call.  Parity row 0 is the XOR repair
+// packet of FECEncoder/FECEncoderCXX byte for byte.
+type RSCodec struct {
+	ctx *C.FECEncoderCtx
+	k   int
+	r   int
+	mu  sync.Mutex
+}
+
+func hipError(what string, code C.int) error {
+	return fmt.Errorf("%s failed with code %d: %s", what, int(code), C.GoString(C.fec_hip_last_error()))
+}
+
+// NewRSCodec binds a codec to GPU `device` (use -1 for the current HIP device).
+func NewRSCodec(k, r, device int) (*RSCodec, error) {
+	if k <= 0 || r <= 0 || k+r > 256 {
+		return nil, fmt.Errorf("unsupported k=%d r=%d", k, r)
+	}
+	var ctx *C.FECEncoderCtx
+	if device < 0 {
+		ctx = C.fec_encoder_new(C.double(float64(r)/float64(k)), 1024)
+	} else {
+		ctx = C.fec_encoder_new_device(C.double(float64(r)/float64(k)), 1024, C.int(device))
+	}
+	if ctx == nil {
+		return nil, fmt.Errorf("no usable GPU: %s", C.GoString(C.fec_hip_last_error()))
+	}
+	c := &RSCodec{ctx: ctx, k: k, r: r}
+	runtime.SetFinalizer(c, (*RSCodec).Close)
+	return c, nil
+}
+
+// EncodeBatch: data holds groups*k packets of packetSize bytes (packet (g,j) at
+// (g*k+j)*packetSize); parity receives groups*r packets (row (g,i) at (g*r+i)*packetSize).
+func (c *RSCodec) EncodeBatch(data []byte, packetSize int, parity []byte) error {
+	if packetSize <= 0 || len(data)%(c.k*packetSize) != 0 {
+		return fmt.Errorf("data length %d is not a whole number of %dx%d groups", len(data), c.k, packetSize)
+	}
+	groups := len(data) / (c.k * packetSize)
+	if len(parity) < groups*c.r*packetSize {
+		return fmt.Errorf("parity buffer too small")
+	}
+	if groups == 0 {
+		return nil
+	}
+	c.mu.Lock()
+	defer c.mu.Unlock()
+	rc := C.fec_encode_batch_rs(c.ctx, (*C.uint8_t)(unsafe.Pointer(&data[0])), nil, C.uint64_t(groups),
+		C.uint32_t(c.k), C.uint32_t(c.r), C.uint32_t(packetSize), (*C.uint8_t)(unsafe.Pointer(&parity[0])))
+	runtime.KeepAlive(data)
+	runtime.KeepAlive(parity)
+	if rc != 0 {
+		return hipError("fec_encode_batch_rs", rc)
+	}
+	return nil
+}
+
+// DecodeBatch rebuilds lost data packets in place.  erasures[g] bit s set means shard s
+// of group g was lost (s < k data packet s, s >= k parity row s-k).  status[g] (optional,
+// len >= groups) is 0 when the group is complete afterwards, 1 when it had more losses
+// than surviving parity rows.  Returns the number of unrecoverable groups.
+func (c *RSCodec) DecodeBatch(data, parity []byte, erasures []uint64, packetSize int, status []byte) (int, error) {
+	groups := len(erasures)
+	if packetSize <= 0 || len(data) < groups*c.k*packetSize || len(parity) < groups*c.r*packetSize {
+		return 0, fmt.Errorf("buffers too small for %d groups", groups)
+	}
+	if status != nil && len(status) < groups {
+		return 0, fmt.Errorf("status buffer too small")
+	}
+	if groups == 0 {
+		return 0, nil
+	}
+	c.mu.Lock()
+	defer c.mu.Unlock()
+	var st *C.uint8_t
+	if status != nil {
+		st = (*C.uint8_t)(unsafe.Pointer(&status[0]))
+	}
+	var bad C.uint64_t
+	rc := C.fec_decode_batch_rs(c.ctx, (*C.uint8_t)(unsafe.Pointer(&data[0])), (*C.uint8_t)(unsafe.Pointer(&parity[0])),
+		(*C.uint64_t)(unsafe.Pointer(&erasures[0])), C.uint64_t(groups), C.uint32_t(c.k), C.uint32_t(c.r),
+		C.uint32_t(packetSize), st, &bad)
+	runtime.KeepAlive(data)
+	runtime.KeepAlive(parity)
+	runtime.KeepAlive(erasures)
+	runtime.KeepAlive(status)
+	if rc != 0 {
+		return 0, hipError("fec_decode_batch_rs", rc)
+	}
+	return int(bad), nil
+}
+
+// Close releases the GPU context.
+func (c *RSCodec) Close() error {
+	c.mu.Lock()
+	defer c.mu.Unlock()
+	if c.ctx != nil {
+		C.fec_encoder_free(c.ctx)
+		c.ctx = nil
+	}
+	return nil
+}

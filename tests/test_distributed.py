@@ -1,0 +1,67 @@
+"""Multi-process path of bench.py on CPU (gloo, world_size 2, 127.0.0.1).
+
+The FEC path shards by group with no data-path collective: each rank owns a contiguous
+slice of the global group stream, and only the elapsed time (MAX) and the group counts
+(SUM) are reduced.  This checks the sharding and the reductions exactly as bench.py runs
+them under torch.distributed.run."""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, str(REPO))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    import bench
+    G_total = 1_000_003
+    g0, g1 = bench.shard_range(G_total, rank, world)
+    elapsed = 0.5 + rank                      # rank 1 is the slow one
+    mx = bench.reduce_max(elapsed)
+    total = bench.reduce_sum(float(g1 - g0))
+    bench.barrier()
+    # the stream offset each rank would pass to fec_fill_random_dev
+    q.put((rank, g0, g1, mx, total, g0 * 10 * 1200))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_group_sharding_and_reductions(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    spans = [(g0, g1) for _, g0, g1, *_ in res]
+    assert spans[0][0] == 0 and spans[-1][1] == 1_000_003
+    assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))      # contiguous, disjoint
+    assert max(g1 - g0 for g0, g1 in spans) - min(g1 - g0 for g0, g1 in spans) <= 1
+    for _, g0, g1, mx, total, off in res:
+        assert mx == pytest.approx(0.5 + (world - 1))
+        assert total == pytest.approx(1_000_003)
+        assert off == g0 * 12000
+
+
+def test_shard_range_single():
+    sys.path.insert(0, str(REPO))
+    import bench
+    assert bench.shard_range(10, 0, 1) == (0, 10)
+    assert bench.shard_range(0, 0, 4) == (0, 0)
