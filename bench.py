@@ -41,6 +41,9 @@ CONFIGS = {
                  workload="C2 encode + C3 decode: k=10 r=3, 1200 B packets, 1M groups/GPU, 2 erasures/group"),
     "c4": dict(k=20, r=5, P=1200, groups=1_000_000, erasures=0, decode=False,
                workload="C4 encode: k=20 r=5, 1200 B packets, 1M groups/GPU (8M over 8 GPUs)"),
+    # satellite profile: iid loss 0.01 per packet (internal/network_profiles.go:78)
+    "c5": dict(k=10, r=3, P=1200, groups=1_000_000, erasures=0, loss=0.01, decode=True,
+               workload="C5 encode + decode, satellite loss (iid p=0.01 per shard): k=10 r=3, 1200 B, 1M groups/GPU"),
 }
 
 
@@ -93,6 +96,44 @@ def erasure_masks(G: int, n_shards: int, erasures: int, seed: int):
     return out
 
 
+def iid_masks(G: int, n_shards: int, p: float, seed: int):
+    """Every shard lost independently with probability p (network_profiles.go:73-82)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    out = np.zeros(G, dtype=np.uint64)
+    chunk = 1 << 18
+    w = np.left_shift(np.uint64(1), np.arange(n_shards, dtype=np.uint64))
+    for c0 in range(0, G, chunk):
+        c1 = min(G, c0 + chunk)
+        lost = rng.random((c1 - c0, n_shards)) < p
+        out[c0:c1] = (lost * w).sum(axis=1, dtype=np.uint64)
+    return out
+
+
+def make_masks(cfg: dict, G: int, seed: int):
+    if cfg.get("loss"):
+        return iid_masks(G, cfg["k"] + cfg["r"], cfg["loss"], seed)
+    return erasure_masks(G, cfg["k"] + cfg["r"], cfg["erasures"], seed)
+
+
+def unrecoverable_count(masks, k: int, r: int) -> int:
+    """Groups with more lost data shards than surviving parity rows."""
+    import numpy as np
+    e = _popcount(masks & np.uint64((1 << k) - 1))
+    lost_par = _popcount((masks >> np.uint64(k)) & np.uint64((1 << r) - 1))
+    return int(((e > 0) & (e > r - lost_par)).sum())
+
+
+def _popcount(x):
+    import numpy as np
+    c = np.zeros(len(x), dtype=np.int64)
+    y = x.copy()
+    while y.any():
+        c += (y & np.uint64(1)).astype(np.int64)
+        y >>= np.uint64(1)
+    return c
+
+
 def decode_algorithmic_bytes(masks, k: int, r: int, P: int) -> int:
     """Sum over groups with lost data shards of (k + e) * P (read k survivors, write e)."""
     import numpy as np
@@ -122,7 +163,7 @@ def cpu_baseline(cfg: dict, seconds: float = 8.0) -> dict:
     threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
     G = 20_000
     data = oracle.splitmix_bytes(G * k * P, SEED + 2)
-    masks = erasure_masks(G, k + r, cfg["erasures"], SEED + 3) if cfg["decode"] else None
+    masks = make_masks(cfg, G, SEED + 3) if cfg["decode"] else None
     done, t_total = 0, 0.0
     while t_total < seconds and done < 2_000_000:
         t0 = time.perf_counter()
@@ -247,6 +288,8 @@ def main() -> int:
     ap.add_argument("--config", default="c2c3", choices=sorted(CONFIGS))
     ap.add_argument("--groups", type=int, default=0, help="groups per GPU (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--loss", type=float, default=None,
+                    help="iid per-shard loss probability (c5; 0.05 = mobile profile)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-resident path (pinned buffers, H2D -> kernel -> D2H)")
@@ -264,6 +307,10 @@ def main() -> int:
         dist.init_process_group(backend="nccl", init_method="env://")
     torch.cuda.set_device(local)
     cfg = dict(CONFIGS[args.config])
+    if args.loss is not None:
+        cfg["loss"] = args.loss
+        cfg["decode"] = True
+        cfg["workload"] += f" (loss override p={args.loss})"
     k, r, P = cfg["k"], cfg["r"], cfg["P"]
     G = args.groups or cfg["groups"]
     g0, _ = shard_range(G * world, rank, world)
@@ -278,7 +325,7 @@ def main() -> int:
     ctx.fill_random_dev(data, data.numel(), SEED + 2, byte_offset=g0 * k * P, stream=sp)
     dec_bytes = 0
     if cfg["decode"]:
-        masks_h = erasure_masks(G, k + r, cfg["erasures"], SEED + 3 + rank)
+        masks_h = make_masks(cfg, G, SEED + 3 + rank)
         dec_bytes = decode_algorithmic_bytes(masks_h, k, r, P)
         masks = torch.from_numpy(masks_h.view(np.int64)).to("cuda")
         ctx.decode_prepare(k, r)
@@ -298,7 +345,13 @@ def main() -> int:
             st = torch.zeros(G, dtype=torch.uint8, device="cuda")
             ctx.decode_dev(data, parity, masks, G, k, r, P, st, stream=sp)
             torch.cuda.synchronize()
-            verified = bool(torch.equal(data, orig)) and int(st.sum().item()) == 0
+            bad_exp = unrecoverable_count(masks_h, k, r)
+            n_bad = int(st.sum().item())
+            if n_bad == 0:
+                verified = bool(torch.equal(data, orig)) and bad_exp == 0
+            else:
+                ok_rows = st == 0
+                verified = bool(torch.equal(data.view(G, -1)[ok_rows], orig.view(G, -1)[ok_rows])) and n_bad == bad_exp
         else:
             torch.cuda.synchronize()
             verified = True
@@ -372,7 +425,8 @@ def main() -> int:
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (counter-based splitmix64 bytes generated in HBM; seeded erasure masks)",
             "config": {"workload": cfg["workload"], "k": k, "r": r, "packet_bytes": P,
-                       "groups_per_gpu": G, "erasures_per_group": cfg["erasures"],
+                       "groups_per_gpu": G, "erasures_per_group": cfg["erasures"] or None,
+                       "iid_loss": cfg.get("loss"),
                        "parallelism": f"group-sharded x{world} (no collective)"},
             "verified": verified,
             "kernels": kernels,
