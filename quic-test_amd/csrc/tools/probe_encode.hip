@@ -152,6 +152,69 @@ __global__ __launch_bounds__(320) void enc_lds(const uint8_t* __restrict__ data,
   for (int i = 0; i < R; ++i) st16<POL>(parity + (g * R + i) * P + col * 16u, acc[i]);
 }
 
+// Persistent, software-pipelined LDS staging: workgroup = 320 lanes, tile = 4 groups
+// (48000 B, 128-B aligned).  Tile t+1 is loaded with aligned, fully coalesced 16-B pieces
+// into registers while tile t is computed from LDS; then registers -> LDS.
+template <int POL>
+__global__ __launch_bounds__(320) void enc_lds2(const uint8_t* __restrict__ data, uint8_t* __restrict__ parity,
+                                                uint32_t groups, const Tab* __restrict__ tabs) {
+  constexpr int K = 10, R = 3, P = 1200, CPP = 75, T = 4, TILE = T * K * P, NT = 320;
+  constexpr int QN = (TILE / 16 + NT - 1) / NT;  // 10 pieces per lane (last round partial)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[TILE];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t ntiles = (groups + T - 1) / T;
+  uint32_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  auto pieces_of = [&](uint32_t t) -> uint32_t {
+    const uint32_t g0 = t * T;
+    const uint32_t gn = (groups - g0 < uint32_t(T)) ? groups - g0 : uint32_t(T);
+    return gn * (K * P / 16);
+  };
+  // Piece indices are clamped to the tile's last piece: surplus lanes load and store that
+  // piece again (same bytes, same LDS address), so no lane needs a branch.
+  u32x4 reg[QN];
+  {
+    const uint8_t* src = data + uint64_t(tile) * TILE;
+    const uint32_t last = pieces_of(tile) - 1;
+#pragma unroll
+    for (int q = 0; q < QN; ++q) reg[q] = ld16<0>(src + min(q * NT + tid, last) * 16u);
+  }
+  const uint32_t gl = tid / CPP, col = tid - gl * CPP;
+  for (; tile < ntiles; tile += gridDim.x) {
+    const uint32_t last = pieces_of(tile) - 1;
+#pragma unroll
+    for (int q = 0; q < QN; ++q) *reinterpret_cast<u32x4*>(lds + min(q * NT + tid, last) * 16u) = reg[q];
+    __syncthreads();
+    const uint32_t next = tile + gridDim.x;
+    if (next < ntiles) {
+      const uint8_t* src = data + uint64_t(next) * TILE;
+      const uint32_t nl = pieces_of(next) - 1;
+#pragma unroll
+      for (int q = 0; q < QN; ++q) reg[q] = ld16<0>(src + min(q * NT + tid, nl) * 16u);
+    }
+    const uint64_t g = uint64_t(tile) * T + gl;
+    if (tid < uint32_t(T * CPP) && g < groups) {
+      const uint8_t* s = lds + gl * (K * P) + col * 16u;
+      u32x4 acc[R];
+      const u32x4 d0 = *reinterpret_cast<const u32x4*>(s);
+#pragma unroll
+      for (int i = 0; i < R; ++i) acc[i] = d0;
+#pragma unroll
+      for (int j = 1; j < K; ++j) {
+        const u32x4 dj = *reinterpret_cast<const u32x4*>(s + j * P);
+        Sel sl;
+        prep(dj, sl);
+        acc[0] ^= dj;
+#pragma unroll
+        for (int i = 1; i < R; ++i) mac(acc[i], sl, tabs[(i - 1) * K + j]);
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) st16<POL>(parity + (g * R + i) * P + col * 16u, acc[i]);
+    }
+    __syncthreads();
+  }
+}
+
 // Pure reads: NR aligned 1 KiB wave rows per lane, one-shot grid; a store only on a
 // practically impossible value keeps the loads alive.
 template <int NR>
@@ -308,6 +371,13 @@ int main(int argc, char** argv) {
   vars.push_back({"enc_pair<T=" #T ",pol" #POL ">", enc_bytes, [&] {                                  \
                     enc_pair<T, POL><<<uint32_t((G + T - 1) / T), ((2 * T * 75 + 63) / 64) * 64>>>(data, par, uint32_t(G), dtab); \
                   }, {}});
+  for (int per_cu : {1, 2, 3}) {
+    const uint32_t ntl = uint32_t((G + 3) / 4);
+    const uint32_t grid = std::min<uint32_t>(ntl, 256u * per_cu);
+    vars.push_back({"enc_lds2 nt x" + std::to_string(per_cu), enc_bytes, [=] {
+                      enc_lds2<2><<<grid, 320>>>(data, par, uint32_t(G), dtab);
+                    }, {}});
+  }
   {
     EncodeLaunch el;
     el.data = data;
