@@ -284,9 +284,9 @@ __device__ __forceinline__ void stw(uint8_t* p, const uint32_t (&v)[NW]) {
 // packet, NW dwords per lane.  The record (survivors, tables) is wave-uniform: SGPRs.
 template <int K, int MAXE, int POL, int NW>
 __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, const Tab* __restrict__ tabs,
-                                             uint8_t* __restrict__ dg, const uint8_t* __restrict__ pg,
-                                             uint32_t k, uint32_t P, uint32_t off, uint32_t e, uint32_t m0,
-                                             bool xor_only) {
+                                             const uint8_t* __restrict__ dg, const uint8_t* __restrict__ pg,
+                                             uint8_t* __restrict__ og, uint32_t k, uint32_t P, uint32_t off,
+                                             uint32_t e, uint32_t m0, bool xor_only) {
   if (xor_only) {  // single data loss rebuilt from parity row 0: the reference XOR
     uint32_t acc[NW] = {};
     for (uint32_t s = 0; s < k; ++s) {
@@ -297,7 +297,7 @@ __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, co
 #pragma unroll
       for (int q = 0; q < NW; ++q) acc[q] ^= v[q];
     }
-    stw<NW, POL>(dg + rec_byte(rw, 64) * static_cast<uint64_t>(P) + off, acc);
+    stw<NW, POL>(og + rec_byte(rw, 64) * static_cast<uint64_t>(P) + off, acc);
     return;
   }
   uint32_t acc[MAXE][NW];
@@ -355,7 +355,7 @@ __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, co
   for (int m = 0; m < MAXE; ++m) {
     if (m0 + m < e) {
       const uint32_t eid = rec_byte(rw, 64 + m0 + m);
-      stw<NW, POL>(dg + eid * static_cast<uint64_t>(P) + off, acc[m]);
+      stw<NW, POL>(og + eid * static_cast<uint64_t>(P) + off, acc[m]);
     }
   }
 }
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256) void decode_wave(uint8_t* __restrict__ data,
                                                    const uint32_t* __restrict__ rec_off,
                                                    const uint8_t* __restrict__ codebook,
                                                    uint64_t groups, uint32_t P, uint32_t k_rt, uint32_t r,
-                                                   uint32_t m0) {
+                                                   uint32_t m0, uint8_t* __restrict__ out) {
   const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * 4u +
                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   if (gw >= groups) return;
@@ -384,14 +384,15 @@ __global__ __launch_bounds__(256) void decode_wave(uint8_t* __restrict__ data,
   const bool xor_only = ((rw[24] >> 8) & 0xFFu) != 0;
   if (m0 >= e) return;
   const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
-  uint8_t* dg = data + gw * k * static_cast<uint64_t>(P);
+  const uint8_t* dg = data + gw * k * static_cast<uint64_t>(P);
   const uint8_t* pg = parity + gw * r * static_cast<uint64_t>(P);
+  uint8_t* og = out + gw * k * static_cast<uint64_t>(P);
   const uint32_t main_end = P & ~1023u;
   for (uint32_t base = 0; base < main_end; base += 1024u)
-    decode_piece<K, MAXE, POL, 4>(rw, tabs, dg, pg, k, P, base + lane * 16u, e, m0, xor_only);
+    decode_piece<K, MAXE, POL, 4>(rw, tabs, dg, pg, og, k, P, base + lane * 16u, e, m0, xor_only);
   for (uint32_t base = main_end; base < P; base += 256u) {
     const uint32_t off = base + lane * 4u;
-    if (off < P) decode_piece<K, MAXE, POL, 1>(rw, tabs, dg, pg, k, P, off, e, m0, xor_only);
+    if (off < P) decode_piece<K, MAXE, POL, 1>(rw, tabs, dg, pg, og, k, P, off, e, m0, xor_only);
   }
 }
 
@@ -546,12 +547,12 @@ __global__ __launch_bounds__(512) void decode_tiled(uint8_t* __restrict__ data,
 }
 
 // Decode, one lane per byte (any size / alignment).
-__global__ __launch_bounds__(256) void decode_bytes(uint8_t* __restrict__ data,
+__global__ __launch_bounds__(256) void decode_bytes(const uint8_t* __restrict__ data,
                                                     const uint8_t* __restrict__ parity,
                                                     const uint32_t* __restrict__ rec_off,
                                                     const uint8_t* __restrict__ codebook,
                                                     uint64_t g_first, uint32_t nthreads, uint32_t P,
-                                                    uint32_t k, uint32_t r) {
+                                                    uint32_t k, uint32_t r, uint8_t* __restrict__ out) {
   const uint32_t t = blockIdx.x * 256u + threadIdx.x;
   if (t >= nthreads) return;
   const uint32_t gl = t / P;
@@ -562,7 +563,7 @@ __global__ __launch_bounds__(256) void decode_bytes(uint8_t* __restrict__ data,
   const uint8_t* recp = codebook + static_cast<uint64_t>(rec) * 32u;
   const uint32_t e = recp[96];
   const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
-  uint8_t* dg = data + g * k * static_cast<uint64_t>(P);
+  const uint8_t* dg = data + g * k * static_cast<uint64_t>(P);
   const uint8_t* pg = parity + g * r * static_cast<uint64_t>(P);
   for (uint32_t m = 0; m < e; ++m) {
     uint32_t acc = 0;
@@ -572,7 +573,7 @@ __global__ __launch_bounds__(256) void decode_bytes(uint8_t* __restrict__ data,
       acc ^= gmul_byte(x, tabs[m * k + s]);
     }
     // Erased shards are never survivors, so writing here cannot feed a later read.
-    dg[recp[64 + m] * static_cast<uint64_t>(P) + b] = static_cast<uint8_t>(acc);
+    out[(g * k + recp[64 + m]) * static_cast<uint64_t>(P) + b] = static_cast<uint8_t>(acc);
   }
 }
 
@@ -766,7 +767,7 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
       hipLaunchKernelGGL((decode_wave<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(256), 0, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                          a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
-                         a.k, a.r, m0);
+                         a.k, a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P));
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
@@ -810,14 +811,15 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
       const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
       const uint32_t n = static_cast<uint32_t>(gn * a.P);
       hipLaunchKernelGGL(decode_bytes, dim3(blocks_for(n)), dim3(256), 0, s, a.data, a.parity,
-                         a.rec_off, a.codebook, g0, n, a.P, a.k, a.r);
+                         a.rec_off, a.codebook, g0, n, a.P, a.k, a.r, a.out ? a.out : a.data);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
   }
   const uint32_t tile = pick_tile(a.P / 16u, a.k, a.P);
-  if (tile > 0 && (a.variant == kDecodeTiledPlain || a.variant == kDecodeTiledNt)) {
+  const bool separate_out = a.out != nullptr && a.out != a.data;  // only decode_wave supports it
+  if (!separate_out && tile > 0 && (a.variant == kDecodeTiledPlain || a.variant == kDecodeTiledNt)) {
     const bool nt = a.variant == kDecodeTiledNt;
 #define QFEC_TILED(KK, RR)                                                                   \
   if (a.k == KK && a.r == RR)                                                                \
@@ -828,14 +830,14 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     QFEC_TILED(4, 2)
 #undef QFEC_TILED
   }
-  if (a.variant == kDecodeWaveNoBranch) {
+  if (a.variant == kDecodeWaveNoBranch && !separate_out) {
 #define QFEC_WAVE_NB(KK, RR) \
   if (a.k == KK && a.r == RR) return run_decode_wave<KK, RR, kNtStore | kNoCoefBranch>(a, s);
     QFEC_WAVE_NB(10, 3)
     QFEC_WAVE_NB(20, 5)
 #undef QFEC_WAVE_NB
   }
-  if (a.variant != kDecodeWavePerGroup) {
+  if (a.variant != kDecodeWavePerGroup || separate_out) {
     const bool nt = a.variant != kDecodeWavePlain;
 #define QFEC_WAVE(KK, RR)                                                                    \
   if (a.k == KK && a.r == RR)                                                                \

@@ -39,6 +39,9 @@ constexpr int kDecodeWaveNoBranch = 6;   //   same, no branch on coefficient 0 /
 
 struct DecodeLaunch {
   int variant = kDecodeAuto;
+  // Where rebuilt shards are stored, same layout as `data`; nullptr = in place in `data`.
+  // May be a device-visible pointer to page-locked host memory (zero-copy writes).
+  uint8_t* out = nullptr;
   uint8_t* data;
   const uint8_t* parity;
   const uint64_t* masks;

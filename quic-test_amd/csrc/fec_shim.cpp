@@ -293,7 +293,8 @@ int encode_dev_locked(FECEncoderCtx* ctx, const uint8_t* d_data, const void* d_o
 
 int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
                       const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
-                      uint8_t* d_status, bool vec16, hipStream_t s, DevBuf* rec = nullptr) {
+                      uint8_t* d_status, bool vec16, hipStream_t s, DevBuf* rec = nullptr,
+                      uint8_t* d_out = nullptr) {
   DecodePlan* plan = nullptr;
   int rc = get_decode_plan(ctx, k, r, &plan);
   if (rc != FEC_OK) return rc;
@@ -304,6 +305,7 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   a.parity = d_parity;
   a.masks = d_masks;
   a.rec_off = ws.as<uint32_t>();
+  a.out = d_out;
   a.status = d_status;
   a.codebook = plan->codebook.as<uint8_t>();
   a.binom = ctx->d_binom.as<uint64_t>();
@@ -372,6 +374,17 @@ int decode_host_pipelined(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
     QFEC_HIP(p.status.ensure(cg));
   }
   const bool vec16 = (P % 16u) == 0;
+  // Page-locked data: the kernel stores the rebuilt shards straight into host memory
+  // (zero-copy PCIe writes of ~e*P bytes per group) instead of a D2H of the whole chunk.
+  uint8_t* host_dev = nullptr;
+  if (classify_ptr(data) == Mem::kPinned) {
+    hipPointerAttribute_t attr;
+    std::memset(&attr, 0, sizeof(attr));
+    if (hipPointerGetAttributes(&attr, data) == hipSuccess && attr.devicePointer)
+      host_dev = static_cast<uint8_t*>(attr.devicePointer);
+    else
+      (void)hipGetLastError();
+  }
   uint64_t c = 0;
   for (uint64_t g0 = 0; g0 < G; g0 += cg, ++c) {
     PipeSlot& sl = ctx->pipe[c % kPipeSlots];
@@ -380,9 +393,10 @@ int decode_host_pipelined(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
     QFEC_HIP(hipMemcpyAsync(sl.par.ptr, parity + g0 * par_g, n * par_g, hipMemcpyHostToDevice, sl.s));
     QFEC_HIP(hipMemcpyAsync(sl.mask.ptr, masks + g0, n * 8, hipMemcpyHostToDevice, sl.s));
     rc = decode_dev_locked(ctx, sl.in.as<uint8_t>(), sl.par.as<uint8_t>(), sl.mask.as<uint64_t>(), n, k, r, P,
-                           sl.status.as<uint8_t>(), vec16, sl.s, &sl.rec);
+                           sl.status.as<uint8_t>(), vec16, sl.s, &sl.rec, host_dev ? host_dev + g0 * in_g : nullptr);
     if (rc != FEC_OK) return rc;
-    QFEC_HIP(hipMemcpyAsync(data + g0 * in_g, sl.in.ptr, n * in_g, hipMemcpyDeviceToHost, sl.s));
+    if (!host_dev)
+      QFEC_HIP(hipMemcpyAsync(data + g0 * in_g, sl.in.ptr, n * in_g, hipMemcpyDeviceToHost, sl.s));
     QFEC_HIP(hipMemcpyAsync(status_out + g0, sl.status.ptr, n, hipMemcpyDeviceToHost, sl.s));
   }
   for (auto& p : ctx->pipe) QFEC_HIP(hipStreamSynchronize(p.s));
