@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "fec_kernels.hpp"
 
@@ -116,7 +117,12 @@ __global__ __launch_bounds__(512) void encode_v16(const uint8_t* __restrict__ da
                                                   uint32_t nthreads, uint32_t cpp, uint32_t P,
                                                   uint32_t k_rt, uint32_t r_total, uint32_t row0,
                                                   const Tab* __restrict__ tabs, uint32_t tile,
-                                                  uint64_t groups) {
+                                                  uint64_t groups, uint32_t never) {
+  // Dynamic LDS is only an occupancy cap (occupancy_cap_lds).  It is declared and
+  // referenced so that every HIP runtime honours the launch's dynamic LDS size; `never`
+  // is always 0.
+  extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];
+  if (never) occupancy_lds[threadIdx.x] = 0;
   uint32_t gl, col;
   if (tile > 0) {
     const uint32_t lane = threadIdx.x;
@@ -370,7 +376,9 @@ __global__ __launch_bounds__(256) void decode_wave(uint8_t* __restrict__ data,
                                                    const uint32_t* __restrict__ rec_off,
                                                    const uint8_t* __restrict__ codebook,
                                                    uint64_t groups, uint32_t P, uint32_t k_rt, uint32_t r,
-                                                   uint32_t m0, uint8_t* __restrict__ out) {
+                                                   uint32_t m0, uint8_t* __restrict__ out, uint32_t never) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];  // see encode_v16
+  if (never) occupancy_lds[threadIdx.x] = 0;
   const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * 4u +
                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   if (gw >= groups) return;
@@ -618,6 +626,12 @@ inline uint32_t blocks_for(uint64_t n) { return static_cast<uint32_t>((n + 255) 
 // ---------------------------------------------------------------------------------
 namespace {
 
+// Tuning override of an occupancy cap from the environment (-1 = none), else `def`.
+int env_waves(const char* name, int def) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : def;
+}
+
 // Groups per workgroup for the tiled mapping: the fewest idle lanes (workgroup = whole
 // waves), preferring tiles whose byte size is a multiple of 128 (tile starts stay
 // cache-line aligned).  0 = use the flat mapping (columns per packet > 512).
@@ -651,13 +665,14 @@ hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
     if (tile > 0) {
       const uint32_t bs = (tile * cpp + 63) / 64 * 64;
       const uint32_t blocks = static_cast<uint32_t>((gn + tile - 1) / tile);
-      hipLaunchKernelGGL((encode_v16<K, R, OFF, FIRST, POL>), dim3(blocks), dim3(bs), 0, s, a.data,
+      const uint32_t smem = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_ENCODE_WAVES", kEncodeWavesPerCU), bs / 64);
+      hipLaunchKernelGGL((encode_v16<K, R, OFF, FIRST, POL>), dim3(blocks), dim3(bs), smem, s, a.data,
                          a.offsets, a.parity, g0, n, cpp, a.P, a.k, a.r, row0,
-                         static_cast<const Tab*>(a.tables), tile, gn);
+                         static_cast<const Tab*>(a.tables), tile, gn, 0u);
     } else {
       hipLaunchKernelGGL((encode_v16<K, R, OFF, FIRST, POL>), dim3(blocks_for(n)), dim3(256), 0, s, a.data,
                          a.offsets, a.parity, g0, n, cpp, a.P, a.k, a.r, row0,
-                         static_cast<const Tab*>(a.tables), 0u, gn);
+                         static_cast<const Tab*>(a.tables), 0u, gn, 0u);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -757,6 +772,7 @@ hipError_t run_decode_v16(const DecodeLaunch& a, hipStream_t s) {
 template <int K, int MAXE, int POL>
 hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
   const uint32_t passes = (a.r + MAXE - 1) / MAXE;  // e <= r
+  const uint32_t smem = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_DECODE_WAVES", kDecodeWavesPerCU), 4);
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t m0 = p * MAXE;
     const uint64_t blocks = (a.groups + 3) / 4;
@@ -764,10 +780,10 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
       const uint64_t bn = (blocks - b0 < (1u << 24)) ? blocks - b0 : (1u << 24);
       const uint64_t g0 = b0 * 4;
       const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
-      hipLaunchKernelGGL((decode_wave<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(256), 0, s,
+      hipLaunchKernelGGL((decode_wave<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                          a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
-                         a.k, a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P));
+                         a.k, a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }

@@ -20,7 +20,24 @@ struct EncodeLaunch {
   uint32_t k, r, P;
   const void* tables;        // (r-1) x k CoefEntry (rows 1..r-1), device
   bool vec16;                // P % 16 == 0 and every packet 16-byte aligned
+  int waves_per_cu = 0;      // occupancy cap of the streaming kernel (0 = tuned default)
 };
+
+// Tuned occupancy caps (waves per CU) of the streaming kernels: fewer concurrent waves
+// than the hardware allows keep the HBM request stream more local and measured faster
+// (tools/probe_encode.hip, tools/probe_decode.hip).
+constexpr int kEncodeWavesPerCU = 10;  // 2 workgroups of 5 waves; measured 5.70 vs 5.26 TB/s uncapped
+constexpr int kDecodeWavesPerCU = 0;   // measured: any cap below ~20 waves/CU is slower
+
+// Dynamic LDS bytes that cap a workgroup of `waves_per_block` waves at about
+// `waves_per_cu` waves per CU (160 KiB LDS per CU); 0 = no cap.
+inline uint32_t occupancy_cap_lds(int waves_per_cu, uint32_t waves_per_block) {
+  if (waves_per_cu <= 0 || waves_per_block == 0) return 0;
+  uint32_t blocks = static_cast<uint32_t>(waves_per_cu) / waves_per_block;
+  if (blocks == 0) blocks = 1;
+  if (blocks * waves_per_block >= 32) return 0;
+  return 160u * 1024u / (blocks + 1) + 16u;
+}
 
 struct LevelMeta {           // codebook levels e = 1..32 (see gf256.hpp)
   uint64_t base[33];
@@ -53,6 +70,7 @@ struct DecodeLaunch {
   uint64_t groups;
   uint32_t k, r, P;
   bool vec16;
+  int waves_per_cu = 0;      // occupancy cap of the decode kernel (0 = tuned default)
 };
 
 hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s);

@@ -107,15 +107,19 @@ int main(int argc, char** argv) {
   struct Var {
     std::string name;
     int variant;
+    int waves;
     std::vector<float> ms;
   };
-  std::vector<Var> vars = {{"wave-per-group v16", kDecodeWavePerGroup, {}},
-                           {"tiled nt-store", kDecodeTiledNt, {}},
-                           {"wave 16B+4B plain", kDecodeWavePlain, {}},
-                           {"wave 16B+4B nt", kDecodeWaveNt, {}},
-                           {"wave nt no-branch", kDecodeWaveNoBranch, {}}};
+  std::vector<Var> vars = {{"wave-per-group v16", kDecodeWavePerGroup, -1, {}},
+                           {"wave nt uncapped", kDecodeWaveNt, -1, {}},
+                           {"wave nt cap 8", kDecodeWaveNt, 8, {}},
+                           {"wave nt cap 12", kDecodeWaveNt, 12, {}},
+                           {"wave nt cap 16", kDecodeWaveNt, 16, {}},
+                           {"wave nt cap 20", kDecodeWaveNt, 20, {}},
+                           {"wave nt cap 24", kDecodeWaveNt, 24, {}}};
   for (auto& v : vars) {
     dl.variant = v.variant;
+    dl.waves_per_cu = v.waves;
     poison<<<uint32_t((nd + 255) / 256), 256>>>(data, masks, G, k, P);
     CK(launch_decode(dl, nullptr));
     CK(hipDeviceSynchronize());
@@ -130,6 +134,7 @@ int main(int argc, char** argv) {
   for (int rd = 0; rd < rounds; ++rd)
     for (auto& v : vars) {
       dl.variant = v.variant;
+      dl.waves_per_cu = v.waves;
       CK(hipEventRecord(e0));
       CK(launch_decode(dl, nullptr));
       CK(hipEventRecord(e1));

@@ -111,6 +111,39 @@ __global__ __launch_bounds__(((T * 75 + 63) / 64) * 64) void enc_blk(const uint8
   for (int i = 0; i < R; ++i) st16<POL>(parity + (g * R + i) * P + col * 16u, acc[i]);
 }
 
+// enc_blk as a persistent grid: each workgroup walks tiles blockIdx.x, +gridDim.x, ...
+template <int T, int POL>
+__global__ __launch_bounds__(((T * 75 + 63) / 64) * 64) void enc_persist(const uint8_t* __restrict__ data,
+                                                                       uint8_t* __restrict__ parity, uint32_t groups,
+                                                                       const Tab* __restrict__ tabs) {
+  constexpr int K = 10, R = 3, P = 1200, CPP = 75;
+  const uint32_t lane = threadIdx.x;
+  if (lane >= T * CPP) return;
+  const uint32_t gl = lane / CPP, col = lane - gl * CPP;
+  const uint32_t ntiles = (groups + T - 1) / T;
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t g = uint64_t(tile) * T + gl;
+    if (g >= groups) break;
+    const uint8_t* src = data + g * K * P + col * 16u;
+    u32x4 d[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) d[j] = ld16<POL>(src + j * P);
+    u32x4 acc[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[i] = d[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+      Sel s;
+      prep(d[j], s);
+      acc[0] ^= d[j];
+#pragma unroll
+      for (int i = 1; i < R; ++i) mac(acc[i], s, tabs[(i - 1) * K + j]);
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) st16<POL>(parity + (g * R + i) * P + col * 16u, acc[i]);
+  }
+}
+
 // LDS-staged: block = 4 groups (48000 B, 128-B aligned tile).  Aligned 1 KiB wave-row loads
 // into LDS, barrier, each lane reads its column of the 10 packets from LDS.
 template <int POL>
@@ -341,7 +374,7 @@ int main(int argc, char** argv) {
   vars.push_back({"enc_mem<10,3> xor-only", enc_bytes, [&] { enc_mem<10, 3><<<blocks, 256>>>(data, par, nth, cpp, P); }, {}});
 #define ENC(POL)                                                                                          \
   vars.push_back({"encode_v16 POL=" #POL, enc_bytes, [&] {                                               \
-                    encode_v16<10, 3, 0, true, POL><<<blocks, 256>>>(data, nullptr, par, 0, nth, cpp, P, k, r, 0, dtab, 0u, G); \
+                    encode_v16<10, 3, 0, true, POL><<<blocks, 256>>>(data, nullptr, par, 0, nth, cpp, P, k, r, 0, dtab, 0u, G, 0u); \
                   }, {}});
   ENC(0)
   ENC(2)
@@ -371,7 +404,20 @@ int main(int argc, char** argv) {
   vars.push_back({"enc_pair<T=" #T ",pol" #POL ">", enc_bytes, [&] {                                  \
                     enc_pair<T, POL><<<uint32_t((G + T - 1) / T), ((2 * T * 75 + 63) / 64) * 64>>>(data, par, uint32_t(G), dtab); \
                   }, {}});
-  for (int per_cu : {1, 2, 3}) {
+  // occupancy caps on the production-shaped kernel via dynamic LDS: blocks per CU <= 160K / smem
+  for (int smem : {40 * 1024, 53 * 1024, 80 * 1024, 81 * 1024}) {
+    vars.push_back({"enc_blk<4> cap " + std::to_string(160 * 1024 / smem) + "/CU smem" + std::to_string(smem / 1024), enc_bytes, [=] {
+                      enc_blk<4, 2><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab);
+                    }, {}});
+  }
+  for (int per_cu : {2, 3, 4}) {
+    const uint32_t ntl = uint32_t((G + 3) / 4);
+    const uint32_t grid = std::min<uint32_t>(ntl, 256u * per_cu);
+    vars.push_back({"enc_persist x" + std::to_string(per_cu), enc_bytes, [=] {
+                      enc_persist<4, 2><<<grid, 320>>>(data, par, uint32_t(G), dtab);
+                    }, {}});
+  }
+  for (int per_cu : {1}) {
     const uint32_t ntl = uint32_t((G + 3) / 4);
     const uint32_t grid = std::min<uint32_t>(ntl, 256u * per_cu);
     vars.push_back({"enc_lds2 nt x" + std::to_string(per_cu), enc_bytes, [=] {
@@ -431,7 +477,7 @@ int main(int argc, char** argv) {
   // every encode variant must reproduce the production kernel's parity bytes
   {
     std::vector<uint8_t> ref(np), got(np);
-    encode_v16<10, 3, 0, true, 0><<<blocks, 256>>>(data, nullptr, par, 0, nth, cpp, P, k, r, 0, dtab, 0u, G);
+    encode_v16<10, 3, 0, true, 0><<<blocks, 256>>>(data, nullptr, par, 0, nth, cpp, P, k, r, 0, dtab, 0u, G, 0u);
     CK(hipMemcpy(ref.data(), par, np, hipMemcpyDeviceToHost));
     for (auto& v : vars) {
       if (v.name.rfind("enc", 0) != 0 || v.name.rfind("enc_mem", 0) == 0) continue;
