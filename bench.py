@@ -78,9 +78,13 @@ def reduce_sum(x: float) -> float:
 
 
 def barrier() -> None:
+    import torch
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
-        dist.barrier()
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
 
 
 def erasure_masks(G: int, n_shards: int, erasures: int, seed: int):
@@ -303,9 +307,12 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group(backend="nccl", init_method="env://")
+    # one process per GPU; bind the GPU before RCCL creates its communicator.  The modulo
+    # and the gloo override only exist to rehearse several ranks on a one-GPU box.
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group(backend=os.environ.get("QUICFEC_DIST_BACKEND", "nccl"), init_method="env://")
     cfg = dict(CONFIGS[args.config])
     if args.loss is not None:
         cfg["loss"] = args.loss
