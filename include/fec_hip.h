@@ -86,7 +86,10 @@ int fec_decode_batch_rs_dev(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* 
 
 /* Build (and upload) the decode codebook for (k, r) ahead of the first decode.  The
  * codebook holds the recovery tables of every recoverable erasure pattern; its size is
- * returned in *bytes_out (nullable).  0, FEC_ERR_RANGE if it would exceed the cap. */
+ * returned in *bytes_out (nullable).  When it would exceed the 2 GiB cap (e.g. k=16 r=16)
+ * decode instead builds records for the patterns present in each call ("sparse plan":
+ * masks are read back to the host and the call completes synchronously); *bytes_out is
+ * then 0.  FEC_ERR_RANGE if k + r > 64. */
 int fec_decode_prepare(FECEncoderCtx* ctx, uint32_t k, uint32_t r, uint64_t* bytes_out);
 
 /* ---- utilities for benchmarks and tests ---- */

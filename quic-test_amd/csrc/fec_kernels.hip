@@ -814,7 +814,7 @@ hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s)
 
 hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
   if (a.groups == 0) return hipSuccess;
-  for (uint64_t g0 = 0; g0 < a.groups; g0 += kMaxThreadsPerLaunch) {
+  for (uint64_t g0 = 0; !a.rec_ready && g0 < a.groups; g0 += kMaxThreadsPerLaunch) {
     const uint64_t gn = (a.groups - g0 < kMaxThreadsPerLaunch) ? a.groups - g0 : kMaxThreadsPerLaunch;
     hipLaunchKernelGGL(classify, dim3(blocks_for(gn)), dim3(256), 0, s, a.masks + g0, gn, a.k, a.r,
                        a.binom, a.meta, a.rec_off + g0, a.status ? a.status + g0 : nullptr);

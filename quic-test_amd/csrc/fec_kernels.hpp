@@ -71,6 +71,7 @@ struct DecodeLaunch {
   uint32_t k, r, P;
   bool vec16;
   int waves_per_cu = 0;      // occupancy cap of the decode kernel (0 = tuned default)
+  bool rec_ready = false;    // rec_off already filled by the host (sparse plan): no classify
 };
 
 hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s);

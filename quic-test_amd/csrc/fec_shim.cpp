@@ -104,8 +104,11 @@ struct EncodePlan {
 };
 
 struct DecodePlan {
+  bool dense = false;          // dense codebook of every pattern (else: sparse per call)
   qfec::CodebookLayout layout;
   DevBuf codebook;
+  std::vector<uint8_t> M;      // parity matrix, for sparse per-call records
+  DevBuf sparse_book;          // the last sparse call's records
 };
 
 constexpr uint64_t kCodebookCap = 2ull << 30;  // 2 GiB of recovery tables per (k, r)
@@ -239,19 +242,22 @@ int get_decode_plan(FECEncoderCtx* ctx, uint32_t k, uint32_t r, DecodePlan** out
   auto it = ctx->dec_plans.find(key);
   if (it == ctx->dec_plans.end()) {
     auto plan = std::make_unique<DecodePlan>();
-    if (!qfec::codebook_layout(k, r, kCodebookCap, plan->layout)) {
-      set_error("decode: unsupported k=%u r=%u (need k+r<=64 and a codebook <= %llu bytes)", k, r,
-                (unsigned long long)kCodebookCap);
+    if (k + r > qfec::kMaxDecodeShards || !qfec::parity_matrix(k, r, plan->M)) {
+      set_error("decode: unsupported k=%u r=%u (need k+r<=64)", k, r);
       return FEC_ERR_RANGE;
     }
-    std::vector<uint8_t> M, book;
-    qfec::parity_matrix(k, r, M);
-    if (!qfec::build_codebook(plan->layout, M, book)) {
-      set_error("decode: singular recovery submatrix for k=%u r=%u", k, r);
-      return FEC_ERR_RANGE;
+    // Dense codebook when it fits the cap; otherwise records are built per call for the
+    // patterns present (build_sparse_plan).
+    plan->dense = qfec::codebook_layout(k, r, kCodebookCap, plan->layout);
+    if (plan->dense) {
+      std::vector<uint8_t> book;
+      if (!qfec::build_codebook(plan->layout, plan->M, book)) {
+        set_error("decode: singular recovery submatrix for k=%u r=%u", k, r);
+        return FEC_ERR_RANGE;
+      }
+      QFEC_HIP(plan->codebook.ensure(book.size()));
+      QFEC_HIP(hipMemcpy(plan->codebook.ptr, book.data(), book.size(), hipMemcpyHostToDevice));
     }
-    QFEC_HIP(plan->codebook.ensure(book.size()));
-    QFEC_HIP(hipMemcpy(plan->codebook.ptr, book.data(), book.size(), hipMemcpyHostToDevice));
     if (!ctx->d_binom.ptr) {
       QFEC_HIP(ctx->d_binom.ensure(sizeof(qfec::binom().c)));
       QFEC_HIP(hipMemcpy(ctx->d_binom.ptr, qfec::binom().c, sizeof(qfec::binom().c),
@@ -308,6 +314,25 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   a.out = d_out;
   a.status = d_status;
   a.codebook = plan->codebook.as<uint8_t>();
+  if (!plan->dense) {
+    // Sparse plan: the masks come to the host (after the stream's earlier work), records
+    // are built for the patterns present, and the call completes synchronously.
+    std::vector<uint64_t> hm(G);
+    QFEC_HIP(hipStreamSynchronize(s));
+    QFEC_HIP(hipMemcpy(hm.data(), d_masks, G * 8, hipMemcpyDefault));
+    std::vector<uint8_t> book, st;
+    std::vector<uint32_t> ro;
+    if (!qfec::build_sparse_plan(k, r, plan->M, hm.data(), G, qfec::kRecNone, qfec::kRecBad, book, ro, st)) {
+      set_error("decode: sparse plan failed for k=%u r=%u", k, r);
+      return FEC_ERR_RANGE;
+    }
+    QFEC_HIP(plan->sparse_book.ensure(book.size() + 32));
+    if (!book.empty()) QFEC_HIP(hipMemcpy(plan->sparse_book.ptr, book.data(), book.size(), hipMemcpyHostToDevice));
+    QFEC_HIP(hipMemcpy(ws.ptr, ro.data(), G * 4, hipMemcpyHostToDevice));
+    if (d_status) QFEC_HIP(hipMemcpy(d_status, st.data(), G, hipMemcpyDefault));
+    a.codebook = plan->sparse_book.as<uint8_t>();
+    a.rec_ready = true;
+  }
   a.binom = ctx->d_binom.as<uint64_t>();
   std::memset(&a.meta, 0, sizeof(a.meta));
   for (uint32_t e = 1; e <= 32; ++e) {
@@ -321,6 +346,7 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   a.P = P;
   a.vec16 = vec16;
   QFEC_HIP(qfec::launch_decode(a, s));
+  if (!plan->dense) QFEC_HIP(hipStreamSynchronize(s));  // the sparse records are reused next call
   return FEC_OK;
 }
 
@@ -830,7 +856,7 @@ QFEC_EXPORT int fec_decode_prepare(FECEncoderCtx* ctx, uint32_t k, uint32_t r, u
   DecodePlan* plan = nullptr;
   rc = get_decode_plan(ctx, k, r, &plan);
   if (rc != FEC_OK) return rc;
-  if (bytes_out) *bytes_out = plan->layout.total_bytes;
+  if (bytes_out) *bytes_out = plan->dense ? plan->layout.total_bytes : 0;  // 0: sparse per-call plans
   return FEC_OK;
 }
 

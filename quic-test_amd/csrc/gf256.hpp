@@ -15,6 +15,8 @@
 
 #include <cstdint>
 #include <cstring>
+#include <map>
+#include <utility>
 #include <vector>
 
 namespace qfec {
@@ -216,56 +218,114 @@ inline void for_each_subset(uint32_t n, uint32_t e, F&& f) {
   }
 }
 
-// Fill `out` (L.total_bytes) with every record.  false on a singular submatrix (cannot
-// happen for this Cauchy construction; kept as a guard).
+inline uint64_t record_bytes(uint32_t k, uint32_t e) {
+  return kRecordHeader + uint64_t(e) * k * sizeof(CoefEntry);
+}
+
+// Write the record of pattern (E, R) (sorted, |E| = |R| = e) at `rec` (record_bytes(k, e)
+// bytes, zeroed by the caller).  false on a singular submatrix (cannot happen for this
+// Cauchy construction; kept as a guard).
+inline bool build_record(uint32_t k, const std::vector<uint8_t>& M, const uint32_t* E, const uint32_t* R,
+                         uint32_t e, uint8_t* rec) {
+  const GF256& g = gf();
+  // survivors: data not in E ascending, then parity rows R
+  uint32_t ns = 0;
+  uint32_t surv[kMaxDecodeShards];
+  for (uint32_t j = 0, t = 0; j < k; ++j) {
+    if (t < e && E[t] == j) {
+      ++t;
+      continue;
+    }
+    surv[ns++] = j;
+  }
+  for (uint32_t t = 0; t < e; ++t) surv[ns++] = k + R[t];
+  for (uint32_t s = 0; s < k; ++s) rec[s] = static_cast<uint8_t>(surv[s]);
+  for (uint32_t t = 0; t < e; ++t) rec[64 + t] = static_cast<uint8_t>(E[t]);
+  rec[96] = static_cast<uint8_t>(e);
+  std::vector<uint8_t> sub(size_t(e) * e, 0), inv;
+  for (uint32_t a = 0; a < e; ++a)
+    for (uint32_t b = 0; b < e; ++b) sub[a * e + b] = M[R[a] * k + E[b]];
+  if (!invert(sub, e, inv)) return false;
+  bool all_one = true;
+  CoefEntry* ent = reinterpret_cast<CoefEntry*>(rec + kRecordHeader);
+  for (uint32_t m = 0; m < e; ++m) {
+    for (uint32_t s = 0; s < k; ++s) {
+      uint8_t c = 0;
+      if (surv[s] < k) {
+        for (uint32_t t = 0; t < e; ++t) c ^= g.mul(inv[m * e + t], M[R[t] * k + surv[s]]);
+      } else {
+        c = inv[m * e + (s - (k - e))];
+      }
+      all_one &= (c == 1);
+      ent[m * k + s] = make_entry(c);
+    }
+  }
+  rec[97] = all_one ? 1 : 0;
+  return true;
+}
+
+// Fill `out` (L.total_bytes) with every record.
 inline bool build_codebook(const CodebookLayout& L, const std::vector<uint8_t>& M,
                            std::vector<uint8_t>& out) {
-  const GF256& g = gf();
   const uint32_t k = L.k, r = L.r;
   out.assign(L.total_bytes, 0);
   bool ok = true;
-  std::vector<uint8_t> sub, inv;
   for (uint32_t e = 1; e <= r && e <= k; ++e) {
     const uint64_t cr = binom().c[r][e];
     for_each_subset(k, e, [&](const uint32_t* E) {
       const uint64_t rankE = colex_rank(E, e);
       for_each_subset(r, e, [&](const uint32_t* R) {
         const uint64_t idx = rankE * cr + colex_rank(R, e);
-        uint8_t* rec = out.data() + L.level_base[e] + idx * L.level_stride[e];
-        // survivors: data not in E ascending, then parity rows R
-        uint32_t ns = 0;
-        uint32_t surv[kMaxDecodeShards];
-        for (uint32_t j = 0, t = 0; j < k; ++j) {
-          if (t < e && E[t] == j) { ++t; continue; }
-          surv[ns++] = j;
-        }
-        for (uint32_t t = 0; t < e; ++t) surv[ns++] = k + R[t];
-        for (uint32_t s = 0; s < k; ++s) rec[s] = static_cast<uint8_t>(surv[s]);
-        for (uint32_t t = 0; t < e; ++t) rec[64 + t] = static_cast<uint8_t>(E[t]);
-        rec[96] = static_cast<uint8_t>(e);
-        sub.assign(size_t(e) * e, 0);
-        for (uint32_t a = 0; a < e; ++a)
-          for (uint32_t b = 0; b < e; ++b) sub[a * e + b] = M[R[a] * k + E[b]];
-        if (!invert(sub, e, inv)) { ok = false; return; }
-        bool all_one = true;
-        CoefEntry* ent = reinterpret_cast<CoefEntry*>(rec + kRecordHeader);
-        for (uint32_t m = 0; m < e; ++m) {
-          for (uint32_t s = 0; s < k; ++s) {
-            uint8_t c = 0;
-            if (surv[s] < k) {
-              for (uint32_t t = 0; t < e; ++t) c ^= g.mul(inv[m * e + t], M[R[t] * k + surv[s]]);
-            } else {
-              c = inv[m * e + (s - (k - e))];
-            }
-            all_one &= (c == 1);
-            ent[m * k + s] = make_entry(c);
-          }
-        }
-        rec[97] = all_one ? 1 : 0;
+        ok &= build_record(k, M, E, R, e, out.data() + L.level_base[e] + idx * L.level_stride[e]);
       });
     });
   }
   return ok;
+}
+
+// Sparse plan: records only for the patterns present in one batch of masks (used when the
+// dense codebook would exceed its cap).  rec_off[g] = record offset / 32, or the kRec*
+// markers of fec_kernels.hpp (passed in as none / bad); status[g] = 1 if unrecoverable.
+inline bool build_sparse_plan(uint32_t k, uint32_t r, const std::vector<uint8_t>& M, const uint64_t* masks,
+                              uint64_t G, uint32_t rec_none, uint32_t rec_bad, std::vector<uint8_t>& book,
+                              std::vector<uint32_t>& rec_off, std::vector<uint8_t>& status) {
+  book.clear();
+  rec_off.assign(G, rec_none);
+  status.assign(G, 0);
+  const uint64_t kmask = k >= 64 ? ~0ull : ((1ull << k) - 1);
+  const uint64_t rmask = r >= 64 ? ~0ull : ((1ull << r) - 1);
+  std::map<std::pair<uint64_t, uint64_t>, uint32_t> seen;
+  for (uint64_t g = 0; g < G; ++g) {
+    const uint64_t dm = masks[g] & kmask;
+    if (!dm) continue;
+    const uint64_t pm = k >= 64 ? 0 : (masks[g] >> k) & rmask;
+    const uint32_t e = static_cast<uint32_t>(__builtin_popcountll(dm));
+    if (e > r - static_cast<uint32_t>(__builtin_popcountll(pm))) {
+      rec_off[g] = rec_bad;
+      status[g] = 1;
+      continue;
+    }
+    uint64_t rsel = 0, alive = ~pm & rmask;
+    for (uint32_t t = 0; t < e; ++t) {
+      rsel |= alive & (~alive + 1);  // lowest surviving parity row
+      alive &= alive - 1;
+    }
+    auto key = std::make_pair(dm, rsel);
+    auto it = seen.find(key);
+    if (it == seen.end()) {
+      uint32_t E[kMaxDecodeShards], R[kMaxDecodeShards];
+      uint32_t ne = 0, nr = 0;
+      for (uint64_t x = dm; x; x &= x - 1) E[ne++] = static_cast<uint32_t>(__builtin_ctzll(x));
+      for (uint64_t x = rsel; x; x &= x - 1) R[nr++] = static_cast<uint32_t>(__builtin_ctzll(x));
+      const uint64_t off = book.size();
+      if ((off >> 5) >= rec_bad) return false;
+      book.resize(off + record_bytes(k, e), 0);
+      if (!build_record(k, M, E, R, e, book.data() + off)) return false;
+      it = seen.emplace(key, static_cast<uint32_t>(off >> 5)).first;
+    }
+    rec_off[g] = it->second;
+  }
+  return true;
 }
 
 }  // namespace qfec

@@ -94,13 +94,10 @@ int main() {
     if (k + r > 64) continue;
     // decode: classify ranking + codebook records
     qfec::CodebookLayout L;
-    if (!qfec::codebook_layout(k, r, 2ull << 30, L)) {
-      // dense codebook over the cap (e.g. 16+16, 32+8): not supported by this path
-      if (k + r <= 25) return fail("layout", k, r, P);
-      continue;
-    }
+    const bool dense = qfec::codebook_layout(k, r, 2ull << 30, L);
+    if (!dense && k + r <= 25) return fail("layout", k, r, P);
     std::vector<uint8_t> book;
-    if (!qfec::build_codebook(L, M, book)) return fail("codebook", k, r, P);
+    if (dense && !qfec::build_codebook(L, M, book)) return fail("codebook", k, r, P);
     for (int trial = 0; trial < 6; ++trial) {
       std::vector<uint64_t> masks(G);
       for (uint64_t g = 0; g < G; ++g) {
@@ -119,6 +116,10 @@ int main() {
       std::vector<uint8_t> st(G);
       const int64_t bad_ref = oracle_rs_decode(ref.data(), ref_par.data(), masks.data(), G, k, r, P, st.data(), 1);
       int64_t bad = 0;
+      std::vector<uint32_t> sro;
+      std::vector<uint8_t> sst;
+      if (!dense && !qfec::build_sparse_plan(k, r, M, masks.data(), G, 0xFFFFFFFFu, 0xFFFFFFFEu, book, sro, sst))
+        return fail("sparse", k, r, P);
       for (uint64_t g = 0; g < G; ++g) {
         // classify (fec_kernels.hip)
         const uint64_t kmask = (1ull << k) - 1, rmask = (r >= 64) ? ~0ull : ((1ull << r) - 1);
@@ -141,7 +142,9 @@ int main() {
           rank_r += qfec::binom().c[__builtin_ctzll(sp)][t + 1];
           sp &= sp - 1;
         }
-        const uint64_t off = L.level_base[e] + (rank_e * qfec::binom().c[r][e] + rank_r) * L.level_stride[e];
+        const uint64_t off = dense ? L.level_base[e] + (rank_e * qfec::binom().c[r][e] + rank_r) * L.level_stride[e]
+                                   : uint64_t(sro[g]) * 32;
+        if (!dense && sst[g] != 0) return fail("sparse-status", k, r, int(g));
         if (off % 32) return fail("align", k, r, int(g));
         const uint8_t* rec = &book[off];
         if (rec[96] != e) return fail("record-e", k, r, int(g));

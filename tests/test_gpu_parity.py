@@ -165,8 +165,9 @@ def _poison(data, masks, G, k, P):
     return d.reshape(-1)
 
 
-@pytest.mark.parametrize("k,r,P", [s for s in SHAPES if s[0] + s[1] <= 25])
+@pytest.mark.parametrize("k,r,P", SHAPES + [(16, 16, 32), (32, 8, 48)])
 def test_rs_decode_matches_oracle(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
+    """Dense codebook shapes and, for (30,20), (16,16), (32,8), the per-call sparse plan."""
     G = 211
     rng = np.random.default_rng(k * 131 + r * 7 + P)
     data = oracle_mod.splitmix_bytes(G * k * P, SEED + 77 + k + r + P)
@@ -267,6 +268,7 @@ def test_fill_random_matches_oracle(gpu_ctx, oracle_mod, torch_cuda):
 def test_decode_prepare_sizes(gpu_ctx):
     assert gpu_ctx.decode_prepare(10, 3) > 0
     assert gpu_ctx.decode_prepare(20, 5) > 0
+    assert gpu_ctx.decode_prepare(16, 16) == 0      # over the dense cap: sparse per-call plans
     import quicfec
     with pytest.raises(quicfec.FecError):
         gpu_ctx.decode_prepare(40, 30)
