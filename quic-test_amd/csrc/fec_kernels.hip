@@ -366,6 +366,118 @@ __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, co
   }
 }
 
+// decode_wave with the main (16 B/lane) and tail (4 B/lane) passes fused: each lane holds
+// NM 16-byte pieces and NT 4-byte pieces of every survivor, so every coefficient table is
+// loaded (scalar) and branched on once per wave instead of once per pass.  Packet sizes
+// with NM = P / 1024 and NT = ceil((P % 1024) / 256) matching the instantiation.
+template <int K, int MAXE, int POL, int NM, int NT>
+__global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ data,
+                                                    const uint8_t* __restrict__ parity,
+                                                    const uint32_t* __restrict__ rec_off,
+                                                    const uint8_t* __restrict__ codebook,
+                                                    uint64_t groups, uint32_t P, uint32_t r, uint32_t m0,
+                                                    uint8_t* __restrict__ out, uint32_t never) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];  // see encode_v16
+  if (never) occupancy_lds[threadIdx.x] = 0;
+  constexpr int NW = 4 * NM + NT;  // dwords per lane and survivor
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * 4u +
+                      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+  if (gw >= groups) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t rec = __builtin_amdgcn_readfirstlane(rec_off[gw]);
+  if (rec >= kRecBad) return;
+  const uint8_t* recp = codebook + static_cast<uint64_t>(rec) * 32u;
+  const uint32_t* rw = reinterpret_cast<const uint32_t*>(recp);
+  const uint32_t e = rw[24] & 0xFFu;
+  const bool xor_only = ((rw[24] >> 8) & 0xFFu) != 0;
+  if (m0 >= e) return;
+  const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
+  const uint8_t* dg = data + gw * K * static_cast<uint64_t>(P);
+  const uint8_t* pg = parity + gw * r * static_cast<uint64_t>(P);
+  uint8_t* og = out + gw * K * static_cast<uint64_t>(P);
+  const uint32_t main_end = NM * 1024u;
+  uint32_t toff[NT > 0 ? NT : 1];
+  bool tok[NT > 0 ? NT : 1];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    toff[t] = main_end + t * 256u + lane * 4u;
+    tok[t] = toff[t] < P;
+    if (!tok[t]) toff[t] = main_end;  // valid address; result discarded
+  }
+  auto load = [&](const uint8_t* base, uint32_t (&v)[NW]) {
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      const u32x4 t = ld16<POL>(base + i * 1024u + lane * 16u);
+      v[4 * i] = t.x;
+      v[4 * i + 1] = t.y;
+      v[4 * i + 2] = t.z;
+      v[4 * i + 3] = t.w;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) v[4 * NM + t] = *reinterpret_cast<const uint32_t*>(base + toff[t]);
+  };
+  auto store = [&](uint8_t* base, const uint32_t (&v)[NW]) {
+#pragma unroll
+    for (int i = 0; i < NM; ++i) st16<POL>(base + i * 1024u + lane * 16u, u32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]});
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (tok[t]) {
+        if constexpr ((POL & kNtStore) != 0) __builtin_nontemporal_store(v[4 * NM + t], reinterpret_cast<uint32_t*>(base + toff[t]));
+        else *reinterpret_cast<uint32_t*>(base + toff[t]) = v[4 * NM + t];
+      }
+    }
+  };
+  auto shard = [&](uint32_t sid) {
+    return sid < K ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - K) * static_cast<uint64_t>(P);
+  };
+  if (xor_only) {  // single data loss rebuilt from parity row 0: the reference XOR
+    uint32_t acc[NW] = {};
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      uint32_t v[NW];
+      load(shard(rec_byte(rw, s)), v);
+#pragma unroll
+      for (int q = 0; q < NW; ++q) acc[q] ^= v[q];
+    }
+    store(og + rec_byte(rw, 64) * static_cast<uint64_t>(P), acc);
+    return;
+  }
+  uint32_t x[K][NW];
+#pragma unroll
+  for (int s = 0; s < K; ++s) load(shard(rec_byte(rw, s)), x[s]);
+  uint32_t acc[MAXE][NW];
+#pragma unroll
+  for (int m = 0; m < MAXE; ++m)
+#pragma unroll
+    for (int q = 0; q < NW; ++q) acc[m][q] = 0;
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    uint32_t s0[NW], s1[NW], s2[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      s0[q] = x[s][q] & 0x07070707u;
+      s1[q] = (x[s][q] >> 3) & 0x07070707u;
+      s2[q] = (x[s][q] >> 6) & 0x03030303u;
+    }
+#pragma unroll
+    for (int m = 0; m < MAXE; ++m) {
+      if (m0 + m < e) {
+        const Tab& t = tabs[(m0 + m) * K + s];
+        if (t.coef == 1u) {
+#pragma unroll
+          for (int q = 0; q < NW; ++q) acc[m][q] ^= x[s][q];
+        } else if (t.coef != 0u) {
+#pragma unroll
+          for (int q = 0; q < NW; ++q) acc[m][q] ^= gmul(s0[q], s1[q], s2[q], t);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MAXE; ++m)
+    if (m0 + m < e) store(og + rec_byte(rw, 64 + m0 + m) * static_cast<uint64_t>(P), acc[m]);
+}
+
 // One wave per group, so the record is wave-uniform (SGPRs).  A packet is covered by
 // whole 1 KiB passes of 16 B per lane, then the remainder (< 1 KiB) by 256 B passes of
 // 4 B per lane: at 1200 B that is 64 + 44 busy lanes instead of 64 + 11 lanes doing
@@ -791,6 +903,41 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
   return hipSuccess;
 }
 
+template <int K, int MAXE, int POL, int NM, int NT>
+hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
+  const uint32_t passes = (a.r + MAXE - 1) / MAXE;
+  const uint32_t smem = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_DECODE_WAVES", kDecodeWavesPerCU), 4);
+  for (uint32_t p = 0; p < passes; ++p) {
+    const uint32_t m0 = p * MAXE;
+    const uint64_t blocks = (a.groups + 3) / 4;
+    for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 24)) {
+      const uint64_t bn = (blocks - b0 < (1u << 24)) ? blocks - b0 : (1u << 24);
+      const uint64_t g0 = b0 * 4;
+      const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
+      hipLaunchKernelGGL((decode_fused<K, MAXE, POL, NM, NT>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
+                         a.data + g0 * a.k * static_cast<uint64_t>(a.P),
+                         a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
+                         a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
+// The fused form for this (k, r, P), if instantiated; hipErrorNotSupported otherwise.
+hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s) {
+  const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
+#define QFEC_FUSED(KK, RR, NMM, NTT) \
+  if (a.k == KK && a.r == RR && nm == NMM && nt == NTT) return run_decode_fused<KK, RR, kNtStore, NMM, NTT>(a, s);
+  QFEC_FUSED(10, 3, 1, 1)
+  QFEC_FUSED(20, 5, 1, 1)
+  QFEC_FUSED(10, 1, 1, 1)
+  QFEC_FUSED(4, 2, 0, 1)
+#undef QFEC_FUSED
+  return hipErrorNotSupported;
+}
+
 template <int K, int MAXE, int POL>
 hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s) {
   const uint32_t cpp = a.P / 16u;
@@ -845,6 +992,12 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     QFEC_TILED(20, 5)
     QFEC_TILED(4, 2)
 #undef QFEC_TILED
+  }
+  // Fused passes win where many rows share each survivor (k=20 r=5, 5 losses: +21%) and
+  // lose slightly at r = 3 (tools/probe_decode.hip): auto picks them for r >= 5.
+  if (a.variant == kDecodeFused || (a.variant == kDecodeAuto && a.r >= 5)) {
+    const hipError_t e = try_decode_fused(a, s);
+    if (e != hipErrorNotSupported) return e;
   }
   if (a.variant == kDecodeWaveNoBranch && !separate_out) {
 #define QFEC_WAVE_NB(KK, RR) \

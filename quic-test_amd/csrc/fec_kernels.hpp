@@ -53,6 +53,7 @@ constexpr int kDecodeTiledNt = 3;        //   same, non-temporal stores
 constexpr int kDecodeWavePlain = 4;      // one wave per group, 16-B passes + 4-B tail
 constexpr int kDecodeWaveNt = 5;         //   same, non-temporal stores (the default)
 constexpr int kDecodeWaveNoBranch = 6;   //   same, no branch on coefficient 0 / 1
+constexpr int kDecodeFused = 7;          // one wave per group, 16-B and 4-B pieces fused
 
 struct DecodeLaunch {
   int variant = kDecodeAuto;

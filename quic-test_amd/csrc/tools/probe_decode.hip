@@ -112,11 +112,9 @@ int main(int argc, char** argv) {
   };
   std::vector<Var> vars = {{"wave-per-group v16", kDecodeWavePerGroup, -1, {}},
                            {"wave nt uncapped", kDecodeWaveNt, -1, {}},
-                           {"wave nt cap 8", kDecodeWaveNt, 8, {}},
-                           {"wave nt cap 12", kDecodeWaveNt, 12, {}},
-                           {"wave nt cap 16", kDecodeWaveNt, 16, {}},
-                           {"wave nt cap 20", kDecodeWaveNt, 20, {}},
-                           {"wave nt cap 24", kDecodeWaveNt, 24, {}}};
+                           {"fused nt", kDecodeFused, -1, {}},
+                           {"fused nt cap 16", kDecodeFused, 16, {}},
+                           {"fused nt cap 24", kDecodeFused, 24, {}}};
   for (auto& v : vars) {
     dl.variant = v.variant;
     dl.waves_per_cu = v.waves;
