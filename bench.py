@@ -392,6 +392,8 @@ def main() -> int:
     dec_ms = (sum(e[1].elapsed_time(e[2]) for e in events) / args.steps) if cfg["decode"] else 0.0
 
     elapsed_max = reduce_max(elapsed)
+    if verified is not None:  # every rank must have rebuilt its shard exactly
+        verified = reduce_max(0.0 if verified else 1.0) == 0.0
     total_groups = reduce_sum(float(G))
     payload = total_groups * k * P * args.steps
     value = payload / elapsed_max / 2**30

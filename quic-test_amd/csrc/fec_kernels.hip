@@ -85,6 +85,16 @@ __device__ __forceinline__ uint8_t gmul_byte(uint32_t x, const Tab& t) {
   return static_cast<uint8_t>(gmul(x & 7u, (x >> 3) & 7u, (x >> 6) & 3u, t));
 }
 
+// XCD-aware order of the workgroups' tiles.  Workgroups are dealt round-robin to the 8
+// XCDs (b and b + 8 share one; MI355X_MICROARCH.md "Workgroup dispatch"), so mapping
+// b -> (b % 8) * (n / 8) + b / 8 hands every XCD one contiguous eighth of the batch
+// instead of every eighth tile.  Placement only changes speed, never results (any
+// bijection of tiles is correct).  Measured +4..8% on encode (tools/probe_encode.hip).
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
+  const uint32_t per = n >> 3;
+  return b < (per << 3) ? (b & 7u) * per + (b >> 3) : b;
+}
+
 template <int OFF>
 __device__ __forceinline__ const uint8_t* packet_ptr(const uint8_t* data, const void* offsets,
                                                      uint64_t g, uint32_t k, uint32_t j, uint32_t P) {
@@ -129,7 +139,7 @@ __global__ __launch_bounds__(512) void encode_v16(const uint8_t* __restrict__ da
     gl = lane / cpp;
     col = lane - gl * cpp;
     if (gl >= tile) return;
-    gl += blockIdx.x * tile;
+    gl += xcd_tile(blockIdx.x, gridDim.x) * tile;
     if (gl >= groups) return;
   } else {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -376,11 +386,11 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ rec_off,
                                                     const uint8_t* __restrict__ codebook,
                                                     uint64_t groups, uint32_t P, uint32_t r, uint32_t m0,
-                                                    uint8_t* __restrict__ out, uint32_t never) {
+                                                    uint8_t* __restrict__ out, uint32_t never, uint32_t swz) {
   extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];  // see encode_v16
   if (never) occupancy_lds[threadIdx.x] = 0;
   constexpr int NW = 4 * NM + NT;  // dwords per lane and survivor
-  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * 4u +
+  const uint64_t gw = static_cast<uint64_t>(swz ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * 4u +
                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   if (gw >= groups) return;
   const uint32_t lane = threadIdx.x & 63u;
@@ -488,10 +498,11 @@ __global__ __launch_bounds__(256) void decode_wave(uint8_t* __restrict__ data,
                                                    const uint32_t* __restrict__ rec_off,
                                                    const uint8_t* __restrict__ codebook,
                                                    uint64_t groups, uint32_t P, uint32_t k_rt, uint32_t r,
-                                                   uint32_t m0, uint8_t* __restrict__ out, uint32_t never) {
+                                                   uint32_t m0, uint8_t* __restrict__ out, uint32_t never,
+                                                   uint32_t swz) {
   extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];  // see encode_v16
   if (never) occupancy_lds[threadIdx.x] = 0;
-  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * 4u +
+  const uint64_t gw = static_cast<uint64_t>(swz ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * 4u +
                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   if (gw >= groups) return;
   const uint32_t lane = threadIdx.x & 63u;
@@ -738,6 +749,12 @@ inline uint32_t blocks_for(uint64_t n) { return static_cast<uint32_t>((n + 255) 
 // ---------------------------------------------------------------------------------
 namespace {
 
+// XCD-aware group order for a decode kernel: at k=10 r=3 measured +10% for decode_fused and
+// -1%..+5% for decode_wave over two boxes (tools/probe_decode.hip; tunable per kernel).
+uint32_t decode_swizzle(const DecodeLaunch& a, int tuned) {
+  return static_cast<uint32_t>(a.xcd_swizzle >= 0 ? a.xcd_swizzle : tuned);
+}
+
 // Tuning override of an occupancy cap from the environment (-1 = none), else `def`.
 int env_waves(const char* name, int def) {
   const char* v = std::getenv(name);
@@ -895,7 +912,8 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
       hipLaunchKernelGGL((decode_wave<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                          a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
-                         a.k, a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u);
+                         a.k, a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u,
+                         decode_swizzle(a, kDecodeWaveXcdSwizzle));
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
@@ -917,7 +935,8 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
       hipLaunchKernelGGL((decode_fused<K, MAXE, POL, NM, NT>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                          a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
-                         a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u);
+                         a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u,
+                         decode_swizzle(a, kDecodeFusedXcdSwizzle));
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
@@ -993,9 +1012,10 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     QFEC_TILED(4, 2)
 #undef QFEC_TILED
   }
-  // Fused passes win where many rows share each survivor (k=20 r=5, 5 losses: +21%) and
-  // lose slightly at r = 3 (tools/probe_decode.hip): auto picks them for r >= 5.
-  if (a.variant == kDecodeFused || (a.variant == kDecodeAuto && a.r >= 5)) {
+  // Fused passes win where many rows share each survivor (k=20 r=5, 5 losses: +21%); with
+  // the XCD-aware order they also win at r = 3 (+2.6%; tools/probe_decode.hip), so auto
+  // takes them wherever they are instantiated.
+  if (a.variant == kDecodeFused || a.variant == kDecodeAuto) {
     const hipError_t e = try_decode_fused(a, s);
     if (e != hipErrorNotSupported) return e;
   }

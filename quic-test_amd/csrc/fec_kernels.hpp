@@ -73,7 +73,11 @@ struct DecodeLaunch {
   bool vec16;
   int waves_per_cu = 0;      // occupancy cap of the decode kernel (0 = tuned default)
   bool rec_ready = false;    // rec_off already filled by the host (sparse plan): no classify
+  int xcd_swizzle = -1;      // XCD-aware group order: -1 tuned default, 0 off, 1 on
 };
+
+constexpr int kDecodeFusedXcdSwizzle = 1;  // tuned per kernel (fec_kernels.hip decode_swizzle)
+constexpr int kDecodeWaveXcdSwizzle = 1;
 
 hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s);
 hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s);

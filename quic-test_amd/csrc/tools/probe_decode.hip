@@ -108,16 +108,19 @@ int main(int argc, char** argv) {
     std::string name;
     int variant;
     int waves;
+    int swz;
     std::vector<float> ms;
   };
-  std::vector<Var> vars = {{"wave-per-group v16", kDecodeWavePerGroup, -1, {}},
-                           {"wave nt uncapped", kDecodeWaveNt, -1, {}},
-                           {"fused nt", kDecodeFused, -1, {}},
-                           {"fused nt cap 16", kDecodeFused, 16, {}},
-                           {"fused nt cap 24", kDecodeFused, 24, {}}};
+  std::vector<Var> vars = {{"wave-per-group v16", kDecodeWavePerGroup, -1, 0, {}},
+                           {"wave nt", kDecodeWaveNt, -1, 0, {}},
+                           {"wave nt xcd", kDecodeWaveNt, -1, 1, {}},
+                           {"auto (library default)", kDecodeAuto, 0, -1, {}},
+                           {"fused nt", kDecodeFused, -1, 0, {}},
+                           {"fused nt xcd", kDecodeFused, -1, 1, {}}};
   for (auto& v : vars) {
     dl.variant = v.variant;
     dl.waves_per_cu = v.waves;
+    dl.xcd_swizzle = v.swz;
     poison<<<uint32_t((nd + 255) / 256), 256>>>(data, masks, G, k, P);
     CK(launch_decode(dl, nullptr));
     CK(hipDeviceSynchronize());
@@ -133,6 +136,7 @@ int main(int argc, char** argv) {
     for (auto& v : vars) {
       dl.variant = v.variant;
       dl.waves_per_cu = v.waves;
+      dl.xcd_swizzle = v.swz;
       CK(hipEventRecord(e0));
       CK(launch_decode(dl, nullptr));
       CK(hipEventRecord(e1));

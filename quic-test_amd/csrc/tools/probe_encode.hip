@@ -111,6 +111,43 @@ __global__ __launch_bounds__(((T * 75 + 63) / 64) * 64) void enc_blk(const uint8
   for (int i = 0; i < R; ++i) st16<POL>(parity + (g * R + i) * P + col * 16u, acc[i]);
 }
 
+// enc_blk with an XCD-aware tile order: blocks b and b+8 share an XCD (round-robin
+// dispatch), so tile = (b % 8) * (nblocks / 8) + b / 8 gives each XCD one contiguous
+// eighth of the data.
+template <int T, int POL>
+__global__ __launch_bounds__(((T * 75 + 63) / 64) * 64) void enc_xcd(const uint8_t* __restrict__ data,
+                                                                   uint8_t* __restrict__ parity, uint32_t groups,
+                                                                   const Tab* __restrict__ tabs) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t cap_lds[];
+  if (groups == 0xFFFFFFFFu) cap_lds[threadIdx.x] = 0;
+  constexpr int K = 10, R = 3, P = 1200, CPP = 75;
+  const uint32_t nb = gridDim.x, b = blockIdx.x;
+  const uint32_t per = nb / 8;
+  const uint32_t tile = (b < per * 8) ? (b % 8) * per + b / 8 : b;
+  const uint32_t lane = threadIdx.x;
+  if (lane >= T * CPP) return;
+  const uint32_t gl = lane / CPP, col = lane - gl * CPP;
+  const uint64_t g = uint64_t(tile) * T + gl;
+  if (g >= groups) return;
+  const uint8_t* src = data + g * K * P + col * 16u;
+  u32x4 d[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) d[j] = ld16<POL>(src + j * P);
+  u32x4 acc[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) acc[i] = d[0];
+#pragma unroll
+  for (int j = 1; j < K; ++j) {
+    Sel s;
+    prep(d[j], s);
+    acc[0] ^= d[j];
+#pragma unroll
+    for (int i = 1; i < R; ++i) mac(acc[i], s, tabs[(i - 1) * K + j]);
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) st16<POL>(parity + (g * R + i) * P + col * 16u, acc[i]);
+}
+
 // enc_blk as a persistent grid: each workgroup walks tiles blockIdx.x, +gridDim.x, ...
 template <int T, int POL>
 __global__ __launch_bounds__(((T * 75 + 63) / 64) * 64) void enc_persist(const uint8_t* __restrict__ data,
@@ -410,11 +447,9 @@ int main(int argc, char** argv) {
                       enc_blk<4, 2><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab);
                     }, {}});
   }
-  for (int per_cu : {2, 3, 4}) {
-    const uint32_t ntl = uint32_t((G + 3) / 4);
-    const uint32_t grid = std::min<uint32_t>(ntl, 256u * per_cu);
-    vars.push_back({"enc_persist x" + std::to_string(per_cu), enc_bytes, [=] {
-                      enc_persist<4, 2><<<grid, 320>>>(data, par, uint32_t(G), dtab);
+  for (int smem : {0, 81 * 1024 / 2 + 16, 80 * 1024}) {
+    vars.push_back({"enc_xcd<4> smem" + std::to_string(smem / 1024), enc_bytes, [=] {
+                      enc_xcd<4, 2><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab);
                     }, {}});
   }
   for (int per_cu : {1}) {
