@@ -258,20 +258,19 @@ bool FECDecoder::AddPacket(const uint8_t* packet, size_t len, uint64_t packetID,
   g.present[packetID] = true;
   g.received++;
   metrics_.PacketsReceived++;
-  if (g.hasRedundancy && g.received < g.packetCount) return tryRecover(g);
+  if ((g.hasRedundancy || !g.rows.empty()) && g.received < g.packetCount) return tryRecover(g, nullptr);
   return false;
 }
 
 std::pair<bool, std::vector<Recovered>> FECDecoder::AddRedundancyPacket(const uint8_t* b, size_t len) {
   std::lock_guard<std::mutex> lk(mu_);
-  // parseRedundancyHeader, decoder.go:72-85
-  if (len < 11 || b[0] != 0xFE || b[1] != 0xC0) return {false, {}};
-  uint64_t groupID = 0;
-  for (int i = 0; i < 8; ++i) groupID |= uint64_t(b[2 + i]) << (8 * i);
-  const int packetCount = b[10];
-  if (packetCount <= 0 || packetCount > kMaxPacketCount) return {false, {}};
-  const uint8_t* payload = b + 11;
-  const size_t plen = len - 11;
+  // parseRedundancyHeader, decoder.go:72-85, extended with the row 1..r-1 form
+  RSRepairHeader h;
+  const uint8_t* payload = nullptr;
+  size_t plen = 0;
+  if (!ParseRepairHeader(b, len, &h, &payload, &plen)) return {false, {}};
+  const uint64_t groupID = h.groupID;
+  const int packetCount = h.count;
 
   if (groups_.find(groupID) == groups_.end() && groups_.size() >= kMaxActiveGroups) evictOldestGroup();
   auto it = groups_.find(groupID);
@@ -284,36 +283,52 @@ std::pair<bool, std::vector<Recovered>> FECDecoder::AddRedundancyPacket(const ui
     metrics_.GroupsActive = static_cast<int64_t>(groups_.size());
   }
   Group& g = it->second;
-  if (g.packetCount != 0 && g.packetCount != packetCount) {  // conflicting counts: drop the group
+  const bool shapeConflict = h.row > 0 && g.k != 0 && (g.k != h.k || g.r != h.r);
+  if ((g.packetCount != 0 && g.packetCount != packetCount) || shapeConflict) {  // conflicting: drop the group
+    if (g.queued) pending_.erase(std::find(pending_.begin(), pending_.end(), groupID));
     groups_.erase(it);
     metrics_.GroupsActive = static_cast<int64_t>(groups_.size());
     return {false, {}};
   }
   g.packetCount = packetCount;
   if (g.symbolLen == 0) g.symbolLen = static_cast<int>(std::min<size_t>(plen, kMaxSymbolLen));
-  g.redundancy = padTo(payload, plen, static_cast<size_t>(g.symbolLen));
-  g.hasRedundancy = true;
+  if (h.row == 0) {
+    g.redundancy = padTo(payload, plen, static_cast<size_t>(g.symbolLen));
+    g.hasRedundancy = true;
+  } else {
+    g.k = h.k;
+    g.r = h.r;
+    g.rows[h.row] = padTo(payload, plen, static_cast<size_t>(g.symbolLen));
+  }
   metrics_.RepairPacketsReceived++;
   if (g.received < g.packetCount) {
-    if (tryRecover(g)) {
-      // decoder.go:170-178 lists ids still marked absent; tryRecover has just marked the
-      // rebuilt one present, so — as in the reference — the list comes back empty.
-      std::vector<Recovered> list;
-      for (uint64_t id = 0; id < static_cast<uint64_t>(g.packetCount); ++id) {
-        auto p = g.present.find(id);
-        if ((p == g.present.end() || !p->second) && g.packets.count(id)) list.push_back({id, g.packets[id]});
-      }
+    std::vector<Recovered> list;
+    if (tryRecover(g, &list)) {
+      // Row 0 alone: decoder.go:170-178 lists ids still marked absent; the single-loss path
+      // has just marked the rebuilt one present, so — as in the reference — the list comes
+      // back empty.  The r > 1 path (new) returns what it rebuilt.
       return {true, list};
     }
   }
   return {false, {}};
 }
 
-bool FECDecoder::tryRecover(Group& g) {  // decoder.go:216-248
-  if (!g.hasRedundancy) return false;
+bool FECDecoder::canRecoverRS(const Group& g) const {
+  if (g.k <= 0 || g.r <= 0 || g.symbolLen <= 0 || g.packetCount > g.k) return false;
+  int missing = 0;
+  for (int id = 0; id < g.packetCount; ++id) {
+    auto p = g.present.find(static_cast<uint64_t>(id));
+    missing += (p == g.present.end() || !p->second) ? 1 : 0;
+  }
+  const int rows = (g.hasRedundancy ? 1 : 0) + static_cast<int>(g.rows.size());
+  return missing >= 1 && missing <= rows;
+}
+
+bool FECDecoder::tryRecover(Group& g, std::vector<Recovered>* list) {  // decoder.go:216-248
+  if (!g.hasRedundancy && g.rows.empty()) return false;
   if (g.received >= g.packetCount) return false;
   const int missing = g.packetCount - g.received;
-  if (missing == 1) {
+  if (missing == 1 && g.hasRedundancy) {
     uint64_t id = 0;
     Bytes data;
     if (recoverSingle(g, &id, &data)) {
@@ -325,9 +340,25 @@ bool FECDecoder::tryRecover(Group& g) {  // decoder.go:216-248
       return true;
     }
     metrics_.FailedRecoveries++;
-  } else {
-    metrics_.FailedRecoveries++;  // multiple losses: XOR recovers one
+    return false;
   }
+  if (canRecoverRS(g)) {  // r > 1 (new): up to as many losses as rows received
+    if (deferred_) {
+      if (!g.queued) {
+        g.queued = true;
+        pending_.push_back(g.groupID);
+      }
+      return false;
+    }
+    std::vector<Group*> one{&g};
+    std::vector<std::vector<Recovered>> lists;
+    if (recoverRS(one, &lists)) {
+      if (list) *list = std::move(lists[0]);
+      return true;
+    }
+    return false;
+  }
+  metrics_.FailedRecoveries++;  // more losses than repair rows (row 0 alone: XOR recovers one)
   return false;
 }
 
@@ -361,6 +392,7 @@ void FECDecoder::evictOldestGroup() {  // decoder.go:306-325
   auto oldest = groups_.begin();
   for (auto it = groups_.begin(); it != groups_.end(); ++it)
     if (it->second.createdAt < oldest->second.createdAt) oldest = it;
+  if (oldest->second.queued) pending_.erase(std::find(pending_.begin(), pending_.end(), oldest->first));
   groups_.erase(oldest);
   metrics_.GroupsEvicted++;
   metrics_.GroupsActive = static_cast<int64_t>(groups_.size());
@@ -371,6 +403,7 @@ void FECDecoder::CleanupGroups() {  // decoder.go:328-343
   const auto now = std::chrono::steady_clock::now();
   for (auto it = groups_.begin(); it != groups_.end();) {
     if (now - it->second.createdAt > std::chrono::seconds(kGroupTTLSeconds)) {
+      if (it->second.queued) pending_.erase(std::find(pending_.begin(), pending_.end(), it->first));
       it = groups_.erase(it);
       metrics_.GroupsEvicted++;
     } else {
@@ -449,6 +482,280 @@ int64_t RecoverBatchRS(Bytes& data, const Bytes& parity, const std::vector<uint6
     return -1;
   }
   return static_cast<int64_t>(bad);
+}
+
+// ===================================================================== r > 1 (new)
+bool ParseRepairHeader(const uint8_t* b, size_t len, RSRepairHeader* h, const uint8_t** payload, size_t* plen) {
+  if (len < kRepairHeaderLen || b[0] != 0xFE || (b[1] != 0xC0 && b[1] != 0xC1)) return false;
+  RSRepairHeader x;
+  for (int i = 0; i < 8; ++i) x.groupID |= uint64_t(b[2 + i]) << (8 * i);
+  x.count = b[10];
+  if (x.count <= 0 || x.count > FECDecoder::kMaxPacketCount) return false;  // decoder.go:80-82
+  size_t hl = kRepairHeaderLen;
+  if (b[1] == 0xC1) {
+    if (len < kRSRepairHeaderLen) return false;
+    x.row = b[11];
+    x.r = b[12];
+    x.k = b[13];
+    if (x.row < 1 || x.row >= x.r || x.k < 1 || x.count > x.k || x.k + x.r > 64) return false;
+    hl = kRSRepairHeaderLen;
+  }
+  *h = x;
+  *payload = b + hl;
+  *plen = len - hl;
+  return true;
+}
+
+Bytes MakeRepairPacket(const RSRepairHeader& h, const uint8_t* payload, size_t plen) {
+  const size_t hl = h.row == 0 ? kRepairHeaderLen : kRSRepairHeaderLen;
+  Bytes out(hl + plen);
+  out[0] = 0xFE;
+  out[1] = h.row == 0 ? 0xC0 : 0xC1;
+  for (int b = 0; b < 8; ++b) out[2 + b] = static_cast<uint8_t>(h.groupID >> (8 * b));
+  out[10] = static_cast<uint8_t>(h.count);
+  if (h.row != 0) {
+    out[11] = static_cast<uint8_t>(h.row);
+    out[12] = static_cast<uint8_t>(h.r);
+    out[13] = static_cast<uint8_t>(h.k);
+  }
+  if (plen) std::memcpy(out.data() + hl, payload, plen);
+  return out;
+}
+
+// ---------------------------------------------------------------- FECDecoder, r > 1
+bool FECDecoder::recoverRS(const std::vector<Group*>& gs, std::vector<std::vector<Recovered>>* lists) {
+  lists->assign(gs.size(), {});
+  if (gs.empty()) return true;
+  FECEncoderCtx* ctx = shared_ctx();
+  if (!ctx) return false;
+  const int k = gs[0]->k, r = gs[0]->r;
+  size_t L = 0;
+  for (Group* g : gs) L = std::max(L, static_cast<size_t>(g->symbolLen));
+  const size_t G = gs.size();
+  // Symbols zero-padded to the widest group's length: bytewise coding keeps every group's
+  // own prefix exact.  Slots count..k-1 are the encoder's zero packets (present).
+  Bytes data(G * k * L, 0), parity(G * r * L, 0), status(G, 0);
+  std::vector<uint64_t> masks(G, 0);
+  for (size_t i = 0; i < G; ++i) {
+    Group& g = *gs[i];
+    for (int id = 0; id < g.packetCount; ++id) {
+      auto p = g.present.find(static_cast<uint64_t>(id));
+      if (p == g.present.end() || !p->second) {
+        masks[i] |= 1ull << id;
+      } else {
+        const Bytes& pk = g.packets[static_cast<uint64_t>(id)];
+        std::memcpy(&data[(i * k + id) * L], pk.data(), std::min(pk.size(), L));
+      }
+    }
+    for (int row = 0; row < r; ++row) {
+      const Bytes* src = nullptr;
+      if (row == 0 && g.hasRedundancy) src = &g.redundancy;
+      if (row > 0) {
+        auto rw = g.rows.find(row);
+        if (rw != g.rows.end()) src = &rw->second;
+      }
+      if (src) std::memcpy(&parity[(i * r + row) * L], src->data(), std::min(src->size(), L));
+      else masks[i] |= 1ull << (k + row);
+    }
+  }
+  uint64_t bad = 0;
+  const int rc = fec_decode_batch_rs(ctx, data.data(), parity.data(), masks.data(), G, static_cast<uint32_t>(k),
+                                     static_cast<uint32_t>(r), static_cast<uint32_t>(L), status.data(), &bad);
+  if (rc != 0) {
+    metrics_.FailedRecoveries += static_cast<int64_t>(G);
+    return false;
+  }
+  for (size_t i = 0; i < G; ++i) {
+    Group& g = *gs[i];
+    g.queued = false;
+    if (status[i] != 0) {
+      metrics_.FailedRecoveries++;
+      continue;
+    }
+    for (int id = 0; id < g.packetCount; ++id) {
+      if (!((masks[i] >> id) & 1)) continue;
+      const uint8_t* src = &data[(i * k + id) * L];
+      Bytes sym(src, src + g.symbolLen);
+      g.packets[static_cast<uint64_t>(id)] = sym;
+      g.present[static_cast<uint64_t>(id)] = true;
+      g.received++;
+      metrics_.PacketsRecovered++;
+      (*lists)[i].push_back({static_cast<uint64_t>(id), std::move(sym)});
+    }
+    metrics_.RecoveryEvents++;
+  }
+  return true;
+}
+
+void FECDecoder::SetDeferredRecovery(bool deferred) {
+  std::lock_guard<std::mutex> lk(mu_);
+  deferred_ = deferred;
+}
+
+std::vector<std::pair<uint64_t, std::vector<Recovered>>> FECDecoder::RecoverPending(Error* err) {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<std::pair<uint64_t, std::vector<Recovered>>> out;
+  // one library call per code shape
+  std::map<std::pair<int, int>, std::vector<Group*>> byShape;
+  for (uint64_t id : pending_) {
+    auto it = groups_.find(id);
+    if (it == groups_.end() || !it->second.queued) continue;
+    it->second.queued = false;
+    if (!canRecoverRS(it->second)) continue;  // completed by data packets meanwhile
+    byShape[{it->second.k, it->second.r}].push_back(&it->second);
+  }
+  pending_.clear();
+  for (auto& kv : byShape) {
+    std::vector<std::vector<Recovered>> lists;
+    if (!recoverRS(kv.second, &lists)) {
+      if (err) *err = errorf("fec_decode_batch_rs failed: %s", fec_hip_last_error());
+      continue;
+    }
+    for (size_t i = 0; i < kv.second.size(); ++i)
+      if (!lists[i].empty()) out.emplace_back(kv.second[i]->groupID, std::move(lists[i]));
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------- RSBatchEncoder
+std::unique_ptr<RSBatchEncoder> RSBatchEncoder::New(int k, int r, int batchGroups, int slotSize) {
+  if (k < 1 || r < 1 || k + r > 64 || k > FECDecoder::kMaxPacketCount || r > 255 || batchGroups < 1 ||
+      slotSize < 1)
+    return nullptr;
+  std::unique_ptr<RSBatchEncoder> e(new RSBatchEncoder());
+  e->k_ = k;
+  e->r_ = r;
+  e->batch_ = batchGroups;
+  e->slot_ = (static_cast<size_t>(slotSize) + 15) / 16 * 16;  // 16-byte packets: the vector kernels
+  e->ctx_ = fec_encoder_new(0.10, static_cast<uint32_t>(batchGroups));
+  if (!e->ctx_) return nullptr;
+  e->slab_ = static_cast<uint8_t*>(fec_alloc_slab(size_t(batchGroups) * k * e->slot_));
+  e->parity_ = static_cast<uint8_t*>(fec_alloc_repair_buffer(size_t(batchGroups) * r * e->slot_));
+  if (!e->slab_ || !e->parity_) return nullptr;  // the destructor frees what was allocated
+  e->count_.assign(batchGroups, 0);
+  e->maxLen_.assign(batchGroups, 0);
+  return e;
+}
+
+RSBatchEncoder::~RSBatchEncoder() { Close(); }
+
+Error RSBatchEncoder::Close() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (slab_) fec_free_slab(slab_);
+  if (parity_) fec_free_repair_buffer(parity_);
+  if (ctx_) fec_encoder_free(ctx_);
+  slab_ = parity_ = nullptr;
+  ctx_ = nullptr;
+  open_ = 0;
+  return {};
+}
+
+Error RSBatchEncoder::encodeLocked(int groups, std::vector<Bytes>* out) {
+  if (groups <= 0) return {};
+  // zero the slots a partial last group does not fill (the slab is reused across batches)
+  const int last = groups - 1;
+  for (uint32_t j = count_[last]; j < static_cast<uint32_t>(k_); ++j)
+    std::memset(slab_ + (size_t(last) * k_ + j) * slot_, 0, slot_);
+  const int rc = fec_encode_batch_rs(ctx_, slab_, nullptr, static_cast<uint64_t>(groups), static_cast<uint32_t>(k_),
+                                     static_cast<uint32_t>(r_), static_cast<uint32_t>(slot_), parity_);
+  if (rc != 0) return errorf("fec_encode_batch_rs failed with code %d: %s", rc, fec_hip_last_error());
+  Error firstErr;
+  for (int g = 0; g < groups; ++g) {
+    const uint64_t gid = groupID_++;
+    if (maxLen_[g] == 0) {  // encoder_hybrid.go:105-107 refuses a group of empty packets
+      if (!firstErr) firstErr = errorf("empty packets in group %llu", static_cast<unsigned long long>(gid));
+      continue;
+    }
+    for (int row = 0; row < r_; ++row) {
+      RSRepairHeader h;
+      h.groupID = gid;
+      h.count = static_cast<int>(count_[g]);
+      h.row = row;
+      h.r = r_;
+      h.k = k_;
+      Bytes pkt = MakeRepairPacket(h, parity_ + (size_t(g) * r_ + row) * slot_, maxLen_[g]);
+      metrics_.RedundancyPackets++;
+      metrics_.RedundancyBytes += static_cast<int64_t>(pkt.size());
+      if (out) out->push_back(std::move(pkt));
+    }
+    metrics_.GroupsProcessed++;
+  }
+  open_ = 0;
+  return firstErr;
+}
+
+Error RSBatchEncoder::widenLocked(size_t newSlot, std::vector<Bytes>* out) {
+  const bool partial = open_ > 0 && count_[open_ - 1] < static_cast<uint32_t>(k_);
+  const int complete = open_ - (partial ? 1 : 0);
+  Bytes keep;
+  uint32_t keepCount = 0, keepMax = 0;
+  if (partial) {
+    keepCount = count_[open_ - 1];
+    keepMax = maxLen_[open_ - 1];
+    const uint8_t* src = slab_ + size_t(open_ - 1) * k_ * slot_;
+    keep.assign(src, src + size_t(keepCount) * slot_);
+  }
+  if (complete > 0) {
+    if (Error e = encodeLocked(complete, out)) return e;
+  }
+  open_ = 0;
+  auto* slab = static_cast<uint8_t*>(fec_alloc_slab(size_t(batch_) * k_ * newSlot));
+  auto* parity = static_cast<uint8_t*>(fec_alloc_repair_buffer(size_t(batch_) * r_ * newSlot));
+  if (!slab || !parity) {
+    if (slab) fec_free_slab(slab);
+    if (parity) fec_free_repair_buffer(parity);
+    return errorf("failed to widen the slab to %zu-byte slots", newSlot);
+  }
+  fec_free_slab(slab_);
+  fec_free_repair_buffer(parity_);
+  slab_ = slab;
+  parity_ = parity;
+  const size_t old = slot_;
+  slot_ = newSlot;
+  if (partial) {
+    for (uint32_t j = 0; j < keepCount; ++j) {
+      std::memcpy(slab_ + size_t(j) * slot_, keep.data() + size_t(j) * old, old);
+      std::memset(slab_ + size_t(j) * slot_ + old, 0, slot_ - old);
+    }
+    count_[0] = keepCount;
+    maxLen_[0] = keepMax;
+    open_ = 1;
+  }
+  return {};
+}
+
+Error RSBatchEncoder::AddPacket(const uint8_t* packet, size_t len, std::vector<Bytes>* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!ctx_) return errorf("encoder closed");
+  if (len > 0xFFFFu) return errorf("packet of %zu bytes is too large", len);
+  if (len > slot_) {
+    if (Error e = widenLocked((len + 15) / 16 * 16, out)) return e;
+  }
+  if (open_ == 0 || count_[open_ - 1] == static_cast<uint32_t>(k_)) {
+    count_[open_] = 0;
+    maxLen_[open_] = 0;
+    ++open_;
+  }
+  const int g = open_ - 1;
+  uint8_t* dst = slab_ + (size_t(g) * k_ + count_[g]) * slot_;
+  if (len) std::memcpy(dst, packet, len);
+  std::memset(dst + len, 0, slot_ - len);
+  count_[g]++;
+  maxLen_[g] = std::max<uint32_t>(maxLen_[g], static_cast<uint32_t>(len));
+  metrics_.PacketsEncoded++;
+  if (open_ == batch_ && count_[g] == static_cast<uint32_t>(k_)) return encodeLocked(open_, out);
+  return {};
+}
+
+Error RSBatchEncoder::Flush(std::vector<Bytes>* out) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!ctx_) return errorf("encoder closed");
+  return encodeLocked(open_, out);
+}
+
+FECMetrics RSBatchEncoder::GetMetrics() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return metrics_;
 }
 
 }  // namespace quicfec

@@ -13,8 +13,9 @@
 //   * Packets shorter than the group's largest are zero-padded and partial groups XOR only
 //     the packets present (the Go semantics, encoder.go:133-143), where the reference's C++
 //     path reads past short packets and reuses stale offsets.
-//   * FECDecoder recovery runs on the GPU (xor_packets via fec_select_xor_impl) and, as a
-//     batch extension, RecoverBatchRS rebuilds up to r losses per group.
+//   * FECDecoder recovery runs on the GPU (xor_packets via fec_select_xor_impl).  New for
+//     r > 1: RSBatchEncoder, the row 1..r-1 wire header, FECDecoder's multi-loss path and
+//     RecoverBatchRS (see "r > 1" below).
 #pragma once
 
 #include <chrono>
@@ -167,6 +168,17 @@ class FECDecoder {
   // Stored symbol of (groupID, packetID), empty if absent (recovered packets included).
   Bytes GetPacket(uint64_t groupID, uint64_t packetID);
 
+  // r > 1 (new).  Deferred mode: groups that become recoverable by rows >= 1 are queued
+  // instead of decoded one by one; RecoverPending rebuilds every queued group in one library
+  // call per (k, r) and returns the recovered packets keyed by group id.  Immediate mode
+  // (the default) decodes such a group as soon as it is recoverable.
+  void SetDeferredRecovery(bool deferred);
+  std::vector<std::pair<uint64_t, std::vector<Recovered>>> RecoverPending(Error* err = nullptr);
+  size_t pending() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return pending_.size();
+  }
+
  private:
   struct Group {
     uint64_t groupID = 0;
@@ -178,14 +190,97 @@ class FECDecoder {
     Bytes redundancy;
     bool hasRedundancy = false;
     int received = 0;
+    // r > 1 (new): rows 1..r-1 by index, and the code shape from their headers
+    std::map<int, Bytes> rows;
+    int k = 0, r = 0;
+    bool queued = false;
   };
-  bool tryRecover(Group& g);
+  bool tryRecover(Group& g, std::vector<Recovered>* list);
+  bool canRecoverRS(const Group& g) const;
+  // One library call over groups of one (k, r); fills lists[i] for gs[i].  True when the
+  // call ran (per-group failures are counted in FailedRecoveries).
+  bool recoverRS(const std::vector<Group*>& gs, std::vector<std::vector<Recovered>>* lists);
   bool recoverSingle(Group& g, uint64_t* id, Bytes* out);
   void evictOldestGroup();
 
   std::map<uint64_t, Group> groups_;
   std::mutex mu_;
   FECDecoderMetrics metrics_;
+  bool deferred_ = false;
+  std::vector<uint64_t> pending_;
+};
+
+// ===================================================================== r > 1 (new)
+// a batched encoder that emits r repair packets per group, the
+// wire header for rows 1..r-1, and the decoder path that rebuilds up to r losses.
+//
+// Wire format.  Row 0 keeps the reference's 11-byte header and payload byte for byte
+// (encoder_hybrid.go:175-192, encoder.go:146-160): FE C0 | groupID u64 LE | count u8.  A
+// receiver that only knows the reference format recovers single losses from it as before.
+// Rows i >= 1 carry a 14-byte header the reference parser rejects (decoder.go:73 checks
+// b[1] == 0xC0), so old receivers ignore them:
+//   FE C1 | groupID u64 LE | count u8 | row u8 (1..r-1) | r u8 | k u8 | payload
+// count = data packets in the group (<= k; slots count..k-1 are zero), payload = the
+// group's largest packet length.  Coding is bytewise, so any common truncation or zero
+// padding of a group's symbols keeps the recovered prefix exact (what lets the decoder keep
+// the reference's symbol-length rule, decoder.go:115-120).
+constexpr size_t kRepairHeaderLen = 11;    // row 0, the reference's header
+constexpr size_t kRSRepairHeaderLen = 14;  // rows 1..r-1
+
+struct RSRepairHeader {
+  uint64_t groupID = 0;
+  int count = 0;  // data packets in the group
+  int row = 0;    // parity row 0..r-1
+  int r = 0;      // 0 when unknown (a row-0 packet)
+  int k = 0;      // 0 when unknown (a row-0 packet)
+};
+
+// Parse either header form; false for anything else (the same bounds as decoder.go:72-85,
+// plus row < r and k + r <= 64 for the new form).
+bool ParseRepairHeader(const uint8_t* b, size_t len, RSRepairHeader* h, const uint8_t** payload, size_t* plen);
+Bytes MakeRepairPacket(const RSRepairHeader& h, const uint8_t* payload, size_t plen);
+
+// Groups of k packets, batchGroups groups per library call (one fec_encode_batch_rs over a
+// pinned slab), r repair packets per group.  Row 0 of every group is byte-identical to
+// HybridFECEncoder's repair packet for the same packets and group id.
+class RSBatchEncoder {
+ public:
+  // nullptr when the GPU library cannot be initialised or the shape is invalid
+  // (1 <= k, 1 <= r, k + r <= 64, batchGroups >= 1).  slotSize = the widest packet expected;
+  // larger packets widen the slot on the fly.
+  static std::unique_ptr<RSBatchEncoder> New(int k, int r, int batchGroups, int slotSize = 1200);
+  ~RSBatchEncoder();
+  RSBatchEncoder(const RSBatchEncoder&) = delete;
+  RSBatchEncoder& operator=(const RSBatchEncoder&) = delete;
+
+  // Copies the packet into the slab; when the batch is full, encodes it and appends every
+  // group's r repair packets (group order, row order) to *out.
+  Error AddPacket(const uint8_t* packet, size_t len, std::vector<Bytes>* out);
+  Error AddPacket(const Bytes& p, std::vector<Bytes>* out) { return AddPacket(p.data(), p.size(), out); }
+  // Encodes the complete groups and the partial one (count < k) now.
+  Error Flush(std::vector<Bytes>* out);
+  FECMetrics GetMetrics();
+  Error Close();
+  int k() const { return k_; }
+  int r() const { return r_; }
+  int slotSize() const { return slot_; }
+  uint64_t nextGroupID() const { return groupID_; }
+
+ private:
+  RSBatchEncoder() = default;
+  Error encodeLocked(int groups, std::vector<Bytes>* out);
+  Error widenLocked(size_t newSlot, std::vector<Bytes>* out);
+
+  FECEncoderCtx* ctx_ = nullptr;
+  int k_ = 0, r_ = 0, batch_ = 0;
+  size_t slot_ = 0;
+  uint8_t* slab_ = nullptr;    // pinned, batch_ * k_ * slot_
+  uint8_t* parity_ = nullptr;  // pinned, batch_ * r_ * slot_
+  std::vector<uint32_t> count_, maxLen_;  // per group of the open batch
+  int open_ = 0;                          // groups started in the open batch
+  uint64_t groupID_ = 0;
+  std::mutex mu_;
+  FECMetrics metrics_;
 };
 
 // Batch extension (new): rebuild up to r lost packets per group on the GPU.

@@ -2,6 +2,7 @@
 // C++ mirror (quic-test_amd/host/fec.hpp) running on the GPU, with the byte-level
 // assertions the reference tests never make checked against the oracle.
 // Run by tests/test_host_mirror.py (GPU).  Prints "PASS <n>" or the failures.
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -265,6 +266,250 @@ static void TestBatchRS() {
   CHECK(broken == data);
 }
 
+// ---------------------------------------------------------------- r > 1
+static Bytes padded(const Bytes& b, size_t n) {
+  Bytes o(n, 0);
+  std::memcpy(o.data(), b.data(), std::min(n, b.size()));
+  return o;
+}
+
+// rows 0..r-1 of one group, each truncated to the group's largest packet (the oracle)
+static std::vector<Bytes> oracle_rows(const std::vector<Bytes>& pk, int k, int r) {
+  size_t mx = 0;
+  for (auto& x : pk) mx = std::max(mx, x.size());
+  const size_t P = (mx + 15) / 16 * 16;
+  Bytes data(size_t(k) * P, 0), par(size_t(r) * P);
+  for (size_t j = 0; j < pk.size(); ++j) std::memcpy(&data[j * P], pk[j].data(), pk[j].size());
+  oracle_rs_encode(data.data(), 1, k, r, static_cast<uint32_t>(P), par.data(), 1);
+  std::vector<Bytes> rows;
+  for (int i = 0; i < r; ++i) rows.emplace_back(par.begin() + size_t(i) * P, par.begin() + size_t(i) * P + mx);
+  return rows;
+}
+
+static void TestRSWireHeader() {
+  const Bytes pay = rnd(100, 5);
+  RSRepairHeader h;
+  h.groupID = 0x0102030405060708ull;
+  h.count = 7;
+  Bytes row0 = MakeRepairPacket(h, pay.data(), pay.size());
+  // row 0 = the reference header byte for byte (encoder_hybrid.go:175-192)
+  CHECK(row0.size() == 111 && row0[0] == 0xFE && row0[1] == 0xC0 && row0[2] == 0x08 && row0[9] == 0x01 &&
+        row0[10] == 7);
+  h.row = 2;
+  h.r = 3;
+  h.k = 10;
+  Bytes row2 = MakeRepairPacket(h, pay.data(), pay.size());
+  CHECK(row2.size() == 114 && row2[1] == 0xC1 && row2[11] == 2 && row2[12] == 3 && row2[13] == 10);
+  RSRepairHeader x;
+  const uint8_t* pl = nullptr;
+  size_t n = 0;
+  CHECK(ParseRepairHeader(row0.data(), row0.size(), &x, &pl, &n) && x.row == 0 && x.r == 0 && x.count == 7 &&
+        x.groupID == h.groupID && n == 100 && Bytes(pl, pl + n) == pay);
+  CHECK(ParseRepairHeader(row2.data(), row2.size(), &x, &pl, &n) && x.row == 2 && x.r == 3 && x.k == 10 &&
+        n == 100 && Bytes(pl, pl + n) == pay);
+  auto rejects = [&](Bytes b) { return !ParseRepairHeader(b.data(), b.size(), &x, &pl, &n); };
+  Bytes b = row2;
+  b[11] = 3;  // row >= r
+  CHECK(rejects(b));
+  b = row2;
+  b[11] = 0;  // row 0 must use the reference header
+  CHECK(rejects(b));
+  b = row2;
+  b[10] = 11;  // count > k
+  CHECK(rejects(b));
+  b = row2;
+  b[13] = 62;  // k + r > 64
+  CHECK(rejects(b));
+  b = row2;
+  b[1] = 0xC2;
+  CHECK(rejects(b));
+  CHECK(rejects(Bytes(row2.begin(), row2.begin() + 13)));
+  b = row0;
+  b[10] = 0;  // count 0 (decoder.go:80)
+  CHECK(rejects(b));
+  // the reference parser (restated in FECDecoder) ignores rows >= 1 when it sees them alone
+  FECDecoder d;
+  CHECK(!d.AddRedundancyPacket(row2).first);
+}
+
+// Row 0 of RSBatchEncoder == HybridFECEncoder's repair packet; rows 1..r-1 == the oracle.
+static void TestRSBatchEncoderMatchesHybridAndOracle() {
+  const int k = 10, r = 3;
+  auto enc = RSBatchEncoder::New(k, r, 7, 1200);
+  CHECK(enc != nullptr);
+  if (!enc) return;
+  HybridFECEncoder hyb(0.1);
+  std::mt19937_64 rng(9);
+  std::vector<Bytes> sent, rs, hy;
+  const int N = 10 * 23 + 4;  // 23 full groups (3 batches + 2 groups) and a partial one
+  for (int i = 0; i < N; ++i) {
+    size_t len = 200 + rng() % 1000;
+    if (i == 95) len = 1400;  // wider than the slot, mid-group: the slab widens
+    if (i == 96) len = 0;     // empty packet inside a group
+    Bytes pkt = rnd(len, 1000 + i);
+    sent.push_back(pkt);
+    CHECK(enc->AddPacket(pkt, &rs).ok());
+    AddPacketResult a = hyb.AddPacket(pkt, i);
+    CHECK(a.err.ok());
+    if (a.needsRedundancy) hy.push_back(a.redundancy);
+  }
+  CHECK(enc->slotSize() == 1408);
+  CHECK(rs.size() == size_t(23) * r);
+  CHECK(enc->Flush(&rs).ok());
+  auto f = hyb.Flush();
+  CHECK(f.second.ok());
+  hy.push_back(f.first);
+  CHECK(rs.size() == size_t(24) * r && hy.size() == 24);
+  bool row0 = true, rows = true, hdr = true;
+  for (int g = 0; g < 24; ++g) {
+    row0 &= rs[size_t(g) * r] == hy[g];
+    std::vector<Bytes> pk(sent.begin() + g * 10, sent.begin() + std::min(N, g * 10 + 10));
+    auto exp = oracle_rows(pk, k, r);
+    for (int i = 1; i < r; ++i) {
+      const Bytes& p = rs[size_t(g) * r + i];
+      RSRepairHeader h;
+      const uint8_t* pl = nullptr;
+      size_t n = 0;
+      hdr &= ParseRepairHeader(p.data(), p.size(), &h, &pl, &n) && h.groupID == uint64_t(g) && h.row == i &&
+             h.count == int(pk.size()) && h.k == k && h.r == r;
+      rows &= Bytes(pl, pl + n) == exp[i];
+    }
+  }
+  CHECK(row0);
+  CHECK(rows);
+  CHECK(hdr);
+  FECMetrics m = enc->GetMetrics();
+  CHECK(m.GroupsProcessed == 24 && m.PacketsEncoded == N && m.RedundancyPackets == 72);
+  CHECK(enc->Flush(&rs).ok() && rs.size() == 72);  // nothing open: no-op
+  enc->Close();
+  CHECK(!enc->AddPacket(sent[0], &rs).ok());
+  CHECK(RSBatchEncoder::New(0, 3, 1) == nullptr && RSBatchEncoder::New(60, 5, 1) == nullptr &&
+        RSBatchEncoder::New(10, 3, 0) == nullptr);
+}
+
+// Encode a stream, lose up to r packets per group (data or repair), decode: every data
+// packet comes back.  deferred = one RecoverPending call for the whole stream.
+static void RunRSDecode(bool deferred, int k, int r, int G, uint64_t seed) {
+  auto enc = RSBatchEncoder::New(k, r, 16, 1200);
+  CHECK(enc != nullptr);
+  if (!enc) return;
+  std::vector<Bytes> data, repairs;
+  for (int i = 0; i < G * k; ++i) {
+    data.push_back(rnd(1200, seed + i));
+    CHECK(enc->AddPacket(data.back(), &repairs).ok());
+  }
+  CHECK(enc->Flush(&repairs).ok());
+  CHECK(repairs.size() == size_t(G) * r);
+  FECDecoder d;
+  d.SetDeferredRecovery(deferred);
+  std::mt19937_64 rng(seed);
+  int lostData = 0, expectRecovered = 0, returned = 0, lostSingles = 0;
+  std::vector<std::vector<int>> lost(G);
+  for (int g = 0; g < G; ++g) {
+    const int n = k + r;
+    std::vector<int> order(n);
+    for (int i = 0; i < n; ++i) order[i] = i;
+    std::shuffle(order.begin(), order.end(), rng);
+    const int drop = g % (r + 1);
+    std::vector<bool> dropped(n, false);
+    for (int i = 0; i < drop; ++i) dropped[order[i]] = true;
+    std::shuffle(order.begin(), order.end(), rng);
+    int lostHere = 0;
+    for (int s = 0; s < k; ++s)
+      if (dropped[s]) {
+        lost[g].push_back(s);
+        ++lostHere;
+      }
+    lostData += lostHere;
+    expectRecovered += lostHere;
+    if (lostHere == 1) ++lostSingles;  // may go the XOR path, whose list is empty (decoder.go:170-178)
+    for (int s : order) {
+      if (dropped[s]) continue;
+      if (s < k) {
+        d.AddPacket(data[size_t(g) * k + s], uint64_t(s), uint64_t(g));
+      } else {
+        auto res = d.AddRedundancyPacket(repairs[size_t(g) * r + (s - k)]);
+        if (res.first) returned += int(res.second.size());
+      }
+    }
+  }
+  if (deferred) {
+    CHECK(d.pending() > 0 || lostData == 0);
+    Error err;
+    auto rec = d.RecoverPending(&err);
+    CHECK(err.ok());
+    for (auto& kv : rec) returned += int(kv.second.size());
+    CHECK(d.pending() == 0);
+  }
+  bool all = true;
+  for (int g = 0; g < G; ++g)
+    for (int s = 0; s < k; ++s) all &= d.GetPacket(uint64_t(g), uint64_t(s)) == data[size_t(g) * k + s];
+  CHECK(all);
+  // Packets still in flight when a group first becomes decodable are rebuilt too (the
+  // decoder cannot tell late from lost), so the counters bound the losses from above.
+  FECDecoderMetrics m = d.GetMetrics();
+  CHECK(m.PacketsRecovered >= expectRecovered);
+  CHECK(returned >= (deferred ? expectRecovered - lostSingles : 0));
+}
+
+static void TestRSDecoderImmediate() { RunRSDecode(false, 10, 3, 64, 500); }
+static void TestRSDecoderDeferredBatch() {
+  RunRSDecode(true, 10, 3, 200, 900);
+  RunRSDecode(true, 20, 5, 40, 1300);
+}
+
+// More losses than rows: counted as failures, nothing rebuilt, no crash; the legacy
+// (row 0 only) receiver still recovers single losses and fails on two (decoder.go:233-248).
+static void TestRSDecoderLimits() {
+  const int k = 10, r = 3;
+  auto enc = RSBatchEncoder::New(k, r, 4, 1200);
+  CHECK(enc != nullptr);
+  if (!enc) return;
+  std::vector<Bytes> data, rep;
+  for (int i = 0; i < 2 * k; ++i) {
+    data.push_back(rnd(1200, 7000 + i));
+    CHECK(enc->AddPacket(data.back(), &rep).ok());
+  }
+  CHECK(enc->Flush(&rep).ok() && rep.size() == 6);
+  FECDecoder d;
+  for (int s = 4; s < k; ++s) d.AddPacket(data[s], s, 0);  // 4 of group 0 lost
+  for (int i = 0; i < r; ++i) CHECK(!d.AddRedundancyPacket(rep[i]).first);
+  CHECK(d.GetMetrics().FailedRecoveries > 0 && d.GetMetrics().PacketsRecovered == 0);
+  CHECK(d.GetPacket(0, 0).empty());
+  FECDecoder legacy;  // row 0 only
+  for (int s = 1; s < k; ++s) legacy.AddPacket(data[k + s], s, 1);
+  auto res = legacy.AddRedundancyPacket(rep[3]);
+  CHECK(res.first && legacy.GetPacket(1, 0) == data[k]);
+  FECDecoder legacy2;
+  for (int s = 2; s < k; ++s) legacy2.AddPacket(data[s], s, 0);
+  CHECK(!legacy2.AddRedundancyPacket(rep[0]).first && legacy2.GetMetrics().FailedRecoveries == 1);
+  CHECK(legacy2.AddRedundancyPacket(rep[1]).first);  // row 1 added: both rebuilt
+  CHECK(legacy2.GetPacket(0, 0) == data[0] && legacy2.GetPacket(0, 1) == data[1]);
+}
+
+// Partial last group (count < k) and packets shorter than the symbol: the decoder keeps
+// the reference's symbol-length rule (first packet seen) and recovers that prefix.
+static void TestRSDecoderPartialAndShort() {
+  const int k = 8, r = 2;
+  auto enc = RSBatchEncoder::New(k, r, 4, 256);
+  CHECK(enc != nullptr);
+  if (!enc) return;
+  std::vector<Bytes> data, rep;
+  for (int i = 0; i < 5; ++i) {
+    data.push_back(rnd(100 + 40 * i, 8000 + i));
+    CHECK(enc->AddPacket(data.back(), &rep).ok());
+  }
+  CHECK(enc->Flush(&rep).ok() && rep.size() == 2);
+  FECDecoder d;
+  CHECK(!d.AddRedundancyPacket(rep[1]).first);  // first seen: symbolLen = 260 (largest packet)
+  d.AddPacket(data[1], 1, 0);
+  d.AddPacket(data[3], 3, 0);
+  d.AddPacket(data[4], 4, 0);
+  auto res = d.AddRedundancyPacket(rep[0]);  // 2 of 5 lost, 2 rows: rebuilt now
+  CHECK(res.first && res.second.size() == 2);
+  CHECK(d.GetPacket(0, 0) == padded(data[0], 260) && d.GetPacket(0, 2) == padded(data[2], 260));
+}
+
 int main() {
   TestNewFECEncoder();
   TestAddPacket();
@@ -279,6 +524,12 @@ int main() {
   TestVariableLengthAndFlushMatchGo();
   TestEncodeBatchManyGroups();
   TestBatchRS();
+  TestRSWireHeader();
+  TestRSBatchEncoderMatchesHybridAndOracle();
+  TestRSDecoderImmediate();
+  TestRSDecoderDeferredBatch();
+  TestRSDecoderLimits();
+  TestRSDecoderPartialAndShort();
   if (g_fail) {
     std::printf("FAILED %d of %d checks\n", g_fail, g_checks);
     return 1;
