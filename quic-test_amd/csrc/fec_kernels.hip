@@ -34,6 +34,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kNtLoad = 1;        // non-temporal loads (data read once)
 constexpr int kNtStore = 2;       // non-temporal stores
 constexpr int kNoCoefBranch = 4;  // decode: multiply by every coefficient, no 0/1 branches
+constexpr int kProbeXorOnly = 8;   // probes only: decode_fused XORs instead of multiplying
+constexpr int kProbeNoStore = 16; // probes only: decode_fused never stores (read pattern alone)
+constexpr int kProbeDense = 32;   // probes only: decode_fused reads data shards 0..K-1, no parity
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
@@ -380,13 +383,21 @@ __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, co
 // NM 16-byte pieces and NT 4-byte pieces of every survivor, so every coefficient table is
 // loaded (scalar) and branched on once per wave instead of once per pass.  Packet sizes
 // with NM = P / 1024 and NT = ceil((P % 1024) / 256) matching the instantiation.
-template <int K, int MAXE, int POL, int NM, int NT>
+//
+// DIRECT: the survivor and erased shard ids come from the group's erasure mask (scalar bit
+// scans) instead of the record header, so the survivor loads depend on one scalar load
+// (the mask) rather than two in a chain (rec_off, then the record); the record is then
+// read only for its coefficient tables, behind the data loads.  Same ids in the same order
+// as the record (gf256.hpp build_record: surviving data ascending, then the e lowest
+// surviving parity rows; erased data ascending).
+template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false>
 __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ data,
                                                     const uint8_t* __restrict__ parity,
                                                     const uint32_t* __restrict__ rec_off,
                                                     const uint8_t* __restrict__ codebook,
                                                     uint64_t groups, uint32_t P, uint32_t r, uint32_t m0,
-                                                    uint8_t* __restrict__ out, uint32_t never, uint32_t swz) {
+                                                    uint8_t* __restrict__ out, uint32_t never, uint32_t swz,
+                                                    const uint64_t* __restrict__ masks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];  // see encode_v16
   if (never) occupancy_lds[threadIdx.x] = 0;
   constexpr int NW = 4 * NM + NT;  // dwords per lane and survivor
@@ -398,8 +409,27 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
   if (rec >= kRecBad) return;
   const uint8_t* recp = codebook + static_cast<uint64_t>(rec) * 32u;
   const uint32_t* rw = reinterpret_cast<const uint32_t*>(recp);
-  const uint32_t e = rw[24] & 0xFFu;
-  const bool xor_only = ((rw[24] >> 8) & 0xFFu) != 0;
+  uint32_t e;
+  bool xor_only;
+  // DIRECT: survivor ids (ascending bits of `surv`) and erased ids (bits of `lost`).
+  uint64_t surv = 0, lost = 0;
+  if constexpr (DIRECT) {
+    const uint64_t m = masks[gw];
+    constexpr uint64_t kmask = (1ull << K) - 1;
+    lost = m & kmask;
+    e = static_cast<uint32_t>(__popcll(lost));
+    uint64_t alive = ~(m >> K) & ((r >= 64 ? 0ull : (1ull << r)) - 1);
+    xor_only = e == 1 && (alive & 1u);
+    uint64_t rsel = 0;
+    for (uint32_t t = 0; t < e; ++t) {
+      rsel |= alive & (~alive + 1);
+      alive &= alive - 1;
+    }
+    surv = (~lost & kmask) | (rsel << K);
+  } else {
+    e = rw[24] & 0xFFu;
+    xor_only = ((rw[24] >> 8) & 0xFFu) != 0;
+  }
   if (m0 >= e) return;
   const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
   const uint8_t* dg = data + gw * K * static_cast<uint64_t>(P);
@@ -424,7 +454,10 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
       v[4 * i + 3] = t.w;
     }
 #pragma unroll
-    for (int t = 0; t < NT; ++t) v[4 * NM + t] = *reinterpret_cast<const uint32_t*>(base + toff[t]);
+    for (int t = 0; t < NT; ++t) {
+      if constexpr ((POL & kNtLoad) != 0) v[4 * NM + t] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(base + toff[t]));
+      else v[4 * NM + t] = *reinterpret_cast<const uint32_t*>(base + toff[t]);
+    }
   };
   auto store = [&](uint8_t* base, const uint32_t (&v)[NW]) {
 #pragma unroll
@@ -440,21 +473,43 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
   auto shard = [&](uint32_t sid) {
     return sid < K ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - K) * static_cast<uint64_t>(P);
   };
+  // Survivor slot s -> shard id, and erased slot m -> data shard id.
+  uint32_t sid[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    if constexpr ((POL & kProbeDense) != 0) {
+      sid[s] = static_cast<uint32_t>(s);
+    } else if constexpr (DIRECT) {
+      sid[s] = static_cast<uint32_t>(__builtin_ctzll(surv));
+      surv &= surv - 1;
+    } else {
+      sid[s] = rec_byte(rw, s);
+    }
+  }
+  auto erased = [&](uint32_t m) -> uint32_t {
+    if constexpr (DIRECT) {
+      uint64_t x = lost;
+      for (uint32_t t = 0; t < m; ++t) x &= x - 1;
+      return static_cast<uint32_t>(__builtin_ctzll(x));
+    } else {
+      return rec_byte(rw, 64 + m);
+    }
+  };
   if (xor_only) {  // single data loss rebuilt from parity row 0: the reference XOR
     uint32_t acc[NW] = {};
 #pragma unroll
     for (int s = 0; s < K; ++s) {
       uint32_t v[NW];
-      load(shard(rec_byte(rw, s)), v);
+      load(shard(sid[s]), v);
 #pragma unroll
       for (int q = 0; q < NW; ++q) acc[q] ^= v[q];
     }
-    store(og + rec_byte(rw, 64) * static_cast<uint64_t>(P), acc);
+    store(og + erased(0) * static_cast<uint64_t>(P), acc);
     return;
   }
   uint32_t x[K][NW];
 #pragma unroll
-  for (int s = 0; s < K; ++s) load(shard(rec_byte(rw, s)), x[s]);
+  for (int s = 0; s < K; ++s) load(shard(sid[s]), x[s]);
   uint32_t acc[MAXE][NW];
 #pragma unroll
   for (int m = 0; m < MAXE; ++m)
@@ -473,7 +528,7 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
     for (int m = 0; m < MAXE; ++m) {
       if (m0 + m < e) {
         const Tab& t = tabs[(m0 + m) * K + s];
-        if (t.coef == 1u) {
+        if (((POL & kProbeXorOnly) != 0) || t.coef == 1u) {
 #pragma unroll
           for (int q = 0; q < NW; ++q) acc[m][q] ^= x[s][q];
         } else if (t.coef != 0u) {
@@ -483,9 +538,12 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
       }
     }
   }
+  if constexpr ((POL & kProbeNoStore) != 0) {
+    if (acc[0][0] != 0x9E3779B9u || acc[MAXE - 1][NW - 1] != 0x7F4A7C15u) return;
+  }
 #pragma unroll
   for (int m = 0; m < MAXE; ++m)
-    if (m0 + m < e) store(og + rec_byte(rw, 64 + m0 + m) * static_cast<uint64_t>(P), acc[m]);
+    if (m0 + m < e) store(og + erased(m0 + m) * static_cast<uint64_t>(P), acc[m]);
 }
 
 // One wave per group, so the record is wave-uniform (SGPRs).  A packet is covered by
@@ -782,9 +840,9 @@ uint32_t pick_tile(uint32_t cpp, uint32_t k, uint32_t P) {
   return best;
 }
 
-template <int K, int R, int OFF, bool FIRST>
+// POL: parity is written once and not re-read by this kernel (non-temporal stores).
+template <int K, int R, int OFF, bool FIRST, int POL = kNtStore>
 hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
-  constexpr int POL = kNtStore;  // parity is written once and not re-read by this kernel
   const uint32_t cpp = a.P / 16u;
   const uint32_t tile = pick_tile(cpp, a.k, a.P);
   const uint64_t gchunk = kMaxThreadsPerLaunch / cpp;
@@ -921,7 +979,7 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
   return hipSuccess;
 }
 
-template <int K, int MAXE, int POL, int NM, int NT>
+template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false>
 hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
   const uint32_t passes = (a.r + MAXE - 1) / MAXE;
   const uint32_t smem = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_DECODE_WAVES", kDecodeWavesPerCU), 4);
@@ -932,11 +990,11 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
       const uint64_t bn = (blocks - b0 < (1u << 24)) ? blocks - b0 : (1u << 24);
       const uint64_t g0 = b0 * 4;
       const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
-      hipLaunchKernelGGL((decode_fused<K, MAXE, POL, NM, NT>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
+      hipLaunchKernelGGL((decode_fused<K, MAXE, POL, NM, NT, DIRECT>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                          a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
                          a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u,
-                         decode_swizzle(a, kDecodeFusedXcdSwizzle));
+                         decode_swizzle(a, kDecodeFusedXcdSwizzle), DIRECT ? a.masks + g0 : nullptr);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
@@ -945,10 +1003,12 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
 }
 
 // The fused form for this (k, r, P), if instantiated; hipErrorNotSupported otherwise.
-hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s) {
+hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct) {
   const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
-#define QFEC_FUSED(KK, RR, NMM, NTT) \
-  if (a.k == KK && a.r == RR && nm == NMM && nt == NTT) return run_decode_fused<KK, RR, kNtStore, NMM, NTT>(a, s);
+#define QFEC_FUSED(KK, RR, NMM, NTT)                                                          \
+  if (a.k == KK && a.r == RR && nm == NMM && nt == NTT)                                       \
+    return direct ? run_decode_fused<KK, RR, kNtStore, NMM, NTT, true>(a, s)                  \
+                  : run_decode_fused<KK, RR, kNtStore, NMM, NTT, false>(a, s);
   QFEC_FUSED(10, 3, 1, 1)
   QFEC_FUSED(20, 5, 1, 1)
   QFEC_FUSED(10, 1, 1, 1)
@@ -1015,8 +1075,12 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
   // Fused passes win where many rows share each survivor (k=20 r=5, 5 losses: +21%); with
   // the XCD-aware order they also win at r = 3 (+2.6%; tools/probe_decode.hip), so auto
   // takes them wherever they are instantiated.
-  if (a.variant == kDecodeFused || a.variant == kDecodeAuto) {
-    const hipError_t e = try_decode_fused(a, s);
+  if (a.variant == kDecodeFused || a.variant == kDecodeAuto || a.variant == kDecodeFusedDirect) {
+    // Mask-addressed survivors: +1.2% at k=10 r=3 (tools/probe_decode.hip, r01_probe_decode_direct.txt);
+    // at k=20 r=5 its extra VGPRs cost a wave per SIMD (-30%), so auto takes it for r <= 3 only.
+    const bool direct = (a.variant == kDecodeFusedDirect || (a.variant == kDecodeAuto && a.r <= 3)) &&
+                        a.masks != nullptr && !a.rec_ready;
+    const hipError_t e = try_decode_fused(a, s, direct);
     if (e != hipErrorNotSupported) return e;
   }
   if (a.variant == kDecodeWaveNoBranch && !separate_out) {

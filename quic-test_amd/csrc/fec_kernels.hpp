@@ -54,6 +54,7 @@ constexpr int kDecodeWavePlain = 4;      // one wave per group, 16-B passes + 4-
 constexpr int kDecodeWaveNt = 5;         //   same, non-temporal stores (the default)
 constexpr int kDecodeWaveNoBranch = 6;   //   same, no branch on coefficient 0 / 1
 constexpr int kDecodeFused = 7;          // one wave per group, 16-B and 4-B pieces fused
+constexpr int kDecodeFusedDirect = 8;    //   same, survivor addresses from the erasure mask
 
 struct DecodeLaunch {
   int variant = kDecodeAuto;

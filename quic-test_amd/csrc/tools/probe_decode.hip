@@ -36,7 +36,8 @@ __global__ void poison(uint8_t* data, const uint64_t* masks, uint64_t groups, ui
 using namespace qfec;
 
 int main(int argc, char** argv) {
-  const uint32_t k = argc > 3 ? std::atoi(argv[3]) : 10, r = argc > 4 ? std::atoi(argv[4]) : 3, P = 1200;
+  const uint32_t k = argc > 3 ? std::atoi(argv[3]) : 10, r = argc > 4 ? std::atoi(argv[4]) : 3;
+  const uint32_t P = argc > 6 ? std::atoi(argv[6]) : 1200;
   const uint32_t ners = argc > 5 ? std::atoi(argv[5]) : 2;
   const uint64_t G = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1000000;
   const int rounds = argc > 2 ? std::atoi(argv[2]) : 7;
@@ -110,14 +111,41 @@ int main(int argc, char** argv) {
     int waves;
     int swz;
     std::vector<float> ms;
+    std::function<hipError_t(const DecodeLaunch&)> fn = nullptr;  // custom launch (no check)
   };
-  std::vector<Var> vars = {{"wave-per-group v16", kDecodeWavePerGroup, -1, 0, {}},
-                           {"wave nt", kDecodeWaveNt, -1, 0, {}},
-                           {"wave nt xcd", kDecodeWaveNt, -1, 1, {}},
+  std::vector<Var> vars = {{"wave nt xcd", kDecodeWaveNt, -1, 1, {}},
                            {"auto (library default)", kDecodeAuto, 0, -1, {}},
-                           {"fused nt", kDecodeFused, -1, 0, {}},
-                           {"fused nt xcd", kDecodeFused, -1, 1, {}}};
+                           {"fused nt xcd", kDecodeFused, -1, 1, {}},
+                           {"direct xcd", kDecodeFusedDirect, -1, 1, {}},
+                           {"direct xcd cap16", kDecodeFusedDirect, 16, 1, {}},
+                           {"direct", kDecodeFusedDirect, -1, 0, {}}};
+  auto probe = [](const DecodeLaunch& a) -> hipError_t {
+    hipLaunchKernelGGL(classify, dim3(blocks_for(a.groups)), dim3(256), 0, nullptr, a.masks, a.groups, a.k, a.r,
+                       a.binom, a.meta, a.rec_off, a.status);
+    return hipSuccess;
+  };
+#define PV(NAME, CAP, POLX, NM, NT)                                                              \
+  vars.push_back({NAME, kDecodeFused, CAP, 1, {}, [probe](const DecodeLaunch& a) {               \
+                    probe(a);                                                                    \
+                    return run_decode_fused<10, 3, kNtStore | (POLX), NM, NT>(a, nullptr);       \
+                  }});
+#define PSET(NM, NT)                                                                             \
+  PV("xor-only math", -1, kProbeXorOnly, NM, NT)                                                 \
+  PV("reads only (xor)", -1, kProbeNoStore | kProbeXorOnly, NM, NT)                              \
+  PV("reads dense", -1, kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)                     \
+  PV("reads dense cap8", 8, kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)                 \
+  PV("reads dense cap12", 12, kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)               \
+  PV("reads dense cap16", 16, kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)               \
+  PV("reads dense nt-load", -1, kNtLoad | kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)
+  if (k == 10 && r == 3 && P == 1200) {
+    PSET(1, 1)
+  } else if (k == 10 && r == 3 && P == 1024) {
+    PSET(1, 0)
+  } else if (k == 10 && r == 3 && P == 2048) {
+    PSET(2, 0)
+  }
   for (auto& v : vars) {
+    if (v.fn) continue;
     dl.variant = v.variant;
     dl.waves_per_cu = v.waves;
     dl.xcd_swizzle = v.swz;
@@ -138,7 +166,7 @@ int main(int argc, char** argv) {
       dl.waves_per_cu = v.waves;
       dl.xcd_swizzle = v.swz;
       CK(hipEventRecord(e0));
-      CK(launch_decode(dl, nullptr));
+      CK(v.fn ? v.fn(dl) : launch_decode(dl, nullptr));
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;

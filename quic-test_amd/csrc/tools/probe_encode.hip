@@ -472,6 +472,13 @@ int main(int argc, char** argv) {
     el.tables = dtab;
     el.vec16 = true;
     vars.push_back({"enc prod launch_encode", enc_bytes, [=] { CK(launch_encode(el, nullptr)); }, {}});
+    for (int w : {5, 10, 15, 20, 40}) {
+      EncodeLaunch e2 = el;
+      e2.waves_per_cu = w;
+      vars.push_back({"enc prod nt-load cap" + std::to_string(w), enc_bytes, [=] {
+                        CK((run_encode_v16<10, 3, 0, true, kNtStore | kNtLoad>(e2, 0, nullptr)));
+                      }, {}});
+    }
   }
 #define LDSV(POL)                                                                                    \
   vars.push_back({"enc_lds<pol" #POL ">", enc_bytes, [&] {                                            \
@@ -493,6 +500,21 @@ int main(int argc, char** argv) {
     vars.push_back({"mix_stream 10:3", nd + nd * 3 / 10, [=] {
                       mix_stream<<<(n + 255) / 256, 256>>>((const u32x4*)data, (u32x4*)scratch, n);
                     }, {}});
+  }
+  if (argc > 3) {  // keep only the variants whose name contains one of the '|'-separated filters
+    const std::string f = argv[3];
+    std::vector<Var> keep;
+    for (auto& v : vars) {
+      size_t p0 = 0;
+      bool hit = false;
+      while (p0 <= f.size()) {
+        const size_t p1 = std::min(f.find('|', p0), f.size());
+        if (p1 > p0 && v.name.find(f.substr(p0, p1 - p0)) != std::string::npos) hit = true;
+        p0 = p1 + 1;
+      }
+      if (hit) keep.push_back(v);
+    }
+    vars.swap(keep);
   }
   hipEvent_t a, b;
   CK(hipEventCreate(&a));

@@ -148,6 +148,25 @@ int main() {
         if (off % 32) return fail("align", k, r, int(g));
         const uint8_t* rec = &book[off];
         if (rec[96] != e) return fail("record-e", k, r, int(g));
+        // decode_fused<..., DIRECT>: survivor / erased ids from the mask must be the record's
+        {
+          const uint64_t lost = masks[g] & kmask;
+          uint64_t alive = ~(masks[g] >> k) & rmask, rsel = 0;
+          for (uint32_t t = 0; t < e; ++t) {
+            rsel |= alive & (~alive + 1);
+            alive &= alive - 1;
+          }
+          uint64_t surv = (~lost & kmask) | (rsel << k);
+          for (uint32_t s = 0; s < k; ++s) {
+            if (uint32_t(__builtin_ctzll(surv)) != rec[s]) return fail("direct-survivor", k, r, int(g));
+            surv &= surv - 1;
+          }
+          uint64_t x = lost;
+          for (uint32_t m = 0; m < e; ++m, x &= x - 1)
+            if (uint32_t(__builtin_ctzll(x)) != rec[64 + m]) return fail("direct-erased", k, r, int(g));
+          const bool xor_only = e == 1 && ((~(masks[g] >> k) & rmask) & 1u);
+          if (xor_only != (rec[97] != 0)) return fail("direct-xor-only", k, r, int(g));
+        }
         const CoefEntry* T = reinterpret_cast<const CoefEntry*>(rec + qfec::kRecordHeader);
         for (uint32_t b = 0; b < P; b += 4)
           for (uint32_t m = 0; m < e; ++m) {
