@@ -19,6 +19,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -113,6 +114,67 @@ struct DecodePlan {
 
 constexpr uint64_t kCodebookCap = 2ull << 30;  // 2 GiB of recovery tables per (k, r)
 
+// Grow-only page-locked host buffer (staging for the compacted host decode).
+struct HostBuf {
+  void* ptr = nullptr;
+  size_t cap = 0;
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  ~HostBuf() { release(); }
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    release();
+    const size_t want = bytes < 4096 ? 4096 : bytes;
+    const hipError_t e = hipHostMalloc(&ptr, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      ptr = nullptr;
+      return e;
+    }
+    cap = want;
+    return hipSuccess;
+  }
+  void release() {
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(ptr); }
+};
+
+// Host threads for the CPU side of the host-resident paths (gathering / scattering
+// packets): QUICFEC_HOST_THREADS, default 8, at most the machine's.
+unsigned host_threads() {
+  static const unsigned n = [] {
+    unsigned hw = std::thread::hardware_concurrency();
+    if (hw == 0) hw = 1;
+    unsigned want = 8;
+    if (const char* v = std::getenv("QUICFEC_HOST_THREADS")) {
+      const int x = std::atoi(v);
+      if (x > 0) want = static_cast<unsigned>(x);
+    }
+    return want < hw ? want : hw;
+  }();
+  return n;
+}
+
+// f(begin, end) over [0, n) split across host_threads() threads (inline when small).
+template <class F>
+void parallel_for(uint64_t n, uint64_t min_per_thread, F&& f) {
+  uint64_t nt = host_threads();
+  if (min_per_thread > 0 && n / min_per_thread < nt) nt = n / min_per_thread;
+  if (nt <= 1) {
+    f(uint64_t(0), n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  for (uint64_t t = 1; t < nt; ++t) th.emplace_back([&f, n, nt, t] { f(n * t / nt, n * (t + 1) / nt); });
+  f(uint64_t(0), n / nt);
+  for (auto& x : th) x.join();
+}
+
 enum class Mem { kHost, kPinned, kDevice };
 
 Mem classify_ptr(const void* p) {
@@ -135,9 +197,21 @@ Mem classify_ptr(const void* p) {
 struct PipeSlot {
   hipStream_t s = nullptr;
   DevBuf in, par, mask, status, rec;
+  HostBuf h_in, h_par, h_mask;          // compacted host decode staging
+  std::vector<uint64_t> h_groups;        // the groups gathered into this slot's staging
 };
 constexpr int kPipeSlots = 3;
 constexpr uint64_t kPipeChunkBytes = 64ull << 20;  // data bytes per pipelined chunk
+
+// QUICFEC_PIPE_CHUNK_BYTES overrides the chunk size (tests use small chunks to run many).
+uint64_t pipe_chunk_bytes() {
+  const char* v = std::getenv("QUICFEC_PIPE_CHUNK_BYTES");
+  const long long x = v ? std::atoll(v) : 0;
+  return x > 0 ? static_cast<uint64_t>(x) : kPipeChunkBytes;
+}
+// Host-resident decode moves only the groups to rebuild when they are at most 1 in
+// kCompactMaxShare of the batch; above that the whole batch streams through the pipeline.
+constexpr uint64_t kCompactMaxShare = 2;
 
 struct FECEncoderCtx {
   double redundancy = 0.10;
@@ -169,6 +243,9 @@ struct FECEncoderCtx {
       p.mask.release();
       p.status.release();
       p.rec.release();
+      p.h_in.release();
+      p.h_par.release();
+      p.h_mask.release();
       if (p.s) (void)hipStreamDestroy(p.s);
     }
     enc_plans.clear();
@@ -365,7 +442,7 @@ int encode_host_pipelined(FECEncoderCtx* ctx, const uint8_t* data, uint64_t G, u
   int rc = ensure_pipe(ctx);
   if (rc != FEC_OK) return rc;
   const uint64_t in_g = uint64_t(k) * P, out_g = uint64_t(r) * P;
-  uint64_t cg = kPipeChunkBytes / in_g;
+  uint64_t cg = pipe_chunk_bytes() / in_g;
   cg = cg == 0 ? 1 : (cg > G ? G : cg);
   for (auto& p : ctx->pipe) {
     QFEC_HIP(p.in.ensure(cg * in_g));
@@ -391,7 +468,7 @@ int decode_host_pipelined(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
   int rc = ensure_pipe(ctx);
   if (rc != FEC_OK) return rc;
   const uint64_t in_g = uint64_t(k) * P, par_g = uint64_t(r) * P;
-  uint64_t cg = kPipeChunkBytes / in_g;
+  uint64_t cg = pipe_chunk_bytes() / in_g;
   cg = cg == 0 ? 1 : (cg > G ? G : cg);
   for (auto& p : ctx->pipe) {
     QFEC_HIP(p.in.ensure(cg * in_g));
@@ -426,6 +503,85 @@ int decode_host_pipelined(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
     QFEC_HIP(hipMemcpyAsync(status_out + g0, sl.status.ptr, n, hipMemcpyDeviceToHost, sl.s));
   }
   for (auto& p : ctx->pipe) QFEC_HIP(hipStreamSynchronize(p.s));
+  return FEC_OK;
+}
+
+// Host-resident decode when few groups lost data shards (e.g. the satellite profile, iid
+// loss p = 0.01: ~11% of k=10 r=3 groups): only those groups cross PCIe.  Per chunk, host
+// threads gather the groups' data and parity into page-locked staging, the chunk goes
+// H2D -> decode -> D2H on its pipeline slot, and the rebuilt packets are scattered back
+// into `data`.  Slot c % 3's previous chunk is scattered before its staging is refilled,
+// so the CPU gather of one chunk overlaps the copies and kernels of the two before it.
+// `need` lists the groups with lost data that are recoverable (status 0); everything
+// else needs no device work.
+int decode_host_compacted(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* parity, const uint64_t* masks,
+                          const std::vector<uint64_t>& need, uint32_t k, uint32_t r, uint32_t P) {
+  int rc = ensure_pipe(ctx);
+  if (rc != FEC_OK) return rc;
+  const uint64_t N = need.size();
+  const uint64_t in_g = uint64_t(k) * P, par_g = uint64_t(r) * P;
+  uint64_t cg = pipe_chunk_bytes() / in_g;
+  cg = cg == 0 ? 1 : (cg > N ? N : cg);
+  for (auto& p : ctx->pipe) {
+    QFEC_HIP(p.in.ensure(cg * in_g));
+    QFEC_HIP(p.par.ensure(cg * par_g));
+    QFEC_HIP(p.mask.ensure(cg * 8));
+    QFEC_HIP(p.h_in.ensure(cg * in_g));
+    QFEC_HIP(p.h_par.ensure(cg * par_g));
+    QFEC_HIP(p.h_mask.ensure(cg * 8));
+    p.h_groups.clear();
+  }
+  const uint64_t kmask = (1ull << k) - 1;
+  // Rebuilt packets of the slot's last chunk: D2H landed in h_in; copy the erased ones out.
+  auto scatter = [&](PipeSlot& sl) -> int {
+    if (sl.h_groups.empty()) return FEC_OK;
+    QFEC_HIP(hipStreamSynchronize(sl.s));
+    const uint8_t* src = sl.h_in.as<uint8_t>();
+    const uint64_t* gl = sl.h_groups.data();
+    parallel_for(sl.h_groups.size(), 512, [&](uint64_t b, uint64_t e) {
+      for (uint64_t i = b; i < e; ++i) {
+        const uint64_t g = gl[i];
+        for (uint64_t lost = masks[g] & kmask; lost; lost &= lost - 1) {
+          const uint32_t j = static_cast<uint32_t>(__builtin_ctzll(lost));
+          std::memcpy(data + g * in_g + uint64_t(j) * P, src + i * in_g + uint64_t(j) * P, P);
+        }
+      }
+    });
+    sl.h_groups.clear();
+    return FEC_OK;
+  };
+  const bool vec16 = (P % 16u) == 0;
+  uint64_t c = 0;
+  for (uint64_t i0 = 0; i0 < N; i0 += cg, ++c) {
+    PipeSlot& sl = ctx->pipe[c % kPipeSlots];
+    rc = scatter(sl);
+    if (rc != FEC_OK) return rc;
+    const uint64_t n = (N - i0 < cg) ? N - i0 : cg;
+    const uint64_t* gl = need.data() + i0;
+    uint8_t* hi = sl.h_in.as<uint8_t>();
+    uint8_t* hp = sl.h_par.as<uint8_t>();
+    uint64_t* hm = sl.h_mask.as<uint64_t>();
+    parallel_for(n, 512, [&](uint64_t b, uint64_t e) {
+      for (uint64_t i = b; i < e; ++i) {
+        const uint64_t g = gl[i];
+        std::memcpy(hi + i * in_g, data + g * in_g, in_g);
+        std::memcpy(hp + i * par_g, parity + g * par_g, par_g);
+        hm[i] = masks[g];
+      }
+    });
+    sl.h_groups.assign(gl, gl + n);
+    QFEC_HIP(hipMemcpyAsync(sl.in.ptr, hi, n * in_g, hipMemcpyHostToDevice, sl.s));
+    QFEC_HIP(hipMemcpyAsync(sl.par.ptr, hp, n * par_g, hipMemcpyHostToDevice, sl.s));
+    QFEC_HIP(hipMemcpyAsync(sl.mask.ptr, hm, n * 8, hipMemcpyHostToDevice, sl.s));
+    rc = decode_dev_locked(ctx, sl.in.as<uint8_t>(), sl.par.as<uint8_t>(), sl.mask.as<uint64_t>(), n, k, r, P,
+                           nullptr, vec16, sl.s, &sl.rec);
+    if (rc != FEC_OK) return rc;
+    QFEC_HIP(hipMemcpyAsync(hi, sl.in.ptr, n * in_g, hipMemcpyDeviceToHost, sl.s));
+  }
+  for (auto& p : ctx->pipe) {
+    rc = scatter(p);
+    if (rc != FEC_OK) return rc;
+  }
   return FEC_OK;
 }
 
@@ -769,13 +925,32 @@ QFEC_EXPORT int fec_decode_batch_rs(FECEncoderCtx* ctx, uint8_t* data, const uin
       st_local.resize(G);
       st = st_local.data();
     }
-    rc = decode_host_pipelined(ctx, data, parity, masks, G, k, r, P, st);
-    if (rc != FEC_OK) return rc;
-    if (unrecoverable_out) {
-      uint64_t bad = 0;
-      for (uint64_t g = 0; g < G; ++g) bad += st[g] != 0;
-      *unrecoverable_out = bad;
+    // Which groups need work: lost data shards, and no more than the surviving parity rows
+    // (the classify rule, fec_kernels.hip); status is known on the host from the masks.
+    const uint64_t kmask = (1ull << k) - 1, rmask = (r >= 64) ? ~0ull : ((1ull << r) - 1);
+    std::vector<uint64_t> need;
+    uint64_t bad = 0;
+    for (uint64_t g = 0; g < G; ++g) {
+      const uint64_t m = masks[g];
+      const uint32_t e = static_cast<uint32_t>(__builtin_popcountll(m & kmask));
+      const uint32_t alive = r - static_cast<uint32_t>(__builtin_popcountll((m >> k) & rmask));
+      const bool unrec = e > 0 && e > alive;
+      bad += unrec;
+      if (e > 0 && !unrec) need.push_back(g);
     }
+    if (need.size() * kCompactMaxShare <= G) {
+      // few groups to rebuild: move only those (statuses from the host scan)
+      for (uint64_t g = 0; g < G; ++g) {
+        const uint64_t m = masks[g];
+        const uint32_t e = static_cast<uint32_t>(__builtin_popcountll(m & kmask));
+        st[g] = (e > 0 && e > r - static_cast<uint32_t>(__builtin_popcountll((m >> k) & rmask))) ? 1 : 0;
+      }
+      if (!need.empty()) rc = decode_host_compacted(ctx, data, parity, masks, need, k, r, P);
+    } else {
+      rc = decode_host_pipelined(ctx, data, parity, masks, G, k, r, P, st);
+    }
+    if (rc != FEC_OK) return rc;
+    if (unrecoverable_out) *unrecoverable_out = bad;
     return FEC_OK;
   }
   uint8_t* d_data = data;

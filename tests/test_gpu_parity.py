@@ -257,6 +257,39 @@ def test_host_pipeline_multi_chunk(gpu_ctx, oracle_mod, torch_cuda, pinned):
     assert np.array_equal(hb, ref)
 
 
+@pytest.mark.parametrize("k,r,P,pinned", [(10, 3, 1200, True), (10, 3, 1200, False), (20, 5, 96, False),
+                                          (10, 3, 100, True), (4, 2, 256, False)])
+def test_host_decode_compacted_sparse_loss(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, k, r, P, pinned):
+    """Host-resident decode under iid loss (satellite profile, network_profiles.go:78): at most
+    half the groups need work, so only those cross PCIe (gathered, decoded, scattered back).
+    Small pipeline chunks so the 3 slots rotate several times; some groups unrecoverable."""
+    G = 6_000
+    monkeypatch.setenv("QUICFEC_PIPE_CHUNK_BYTES", str(k * P * 97))
+    data = oracle_mod.splitmix_bytes(G * k * P, SEED + 21 + k + P)
+    par = oracle_mod.rs_encode(data, G, k, r, P, nthreads=8)
+    rng = np.random.default_rng(k * 7 + P)
+    w = np.left_shift(np.uint64(1), np.arange(k + r, dtype=np.uint64))
+    masks = ((rng.random((G, k + r)) < 0.02) * w).sum(axis=1, dtype=np.uint64)
+    masks[rng.integers(0, G, size=9)] = np.uint64((1 << (r + 1)) - 1)   # r+1 data shards lost
+    masks[5] = np.uint64(0)
+    broken = _poison(data, masks, G, k, P)
+    ref = broken.copy()
+    bad_exp, st_exp = oracle_mod.rs_decode(ref, par, masks, G, k, r, P, nthreads=8)
+    assert 0 < bad_exp and (st_exp == 0).sum() > 0
+    if pinned:
+        hb = torch_cuda.from_numpy(broken).pin_memory()
+        hp = torch_cuda.from_numpy(par).pin_memory()
+        st = np.zeros(G, dtype=np.uint8)
+        bad = gpu_ctx.decode(hb, hp, masks, k, r, P, status_out=st, num_groups=G)
+        got = hb.numpy()
+    else:
+        got, st = broken.copy(), np.zeros(G, dtype=np.uint8)
+        bad = gpu_ctx.decode(got, par, masks, k, r, P, status_out=st)
+    assert bad == bad_exp
+    assert np.array_equal(st, st_exp)
+    assert np.array_equal(got, ref)
+
+
 def test_fill_random_matches_oracle(gpu_ctx, oracle_mod, torch_cuda):
     for n, off in ((4096, 0), (1000, 8), (777, 3)):
         d = torch_cuda.zeros(n + 16, dtype=torch_cuda.uint8, device="cuda")
