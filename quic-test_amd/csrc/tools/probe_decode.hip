@@ -38,6 +38,7 @@ using namespace qfec;
 int main(int argc, char** argv) {
   const uint32_t k = argc > 3 ? std::atoi(argv[3]) : 10, r = argc > 4 ? std::atoi(argv[4]) : 3;
   const uint32_t P = argc > 6 ? std::atoi(argv[6]) : 1200;
+  const double loss = argc > 7 ? std::atof(argv[7]) : 0.0;  // > 0: iid loss per shard instead
   const uint32_t ners = argc > 5 ? std::atoi(argv[5]) : 2;
   const uint64_t G = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1000000;
   const int rounds = argc > 2 ? std::atoi(argv[2]) : 7;
@@ -70,10 +71,19 @@ int main(int argc, char** argv) {
   uint64_t alg = 0;
   for (uint64_t g = 0; g < G; ++g) {
     uint64_t m = 0;
-    while (uint32_t(__builtin_popcountll(m)) < ners) m |= 1ull << (rng() % (k + r));
+    if (loss > 0) {  // resampled until recoverable, so every poisoned group is rebuilt
+      do {
+        m = 0;
+        for (uint32_t j = 0; j < k + r; ++j)
+          if (double(rng() >> 11) * 0x1.0p-53 < loss) m |= 1ull << j;
+      } while (uint32_t(__builtin_popcountll(m & ((1ull << k) - 1))) > r - uint32_t(__builtin_popcountll((m >> k) & ((1ull << r) - 1))));
+    } else {
+      while (uint32_t(__builtin_popcountll(m)) < ners) m |= 1ull << (rng() % (k + r));
+    }
     hm[g] = m;
     const uint32_t e = __builtin_popcountll(m & ((1ull << k) - 1));
-    if (e) alg += uint64_t(k + e) * P;
+    const uint32_t alive = r - __builtin_popcountll((m >> k) & ((1ull << r) - 1));
+    if (e && e <= alive) alg += uint64_t(k + e) * P;
   }
   CK(hipMemcpy(masks, hm.data(), G * 8, hipMemcpyHostToDevice));
   CodebookLayout L;
@@ -119,6 +129,12 @@ int main(int argc, char** argv) {
                            {"direct xcd", kDecodeFusedDirect, -1, 1, {}},
                            {"direct xcd cap16", kDecodeFusedDirect, 16, 1, {}},
                            {"direct", kDecodeFusedDirect, -1, 0, {}}};
+  if (loss > 0) {  // sparse-loss runs: the library forms only
+    std::vector<Var> keep;
+    for (auto& v : vars)
+      if (v.name.rfind("auto", 0) == 0 || v.name.rfind("direct xcd", 0) == 0) keep.push_back(v);
+    vars.swap(keep);
+  }
   auto probe = [](const DecodeLaunch& a) -> hipError_t {
     hipLaunchKernelGGL(classify, dim3(blocks_for(a.groups)), dim3(256), 0, nullptr, a.masks, a.groups, a.k, a.r,
                        a.binom, a.meta, a.rec_off, a.status);
@@ -165,7 +181,7 @@ int main(int argc, char** argv) {
       dl.variant = v.variant;
       dl.waves_per_cu = v.waves;
       dl.xcd_swizzle = v.swz;
-      CK(hipEventRecord(e0));
+        CK(hipEventRecord(e0));
       CK(v.fn ? v.fn(dl) : launch_decode(dl, nullptr));
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
