@@ -26,14 +26,17 @@ struct EncodeLaunch {
 // Tuned occupancy caps (waves per CU) of the streaming kernels: fewer concurrent waves
 // than the hardware allows keep the HBM request stream more local and measured faster
 // (tools/probe_encode.hip, tools/probe_decode.hip).
-constexpr int kEncodeWavesPerCU = 10;  // 2 workgroups of 5 waves; measured 5.70 vs 5.26 TB/s uncapped
+// Encode: 2 workgroups per CU (k=10/1200 B: 2 x 5 waves, 5.70 vs 5.26 TB/s uncapped;
+// 1024 B: 2 x 4 waves 6.12 vs 5.92 at 3; 1216 B: 2 x 6 waves 5.92 vs 5.25 at 1).
+constexpr int kEncodeBlocksPerCU = 2;
 constexpr int kDecodeWavesPerCU = 0;   // measured: any cap below ~20 waves/CU is slower
 
 // Dynamic LDS bytes that cap a workgroup of `waves_per_block` waves at about
 // `waves_per_cu` waves per CU (160 KiB LDS per CU); 0 = no cap.
 inline uint32_t occupancy_cap_lds(int waves_per_cu, uint32_t waves_per_block) {
   if (waves_per_cu <= 0 || waves_per_block == 0) return 0;
-  uint32_t blocks = static_cast<uint32_t>(waves_per_cu) / waves_per_block;
+  // nearest whole number of workgroups (a 6-wave workgroup under a 10-wave cap gets 2, not 1)
+  uint32_t blocks = (static_cast<uint32_t>(waves_per_cu) + waves_per_block / 2) / waves_per_block;
   if (blocks == 0) blocks = 1;
   if (blocks * waves_per_block >= 32) return 0;
   return 160u * 1024u / (blocks + 1) + 16u;

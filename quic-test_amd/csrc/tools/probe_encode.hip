@@ -377,7 +377,7 @@ __global__ __launch_bounds__(((2 * T * 75 + 63) / 64) * 64) void enc_pair(const 
 using namespace qfec;
 
 int main(int argc, char** argv) {
-  const uint32_t k = 10, r = 3, P = 1200;
+  const uint32_t k = 10, r = 3, P = argc > 4 ? std::atoi(argv[4]) : 1200;
   const uint64_t G = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 1000000;
   const int rounds = argc > 2 ? std::atoi(argv[2]) : 7;
   const uint64_t nd = G * k * P, np = G * r * P;
@@ -478,6 +478,11 @@ int main(int argc, char** argv) {
       vars.push_back({"enc prod nt-load cap" + std::to_string(w), enc_bytes, [=] {
                         CK((run_encode_v16<10, 3, 0, true, kNtStore | kNtLoad>(e2, 0, nullptr)));
                       }, {}});
+    }
+    for (int w : {6, 8, 10, 12, 16, 20}) {
+      EncodeLaunch e2 = el;
+      e2.waves_per_cu = w;
+      vars.push_back({"enc prod cap" + std::to_string(w), enc_bytes, [=] { CK(launch_encode(e2, nullptr)); }, {}});
     }
   }
 #define LDSV(POL)                                                                                    \
