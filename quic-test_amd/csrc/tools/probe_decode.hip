@@ -160,6 +160,21 @@ int main(int argc, char** argv) {
   } else if (k == 10 && r == 3 && P == 2048) {
     PSET(2, 0)
   }
+  if (std::getenv("PROBE_FILTER")) {  // keep variants whose name contains one of '|'-separated words
+    const std::string f = std::getenv("PROBE_FILTER");
+    std::vector<Var> keep;
+    for (auto& v : vars) {
+      size_t p0 = 0;
+      bool hit = false;
+      while (p0 <= f.size()) {
+        const size_t p1 = std::min(f.find('|', p0), f.size());
+        if (p1 > p0 && v.name.find(f.substr(p0, p1 - p0)) != std::string::npos) hit = true;
+        p0 = p1 + 1;
+      }
+      if (hit) keep.push_back(v);
+    }
+    vars.swap(keep);
+  }
   for (auto& v : vars) {
     if (v.fn) continue;
     dl.variant = v.variant;
