@@ -101,6 +101,30 @@ int fec_fill_random_dev(FECEncoderCtx* ctx, uint8_t* d_dst, uint64_t nbytes, uin
 /* Wait for the context's own stream. */
 int fec_synchronize(FECEncoderCtx* ctx);
 
+/* ---- device groups: one host batch sharded over several GPUs ----
+ * Groups are independent: shard i of n takes groups [G*i/n, G*(i+1)/n) on its own
+ * context (device, streams, staging buffers) from its own host thread; no data moves
+ * between devices.  Host buffers only (page-locked ones from
+ * fec_alloc_slab stream at DMA rate); a device buffer gives FEC_ERR_RANGE.  Return codes
+ * as the single-context calls; on failure fec_hip_last_error() names the shard. */
+typedef struct FECDeviceGroup FECDeviceGroup;
+
+/* devices: ordinals to use (repeats allowed), or NULL / ndevices <= 0 for every visible
+ * device.  NULL when no GPU is usable or an ordinal is out of range. */
+FECDeviceGroup* fec_group_new(const int* devices, int ndevices);
+void fec_group_free(FECDeviceGroup* group);
+int fec_group_size(const FECDeviceGroup* group);
+/* Context of shard i (for device-resident work on that GPU), NULL if out of range. */
+FECEncoderCtx* fec_group_context(FECDeviceGroup* group, int i);
+
+int fec_group_encode_batch_rs(FECDeviceGroup* group, const uint8_t* data, uint64_t num_groups,
+                              uint32_t k, uint32_t r, uint32_t packet_size, uint8_t* parity_out);
+
+int fec_group_decode_batch_rs(FECDeviceGroup* group, uint8_t* data, const uint8_t* parity,
+                              const uint64_t* erasure_masks, uint64_t num_groups, uint32_t k,
+                              uint32_t r, uint32_t packet_size, uint8_t* status_out,
+                              uint64_t* unrecoverable_out);
+
 #ifdef __cplusplus
 }
 #endif

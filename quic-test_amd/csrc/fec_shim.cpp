@@ -1051,3 +1051,129 @@ QFEC_EXPORT int fec_synchronize(FECEncoderCtx* ctx) {
   QFEC_HIP(hipStreamSynchronize(ctx->stream));
   return FEC_OK;
 }
+
+// ---------------------------------------------------------------------------------
+// Device groups: one host batch sharded over several GPUs.  Groups
+// are independent, so shard i of n takes the contiguous range [G*i/n, G*(i+1)/n) and
+// runs on its own context (device, streams, staging) from its own host thread; there is
+// no exchange between devices.
+// ---------------------------------------------------------------------------------
+struct FECDeviceGroup {
+  std::vector<FECEncoderCtx*> ctxs;
+  ~FECDeviceGroup() {
+    for (auto* c : ctxs) delete c;
+  }
+};
+
+namespace {
+
+// Run f(i, g0, n) for every shard, shard 0 on the calling thread; the first failing
+// shard's code and message become the caller's.
+template <class F>
+int for_each_shard(FECDeviceGroup* grp, uint64_t G, F&& f) {
+  const uint64_t n = grp->ctxs.size();
+  std::vector<int> rc(n, FEC_OK);
+  std::vector<std::string> msg(n);
+  auto run = [&](uint64_t i) {
+    const uint64_t g0 = G * i / n, g1 = G * (i + 1) / n;
+    if (g1 > g0) rc[i] = f(i, g0, g1 - g0);
+    if (rc[i] != FEC_OK) msg[i] = g_last_error;
+  };
+  std::vector<std::thread> th;
+  for (uint64_t i = 1; i < n; ++i) th.emplace_back(run, i);
+  run(0);
+  for (auto& t : th) t.join();
+  for (uint64_t i = 0; i < n; ++i)
+    if (rc[i] != FEC_OK) {
+      g_last_error = "shard " + std::to_string(i) + " (device " + std::to_string(grp->ctxs[i]->device) +
+                     "): " + msg[i];
+      return rc[i];
+    }
+  return FEC_OK;
+}
+
+bool any_device_ptr(std::initializer_list<const void*> ps) {
+  for (const void* p : ps)
+    if (p && classify_ptr(p) == Mem::kDevice) return true;
+  return false;
+}
+
+}  // namespace
+
+QFEC_EXPORT FECDeviceGroup* fec_group_new(const int* devices, int ndevices) {
+  const int n = fec_hip_device_count();
+  if (n <= 0) {
+    set_error("fec_group_new: no HIP device available");
+    return nullptr;
+  }
+  std::vector<int> devs;
+  if (!devices || ndevices <= 0) {
+    for (int d = 0; d < n; ++d) devs.push_back(d);
+  } else {
+    for (int i = 0; i < ndevices; ++i) {
+      if (devices[i] < 0 || devices[i] >= n) {
+        set_error("fec_group_new: device %d out of range (%d devices)", devices[i], n);
+        return nullptr;
+      }
+      devs.push_back(devices[i]);
+    }
+  }
+  auto* grp = new FECDeviceGroup();
+  for (int d : devs) {
+    FECEncoderCtx* c = make_ctx(0.10, 1024, d);
+    if (!c) {
+      delete grp;
+      return nullptr;
+    }
+    grp->ctxs.push_back(c);
+  }
+  return grp;
+}
+
+QFEC_EXPORT void fec_group_free(FECDeviceGroup* grp) { delete grp; }
+
+QFEC_EXPORT int fec_group_size(const FECDeviceGroup* grp) { return grp ? static_cast<int>(grp->ctxs.size()) : 0; }
+
+QFEC_EXPORT FECEncoderCtx* fec_group_context(FECDeviceGroup* grp, int i) {
+  if (!grp || i < 0 || i >= static_cast<int>(grp->ctxs.size())) return nullptr;
+  return grp->ctxs[i];
+}
+
+QFEC_EXPORT int fec_group_encode_batch_rs(FECDeviceGroup* grp, const uint8_t* data, uint64_t G, uint32_t k,
+                                          uint32_t r, uint32_t P, uint8_t* parity_out) {
+  if (!grp || !data || !parity_out) return FEC_ERR_NULL;
+  int rc = check_shape(G, k, r, P, false);
+  if (rc != FEC_OK) return rc;
+  if (G == 0) return FEC_OK;
+  if (any_device_ptr({data, parity_out})) {
+    set_error("fec_group_encode_batch_rs: host buffers only (device buffers belong to one context)");
+    return FEC_ERR_RANGE;
+  }
+  return for_each_shard(grp, G, [&](uint64_t i, uint64_t g0, uint64_t n) {
+    return fec_encode_batch_rs(grp->ctxs[i], data + g0 * k * uint64_t(P), nullptr, n, k, r, P,
+                               parity_out + g0 * r * uint64_t(P));
+  });
+}
+
+QFEC_EXPORT int fec_group_decode_batch_rs(FECDeviceGroup* grp, uint8_t* data, const uint8_t* parity,
+                                          const uint64_t* masks, uint64_t G, uint32_t k, uint32_t r,
+                                          uint32_t P, uint8_t* status_out, uint64_t* unrecoverable_out) {
+  if (!grp || !data || !parity || !masks) return FEC_ERR_NULL;
+  int rc = check_shape(G, k, r, P, true);
+  if (rc != FEC_OK) return rc;
+  if (unrecoverable_out) *unrecoverable_out = 0;
+  if (G == 0) return FEC_OK;
+  if (any_device_ptr({data, parity, masks, status_out})) {
+    set_error("fec_group_decode_batch_rs: host buffers only (device buffers belong to one context)");
+    return FEC_ERR_RANGE;
+  }
+  std::vector<uint64_t> bad(grp->ctxs.size(), 0);
+  rc = for_each_shard(grp, G, [&](uint64_t i, uint64_t g0, uint64_t n) {
+    return fec_decode_batch_rs(grp->ctxs[i], data + g0 * k * uint64_t(P), parity + g0 * r * uint64_t(P),
+                               masks + g0, n, k, r, P, status_out ? status_out + g0 : nullptr, &bad[i]);
+  });
+  if (rc != FEC_OK) return rc;
+  if (unrecoverable_out)
+    for (uint64_t b : bad) *unrecoverable_out += b;
+  return FEC_OK;
+}

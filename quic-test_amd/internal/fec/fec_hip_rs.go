@@ -127,3 +127,106 @@ func (c *RSCodec) Close() error {
 	}
 	return nil
 }
+
+// RSDeviceGroup is an RSCodec over several GPUs of one node: each batch is split into
+// contiguous group ranges, one per device, run concurrently by the library (one context
+// and host thread per device; include/fec_hip.h fec_group_*).  Host buffers only.
+type RSDeviceGroup struct {
+	grp *C.FECDeviceGroup
+	k   int
+	r   int
+	mu  sync.Mutex
+}
+
+// NewRSDeviceGroup binds a group to the given device ordinals (nil: every visible GPU).
+func NewRSDeviceGroup(k, r int, devices []int) (*RSDeviceGroup, error) {
+	if k <= 0 || r <= 0 || k+r > 256 {
+		return nil, fmt.Errorf("unsupported k=%d r=%d", k, r)
+	}
+	var grp *C.FECDeviceGroup
+	if len(devices) == 0 {
+		grp = C.fec_group_new(nil, 0)
+	} else {
+		ids := make([]C.int, len(devices))
+		for i, d := range devices {
+			ids[i] = C.int(d)
+		}
+		grp = C.fec_group_new(&ids[0], C.int(len(ids)))
+	}
+	if grp == nil {
+		return nil, fmt.Errorf("no usable GPU group: %s", C.GoString(C.fec_hip_last_error()))
+	}
+	g := &RSDeviceGroup{grp: grp, k: k, r: r}
+	runtime.SetFinalizer(g, (*RSDeviceGroup).Close)
+	return g, nil
+}
+
+// Devices is the number of shards (devices, repeats counted).
+func (g *RSDeviceGroup) Devices() int { return int(C.fec_group_size(g.grp)) }
+
+// EncodeBatch: as RSCodec.EncodeBatch, sharded over the group's devices.
+func (g *RSDeviceGroup) EncodeBatch(data []byte, packetSize int, parity []byte) error {
+	if packetSize <= 0 || len(data)%(g.k*packetSize) != 0 {
+		return fmt.Errorf("data length %d is not a whole number of %dx%d groups", len(data), g.k, packetSize)
+	}
+	groups := len(data) / (g.k * packetSize)
+	if len(parity) < groups*g.r*packetSize {
+		return fmt.Errorf("parity buffer too small")
+	}
+	if groups == 0 {
+		return nil
+	}
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	rc := C.fec_group_encode_batch_rs(g.grp, (*C.uint8_t)(unsafe.Pointer(&data[0])), C.uint64_t(groups),
+		C.uint32_t(g.k), C.uint32_t(g.r), C.uint32_t(packetSize), (*C.uint8_t)(unsafe.Pointer(&parity[0])))
+	runtime.KeepAlive(data)
+	runtime.KeepAlive(parity)
+	if rc != 0 {
+		return hipError("fec_group_encode_batch_rs", rc)
+	}
+	return nil
+}
+
+// DecodeBatch: as RSCodec.DecodeBatch, sharded over the group's devices.
+func (g *RSDeviceGroup) DecodeBatch(data, parity []byte, erasures []uint64, packetSize int, status []byte) (int, error) {
+	groups := len(erasures)
+	if packetSize <= 0 || len(data) < groups*g.k*packetSize || len(parity) < groups*g.r*packetSize {
+		return 0, fmt.Errorf("buffers too small for %d groups", groups)
+	}
+	if status != nil && len(status) < groups {
+		return 0, fmt.Errorf("status buffer too small")
+	}
+	if groups == 0 {
+		return 0, nil
+	}
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	var st *C.uint8_t
+	if status != nil {
+		st = (*C.uint8_t)(unsafe.Pointer(&status[0]))
+	}
+	var bad C.uint64_t
+	rc := C.fec_group_decode_batch_rs(g.grp, (*C.uint8_t)(unsafe.Pointer(&data[0])), (*C.uint8_t)(unsafe.Pointer(&parity[0])),
+		(*C.uint64_t)(unsafe.Pointer(&erasures[0])), C.uint64_t(groups), C.uint32_t(g.k), C.uint32_t(g.r),
+		C.uint32_t(packetSize), st, &bad)
+	runtime.KeepAlive(data)
+	runtime.KeepAlive(parity)
+	runtime.KeepAlive(erasures)
+	runtime.KeepAlive(status)
+	if rc != 0 {
+		return 0, hipError("fec_group_decode_batch_rs", rc)
+	}
+	return int(bad), nil
+}
+
+// Close releases every device context of the group.
+func (g *RSDeviceGroup) Close() error {
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	if g.grp != nil {
+		C.fec_group_free(g.grp)
+		g.grp = nil
+	}
+	return nil
+}

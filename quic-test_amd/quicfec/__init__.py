@@ -42,6 +42,8 @@ HIP_SYMBOLS = (
     "fec_hip_version", "fec_parity_matrix", "fec_encode_batch_rs", "fec_decode_batch_rs",
     "fec_encode_batch_rs_dev", "fec_decode_batch_rs_dev", "fec_decode_prepare",
     "fec_fill_random_dev", "fec_synchronize",
+    "fec_group_new", "fec_group_free", "fec_group_size", "fec_group_context",
+    "fec_group_encode_batch_rs", "fec_group_decode_batch_rs",
 )
 
 
@@ -105,6 +107,12 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
         "fec_decode_prepare": (_int, [_vp, _u32, _u32, ctypes.POINTER(_u64)]),
         "fec_fill_random_dev": (_int, [_vp, _vp, _u64, _u64, _u64, _vp]),
         "fec_synchronize": (_int, [_vp]),
+        "fec_group_new": (_vp, [ctypes.POINTER(_int), _int]),
+        "fec_group_free": (None, [_vp]),
+        "fec_group_size": (_int, [_vp]),
+        "fec_group_context": (_vp, [_vp, _int]),
+        "fec_group_encode_batch_rs": (_int, [_vp, _vp, _u64, _u32, _u32, _u32, _vp]),
+        "fec_group_decode_batch_rs": (_int, [_vp, _vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -237,6 +245,57 @@ class Context:
 
     def synchronize(self) -> None:
         _check(self.lib.fec_synchronize(self.handle), "fec_synchronize")
+
+
+class DeviceGroup:
+    """An FECDeviceGroup: host batches sharded over several GPUs (one context and host
+    thread per shard, contiguous group ranges, no data moved between devices)."""
+
+    def __init__(self, devices=None):
+        self.lib = load_library()
+        if devices is None:
+            h = self.lib.fec_group_new(None, 0)
+        else:
+            arr = (_int * max(1, len(devices)))(*devices)
+            h = self.lib.fec_group_new(arr, len(devices))
+        if not h:
+            raise FecError("fec_group_new", FEC_ERR_NODEV, last_error())
+        self.handle = h
+
+    def __len__(self) -> int:
+        return int(self.lib.fec_group_size(self.handle))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self.lib.fec_group_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def encode(self, data, k: int, r: int, packet_size: int, parity_out, num_groups: Optional[int] = None) -> None:
+        G = num_groups if num_groups is not None else _nbytes(data) // (k * packet_size)
+        _check(self.lib.fec_group_encode_batch_rs(self.handle, _ptr(data), G, k, r, packet_size, _ptr(parity_out)),
+               "fec_group_encode_batch_rs")
+
+    def decode(self, data, parity, masks, k: int, r: int, packet_size: int, status_out=None,
+               num_groups: Optional[int] = None) -> int:
+        G = num_groups if num_groups is not None else _nbytes(masks) // 8
+        bad = ctypes.c_uint64(0)
+        rc = self.lib.fec_group_decode_batch_rs(self.handle, _ptr(data), _ptr(parity), _ptr(masks), G, k, r,
+                                                packet_size, _ptr(status_out) if status_out is not None else None,
+                                                ctypes.byref(bad))
+        _check(rc, "fec_group_decode_batch_rs")
+        return int(bad.value)
 
 
 def _nbytes(a) -> int:

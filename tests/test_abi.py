@@ -67,6 +67,11 @@ def test_null_arguments_need_no_gpu(quicfec_mod):
     lib.fec_free_slab(None)
     lib.fec_free_repair_buffer(None)
     assert lib.fec_encoder_device(None) == -1
+    assert lib.fec_group_encode_batch_rs(None, None, 0, 1, 1, 1, None) == quicfec_mod.FEC_ERR_NULL
+    assert lib.fec_group_decode_batch_rs(None, None, None, None, 0, 1, 1, 1, None, None) == quicfec_mod.FEC_ERR_NULL
+    assert lib.fec_group_size(None) == 0
+    assert not lib.fec_group_context(None, 0)
+    lib.fec_group_free(None)
 
 
 def test_no_gpu_context_is_null_not_abort(quicfec_mod):
@@ -77,6 +82,9 @@ def test_no_gpu_context_is_null_not_abort(quicfec_mod):
     assert "no HIP device" in quicfec_mod.last_error()
     with pytest.raises(quicfec_mod.FecError):
         quicfec_mod.Context()
+    assert not lib.fec_group_new(None, 0)
+    with pytest.raises(quicfec_mod.FecError):
+        quicfec_mod.DeviceGroup()
 
 
 def test_parity_matrix_matches_oracle_and_fixture(quicfec_mod, oracle_mod, golden_dir):

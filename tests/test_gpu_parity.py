@@ -290,6 +290,37 @@ def test_host_decode_compacted_sparse_loss(gpu_ctx, oracle_mod, torch_cuda, monk
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("devices", [None, [0, 0, 0]])
+def test_device_group_shards_host_batches(quicfec_mod, oracle_mod, torch_cuda, devices):
+    """fec_group_*: a host batch split over shards (one context + host thread each); with
+    one GPU, [0, 0, 0] runs three shards concurrently on it.  Bit-exact vs the oracle."""
+    k, r, P, G = 10, 3, 1200, 3001
+    data = oracle_mod.splitmix_bytes(G * k * P, SEED + 31)
+    exp = oracle_mod.rs_encode(data, G, k, r, P, nthreads=8)
+    rng = np.random.default_rng(31)
+    masks = _random_masks(rng, G, k, r, r + 1)
+    broken = _poison(data, masks, G, k, P)
+    ref = broken.copy()
+    bad_exp, st_exp = oracle_mod.rs_decode(ref, exp, masks, G, k, r, P, nthreads=8)
+    with quicfec_mod.DeviceGroup(devices) as grp:
+        assert len(grp) == (3 if devices else quicfec_mod.device_count())
+        par = np.zeros(G * r * P, dtype=np.uint8)
+        grp.encode(data, k, r, P, par)
+        assert np.array_equal(par, exp)
+        h_par = torch_cuda.from_numpy(par).pin_memory()         # page-locked parity
+        st = np.zeros(G, dtype=np.uint8)
+        bad = grp.decode(broken, h_par, masks, k, r, P, status_out=st)
+        assert bad == bad_exp
+        assert np.array_equal(st, st_exp)
+        assert np.array_equal(broken, ref)
+        dd = torch_cuda.from_numpy(data).cuda()                  # device buffers are refused
+        with pytest.raises(quicfec_mod.FecError) as ei:
+            grp.encode(dd, k, r, P, par, num_groups=G)
+        assert ei.value.code == quicfec_mod.FEC_ERR_RANGE
+    with pytest.raises(quicfec_mod.FecError):
+        quicfec_mod.DeviceGroup([quicfec_mod.device_count()])    # ordinal out of range
+
+
 def test_fill_random_matches_oracle(gpu_ctx, oracle_mod, torch_cuda):
     for n, off in ((4096, 0), (1000, 8), (777, 3)):
         d = torch_cuda.zeros(n + 16, dtype=torch_cuda.uint8, device="cuda")
