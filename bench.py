@@ -295,6 +295,8 @@ def main() -> int:
     ap.add_argument("--loss", type=float, default=None,
                     help="iid per-shard loss probability (c5; 0.05 = mobile profile)")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--shape", default=None,
+                    help="k,r,P override of the config's code shape (tuning sweeps; not the headline)")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-resident path (pinned buffers, H2D -> kernel -> D2H)")
     args = ap.parse_args()
@@ -318,6 +320,10 @@ def main() -> int:
         cfg["loss"] = args.loss
         cfg["decode"] = True
         cfg["workload"] += f" (loss override p={args.loss})"
+    if args.shape:
+        cfg["k"], cfg["r"], cfg["P"] = (int(x) for x in args.shape.split(","))
+        cfg["erasures"] = min(cfg["erasures"], cfg["r"])
+        cfg["workload"] += f" (shape override k={cfg['k']} r={cfg['r']} P={cfg['P']})"
     k, r, P = cfg["k"], cfg["r"], cfg["P"]
     G = args.groups or cfg["groups"]
     g0, _ = shard_range(G * world, rank, world)

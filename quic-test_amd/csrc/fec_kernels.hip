@@ -852,8 +852,12 @@ hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
     if (tile > 0) {
       const uint32_t bs = (tile * cpp + 63) / 64 * 64;
       const uint32_t blocks = static_cast<uint32_t>((gn + tile - 1) / tile);
+      // Workgroups per CU: the compile-time-k kernels stream best at 2 (3 when r >= 4 rows of
+      // table arithmetic share each load); the runtime-k loop needs every wave it can get.
+      constexpr int kDefBlocks = K == 0 ? 0 : (R >= 4 ? kEncodeBlocksPerCU + 1 : kEncodeBlocksPerCU);
+      const int blocks_per_cu = env_waves("QUICFEC_ENCODE_BLOCKS", kDefBlocks);
       const int waves = a.waves_per_cu ? a.waves_per_cu
-                                       : env_waves("QUICFEC_ENCODE_WAVES", kEncodeBlocksPerCU * static_cast<int>(bs / 64));
+                                       : env_waves("QUICFEC_ENCODE_WAVES", blocks_per_cu * static_cast<int>(bs / 64));
       const uint32_t smem = occupancy_cap_lds(waves, bs / 64);
       hipLaunchKernelGGL((encode_v16<K, R, OFF, FIRST, POL>), dim3(blocks), dim3(bs), smem, s, a.data,
                          a.offsets, a.parity, g0, n, cpp, a.P, a.k, a.r, row0,

@@ -27,7 +27,9 @@ struct EncodeLaunch {
 // than the hardware allows keep the HBM request stream more local and measured faster
 // (tools/probe_encode.hip, tools/probe_decode.hip).
 // Encode: 2 workgroups per CU (k=10/1200 B: 2 x 5 waves, 5.70 vs 5.26 TB/s uncapped;
-// 1024 B: 2 x 4 waves 6.12 vs 5.92 at 3; 1216 B: 2 x 6 waves 5.92 vs 5.25 at 1).
+// 1024 B: 2 x 4 waves 6.12 vs 5.92 at 3; 1216 B: 2 x 6 waves 5.92 vs 5.25 at 1); one more
+// for r >= 4 (k=20 r=5: 5.47 at 3 vs 4.99 at 2); none for the runtime-k kernel
+// (k=10 r=2: 5.61 uncapped vs 3.66 at 2).  profiles/r01_encode_blocks_sweep.txt.
 constexpr int kEncodeBlocksPerCU = 2;
 constexpr int kDecodeWavesPerCU = 0;   // measured: any cap below ~20 waves/CU is slower
 

@@ -63,4 +63,4 @@ run_bench() {
 run_bench c2c3 --config c2c3 --steps 30 --warmup 5
 run_bench c4 --config c4 --steps 30 --warmup 5 --no-cpu-baseline
 run_bench c5_satellite --config c5 --steps 30 --warmup 5 --no-cpu-baseline --e2e
-run_bench c5_mobile --config c5 --loss 0.05 --steps 30 --warmup 5 --no-cpu-baseline
+run_bench c5_mobile --config c5 --loss 0.05 --steps 30 --warmup 5 --no-cpu-baseline --e2e
