@@ -306,15 +306,24 @@ __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, co
                                              const uint8_t* __restrict__ dg, const uint8_t* __restrict__ pg,
                                              uint8_t* __restrict__ og, uint32_t k, uint32_t P, uint32_t off,
                                              uint32_t e, uint32_t m0, bool xor_only) {
+  auto src_of = [&](uint32_t s) {
+    const uint32_t sid = rec_byte(rw, s);
+    return sid < k ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - k) * static_cast<uint64_t>(P);
+  };
+  // Runtime k: survivors in batches of kBatch loads in flight (slots past k re-load
+  // survivor 0, a valid address, and are not used).
+  constexpr uint32_t kBatch = 8;
   if (xor_only) {  // single data loss rebuilt from parity row 0: the reference XOR
     uint32_t acc[NW] = {};
-    for (uint32_t s = 0; s < k; ++s) {
-      const uint32_t sid = rec_byte(rw, s);
-      const uint8_t* src = sid < k ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - k) * static_cast<uint64_t>(P);
-      uint32_t v[NW];
-      ldw<NW, POL>(src + off, v);
+    for (uint32_t s0 = 0; s0 < k; s0 += kBatch) {
+      uint32_t v[kBatch][NW];
 #pragma unroll
-      for (int q = 0; q < NW; ++q) acc[q] ^= v[q];
+      for (uint32_t b = 0; b < kBatch; ++b) ldw<NW, POL>(src_of(s0 + b < k ? s0 + b : 0) + off, v[b]);
+#pragma unroll
+      for (uint32_t b = 0; b < kBatch; ++b)
+        if (s0 + b < k)
+#pragma unroll
+          for (int q = 0; q < NW; ++q) acc[q] ^= v[b][q];
     }
     stw<NW, POL>(og + rec_byte(rw, 64) * static_cast<uint64_t>(P) + off, acc);
     return;
@@ -361,13 +370,13 @@ __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, co
 #pragma unroll
     for (int s = 0; s < K; ++s) consume(x[s], s, K);
   } else {
-#pragma unroll 2
-    for (uint32_t s = 0; s < k; ++s) {
-      const uint32_t sid = rec_byte(rw, s);
-      const uint8_t* src = sid < k ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - k) * static_cast<uint64_t>(P);
-      uint32_t v[NW];
-      ldw<NW, POL>(src + off, v);
-      consume(v, s, k);
+    for (uint32_t s0 = 0; s0 < k; s0 += kBatch) {
+      uint32_t v[kBatch][NW];
+#pragma unroll
+      for (uint32_t b = 0; b < kBatch; ++b) ldw<NW, POL>(src_of(s0 + b < k ? s0 + b : 0) + off, v[b]);
+#pragma unroll
+      for (uint32_t b = 0; b < kBatch; ++b)
+        if (s0 + b < k) consume(v[b], s0 + b, k);
     }
   }
 #pragma unroll
