@@ -111,6 +111,48 @@ __global__ __launch_bounds__(((T * 75 + 63) / 64) * 64) void enc_blk(const uint8
   for (int i = 0; i < R; ++i) st16<POL>(parity + (g * R + i) * P + col * 16u, acc[i]);
 }
 
+// Memory-pattern probe: enc_xcd<4> with every packet / parity row base rounded down to a
+// 128-B line (LA: loads, SA: stores).  Results are garbage when rounded; timing only.
+template <bool LA, bool SA>
+__global__ __launch_bounds__(320) void enc_align(const uint8_t* __restrict__ data, uint8_t* __restrict__ parity,
+                                                 uint32_t groups, const Tab* __restrict__ tabs) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t cap_lds[];
+  if (groups == 0xFFFFFFFFu) cap_lds[threadIdx.x] = 0;
+  constexpr int T = 4, K = 10, R = 3, P = 1200, CPP = 75;
+  const uint32_t nb = gridDim.x, b = blockIdx.x;
+  const uint32_t per = nb / 8;
+  const uint32_t tile = (b < per * 8) ? (b % 8) * per + b / 8 : b;
+  const uint32_t lane = threadIdx.x;
+  if (lane >= T * CPP) return;
+  const uint32_t gl = lane / CPP, col = lane - gl * CPP;
+  const uint64_t g = uint64_t(tile) * T + gl;
+  if (g >= groups) return;
+  u32x4 d[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    uint64_t pb = (g * K + j) * P;
+    if (LA) pb &= ~uint64_t(127);
+    d[j] = ld16<0>(data + pb + col * 16u);
+  }
+  u32x4 acc[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) acc[i] = d[0];
+#pragma unroll
+  for (int j = 1; j < K; ++j) {
+    Sel s;
+    prep(d[j], s);
+    acc[0] ^= d[j];
+#pragma unroll
+    for (int i = 1; i < R; ++i) mac(acc[i], s, tabs[(i - 1) * K + j]);
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    uint64_t pb = (g * R + i) * P;
+    if (SA) pb &= ~uint64_t(127);
+    st16<2>(parity + pb + col * 16u, acc[i]);
+  }
+}
+
 // enc_blk with an XCD-aware tile order: blocks b and b+8 share an XCD (round-robin
 // dispatch), so tile = (b % 8) * (nblocks / 8) + b / 8 gives each XCD one contiguous
 // eighth of the data.
@@ -451,6 +493,13 @@ int main(int argc, char** argv) {
     vars.push_back({"enc_xcd<4> smem" + std::to_string(smem / 1024), enc_bytes, [=] {
                       enc_xcd<4, 2><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab);
                     }, {}});
+  }
+  {
+    const uint32_t smem = 160 * 1024 / 3 + 16;  // 2 workgroups (10 waves) per CU
+    vars.push_back({"algn ld0 st0", enc_bytes, [=] { enc_align<false, false><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab); }, {}});
+    vars.push_back({"algn ld1 st0", enc_bytes, [=] { enc_align<true, false><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab); }, {}});
+    vars.push_back({"algn ld0 st1", enc_bytes, [=] { enc_align<false, true><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab); }, {}});
+    vars.push_back({"algn ld1 st1", enc_bytes, [=] { enc_align<true, true><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab); }, {}});
   }
   for (int per_cu : {1}) {
     const uint32_t ntl = uint32_t((G + 3) / 4);
