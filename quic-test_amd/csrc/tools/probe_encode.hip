@@ -113,7 +113,7 @@ __global__ __launch_bounds__(((T * 75 + 63) / 64) * 64) void enc_blk(const uint8
 
 // Memory-pattern probe: enc_xcd<4> with every packet / parity row base rounded down to a
 // 128-B line (LA: loads, SA: stores).  Results are garbage when rounded; timing only.
-template <bool LA, bool SA>
+template <bool LA, bool SA, bool NS = false>
 __global__ __launch_bounds__(320) void enc_align(const uint8_t* __restrict__ data, uint8_t* __restrict__ parity,
                                                  uint32_t groups, const Tab* __restrict__ tabs) {
   extern __shared__ __attribute__((aligned(16))) uint8_t cap_lds[];
@@ -145,6 +145,7 @@ __global__ __launch_bounds__(320) void enc_align(const uint8_t* __restrict__ dat
 #pragma unroll
     for (int i = 1; i < R; ++i) mac(acc[i], s, tabs[(i - 1) * K + j]);
   }
+  if (NS && (acc[0].x != 0x9E3779B9u || acc[R - 1].w != 0x7F4A7C15u)) return;  // reads only
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     uint64_t pb = (g * R + i) * P;
@@ -499,6 +500,8 @@ int main(int argc, char** argv) {
     vars.push_back({"algn ld0 st0", enc_bytes, [=] { enc_align<false, false><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab); }, {}});
     vars.push_back({"algn ld1 st0", enc_bytes, [=] { enc_align<true, false><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab); }, {}});
     vars.push_back({"algn ld0 st1", enc_bytes, [=] { enc_align<false, true><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab); }, {}});
+    vars.push_back({"algn reads only", nd, [=] { enc_align<false, false, true><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab); }, {}});
+    vars.push_back({"algn reads only uncapped", nd, [=] { enc_align<false, false, true><<<uint32_t((G + 3) / 4), 320, 0>>>(data, par, uint32_t(G), dtab); }, {}});
     vars.push_back({"algn ld1 st1", enc_bytes, [=] { enc_align<true, true><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab); }, {}});
   }
   for (int per_cu : {1}) {
