@@ -13,7 +13,14 @@
 //    data set and of the parity rows used), status byte.
 //  * decode_v16<K,MAXE>: one wave per group, so the record (survivor list + tables) is
 //    wave-uniform and lives in SGPRs; lanes walk the group's 16-byte columns.
-//  * *_bytes: any packet size / alignment (one lane per byte), same tables.
+//  * *_bytes: packets shorter than 16 B (one lane per byte), same tables.
+//
+// Any packet size P >= 16 and any packet alignment run on the vector kernels: the last
+// 16-byte column of a packet is shifted back to [P - 16, P) (it overlaps the column before
+// it; both lanes compute the same bytes and store the same values), and loads / stores of
+// 16 B at any byte address are legal on gfx950 (unaligned global access, which the
+// compiler also assumes for amdhsa).  GF arithmetic is byte-wise with one coefficient per
+// packet, so a column's position inside its packet never changes its arithmetic.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -29,6 +36,10 @@ struct Tab {
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Byte-aligned views for packet memory (any P, any packet address): same dwordx4 / dword
+// instructions as the aligned types.
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32u __attribute__((aligned(1)));
 
 // Memory policy bits of the streaming kernels.
 constexpr int kNtLoad = 1;        // non-temporal loads (data read once)
@@ -40,14 +51,14 @@ constexpr int kProbeDense = 32;   // probes only: decode_fused reads data shards
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
-  if constexpr ((POL & kNtLoad) != 0) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-  else return *reinterpret_cast<const u32x4*>(p);
+  if constexpr ((POL & kNtLoad) != 0) return __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(p));
+  else return *reinterpret_cast<const u32x4u*>(p);
 }
 
 template <int POL>
 __device__ __forceinline__ void st16(uint8_t* p, u32x4 v) {
-  if constexpr ((POL & kNtStore) != 0) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-  else *reinterpret_cast<u32x4*>(p) = v;
+  if constexpr ((POL & kNtStore) != 0) __builtin_nontemporal_store(v, reinterpret_cast<u32x4u*>(p));
+  else *reinterpret_cast<u32x4u*>(p) = v;
 }
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -98,6 +109,13 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
   return b < (per << 3) ? (b & 7u) * per + (b >> 3) : b;
 }
 
+// Byte offset of 16-byte column `col` inside a packet of P >= 16 bytes: the last column
+// is shifted back to end at P (see the header).
+__device__ __forceinline__ uint32_t col_off16(uint32_t col, uint32_t P) {
+  const uint32_t o = col * 16u;
+  return o + 16u <= P ? o : P - 16u;
+}
+
 template <int OFF>
 __device__ __forceinline__ const uint8_t* packet_ptr(const uint8_t* data, const void* offsets,
                                                      uint64_t g, uint32_t k, uint32_t j, uint32_t P) {
@@ -116,6 +134,7 @@ __device__ __forceinline__ const uint8_t* packet_ptr(const uint8_t* data, const 
 // FIRST (row0 == 0) row 0 is the plain XOR.  Column 0 of every row is 1 by construction.
 // ---------------------------------------------------------------------------------
 //
+// Columns per packet cpp = ceil(P / 16); column c covers bytes [min(16c, P - 16), +16).
 // Thread -> (group, column) mapping, two forms:
 //  * tiled (tile > 0): a workgroup owns `tile` whole groups (lanes [0, tile*cpp), the rest
 //    idle).  The workgroup's data window then starts and ends on group boundaries, so no
@@ -152,7 +171,7 @@ __global__ __launch_bounds__(512) void encode_v16(const uint8_t* __restrict__ da
   }
   const uint64_t g = g_first + gl;
   const uint32_t k = K > 0 ? static_cast<uint32_t>(K) : k_rt;
-  const size_t coff = static_cast<size_t>(col) * 16u;
+  const size_t coff = col_off16(col, P);
 
   u32x4 acc[R];
   if constexpr (K > 0) {
@@ -285,7 +304,7 @@ __device__ __forceinline__ void ldw(const uint8_t* p, uint32_t (&v)[NW]) {
     v[2] = t.z;
     v[3] = t.w;
   } else {
-    v[0] = *reinterpret_cast<const uint32_t*>(p);
+    v[0] = *reinterpret_cast<const u32u*>(p);
   }
 }
 
@@ -294,8 +313,8 @@ __device__ __forceinline__ void stw(uint8_t* p, const uint32_t (&v)[NW]) {
   if constexpr (NW == 4) {
     st16<POL>(p, u32x4{v[0], v[1], v[2], v[3]});
   } else {
-    if constexpr ((POL & kNtStore) != 0) __builtin_nontemporal_store(v[0], reinterpret_cast<uint32_t*>(p));
-    else *reinterpret_cast<uint32_t*>(p) = v[0];
+    if constexpr ((POL & kNtStore) != 0) __builtin_nontemporal_store(v[0], reinterpret_cast<u32u*>(p));
+    else *reinterpret_cast<u32u*>(p) = v[0];
   }
 }
 
@@ -391,7 +410,10 @@ __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, co
 // decode_wave with the main (16 B/lane) and tail (4 B/lane) passes fused: each lane holds
 // NM 16-byte pieces and NT 4-byte pieces of every survivor, so every coefficient table is
 // loaded (scalar) and branched on once per wave instead of once per pass.  Packet sizes
-// with NM = P / 1024 and NT = ceil((P % 1024) / 256) matching the instantiation.
+// with NM = P / 1024 and NT = ceil((P % 1024) / 256) matching the instantiation.  Tail
+// pieces past the packet end are shifted back to [P - 4, P) (same bytes, same values as
+// the lane that owns them), so every lane loads and stores and no packet size needs a
+// mask; P >= 4.
 //
 // DIRECT: the survivor and erased shard ids come from the group's erasure mask (scalar bit
 // scans) instead of the record header, so the survivor loads depend on one scalar load
@@ -446,12 +468,10 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
   uint8_t* og = out + gw * K * static_cast<uint64_t>(P);
   const uint32_t main_end = NM * 1024u;
   uint32_t toff[NT > 0 ? NT : 1];
-  bool tok[NT > 0 ? NT : 1];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     toff[t] = main_end + t * 256u + lane * 4u;
-    tok[t] = toff[t] < P;
-    if (!tok[t]) toff[t] = main_end;  // valid address; result discarded
+    if (toff[t] + 4u > P) toff[t] = P - 4u;
   }
   auto load = [&](const uint8_t* base, uint32_t (&v)[NW]) {
 #pragma unroll
@@ -464,8 +484,8 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      if constexpr ((POL & kNtLoad) != 0) v[4 * NM + t] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(base + toff[t]));
-      else v[4 * NM + t] = *reinterpret_cast<const uint32_t*>(base + toff[t]);
+      if constexpr ((POL & kNtLoad) != 0) v[4 * NM + t] = __builtin_nontemporal_load(reinterpret_cast<const u32u*>(base + toff[t]));
+      else v[4 * NM + t] = *reinterpret_cast<const u32u*>(base + toff[t]);
     }
   };
   auto store = [&](uint8_t* base, const uint32_t (&v)[NW]) {
@@ -473,10 +493,8 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
     for (int i = 0; i < NM; ++i) st16<POL>(base + i * 1024u + lane * 16u, u32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]});
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      if (tok[t]) {
-        if constexpr ((POL & kNtStore) != 0) __builtin_nontemporal_store(v[4 * NM + t], reinterpret_cast<uint32_t*>(base + toff[t]));
-        else *reinterpret_cast<uint32_t*>(base + toff[t]) = v[4 * NM + t];
-      }
+      if constexpr ((POL & kNtStore) != 0) __builtin_nontemporal_store(v[4 * NM + t], reinterpret_cast<u32u*>(base + toff[t]));
+      else *reinterpret_cast<u32u*>(base + toff[t]) = v[4 * NM + t];
     }
   };
   auto shard = [&](uint32_t sid) {
@@ -558,7 +576,9 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
 // One wave per group, so the record is wave-uniform (SGPRs).  A packet is covered by
 // whole 1 KiB passes of 16 B per lane, then the remainder (< 1 KiB) by 256 B passes of
 // 4 B per lane: at 1200 B that is 64 + 44 busy lanes instead of 64 + 11 lanes doing
-// 16-B work, i.e. 5 instead of 8 dword slots of VALU per lane and survivor.
+// 16-B work, i.e. 5 instead of 8 dword slots of VALU per lane and survivor.  Tail pieces
+// past the packet end are shifted back to [P - 4, P) (duplicates of a neighbour's bytes,
+// same values), so any P >= 4 works and no lane branches on the packet end.
 template <int K, int MAXE, int POL = 0>
 __global__ __launch_bounds__(256) void decode_wave(uint8_t* __restrict__ data,
                                                    const uint8_t* __restrict__ parity,
@@ -590,7 +610,7 @@ __global__ __launch_bounds__(256) void decode_wave(uint8_t* __restrict__ data,
     decode_piece<K, MAXE, POL, 4>(rw, tabs, dg, pg, og, k, P, base + lane * 16u, e, m0, xor_only);
   for (uint32_t base = main_end; base < P; base += 256u) {
     const uint32_t off = base + lane * 4u;
-    if (off < P) decode_piece<K, MAXE, POL, 1>(rw, tabs, dg, pg, og, k, P, off, e, m0, xor_only);
+    decode_piece<K, MAXE, POL, 1>(rw, tabs, dg, pg, og, k, P, off + 4u <= P ? off : P - 4u, e, m0, xor_only);
   }
 }
 
@@ -620,7 +640,7 @@ __global__ __launch_bounds__(256) void decode_v16(uint8_t* __restrict__ data,
   const uint8_t* pg = parity + gw * r * static_cast<uint64_t>(P);
 
   for (uint32_t col = lane; col < cpp; col += 64u) {
-    const size_t coff = static_cast<size_t>(col) * 16u;
+    const size_t coff = col_off16(col, P);
     if (xor_only) {  // single data loss rebuilt from parity row 0: the reference XOR
       u32x4 acc = {0u, 0u, 0u, 0u};
       for (uint32_t s = 0; s < k; ++s) {
@@ -711,7 +731,7 @@ __global__ __launch_bounds__(512) void decode_tiled(uint8_t* __restrict__ data,
   const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
   uint8_t* dg = data + g * K * static_cast<uint64_t>(P);
   const uint8_t* pg = parity + g * r * static_cast<uint64_t>(P);
-  const size_t coff = static_cast<size_t>(col) * 16u;
+  const size_t coff = col_off16(col, P);
   uint32_t sw[(K + 3) / 4];
 #pragma unroll
   for (int q = 0; q < (K + 3) / 4; ++q) sw[q] = rw[q];
@@ -744,7 +764,7 @@ __global__ __launch_bounds__(512) void decode_tiled(uint8_t* __restrict__ data,
   }
 }
 
-// Decode, one lane per byte (any size / alignment).
+// Decode, one lane per byte (packets shorter than 16 B).
 __global__ __launch_bounds__(256) void decode_bytes(const uint8_t* __restrict__ data,
                                                     const uint8_t* __restrict__ parity,
                                                     const uint32_t* __restrict__ rec_off,
@@ -806,6 +826,7 @@ __global__ __launch_bounds__(256) void fill_bytes(uint8_t* __restrict__ dst, uin
 }
 
 constexpr uint32_t kMaxThreadsPerLaunch = 1u << 30;
+constexpr uint32_t kVecMinP = 16;  // shorter packets take the byte kernels
 
 inline uint32_t blocks_for(uint64_t n) { return static_cast<uint32_t>((n + 255) / 256); }
 
@@ -852,7 +873,7 @@ uint32_t pick_tile(uint32_t cpp, uint32_t k, uint32_t P) {
 // POL: parity is written once and not re-read by this kernel (non-temporal stores).
 template <int K, int R, int OFF, bool FIRST, int POL = kNtStore>
 hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
-  const uint32_t cpp = a.P / 16u;
+  const uint32_t cpp = (a.P + 15u) / 16u;
   const uint32_t tile = pick_tile(cpp, a.k, a.P);
   const uint64_t gchunk = kMaxThreadsPerLaunch / cpp;
   for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
@@ -884,7 +905,7 @@ hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
 
 template <int OFF>
 hipError_t run_encode_generic(const EncodeLaunch& a, hipStream_t s) {
-  if (!a.vec16) {
+  if (a.P < kVecMinP) {
     const uint64_t gchunk = kMaxThreadsPerLaunch / a.P;
     for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
       const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
@@ -927,7 +948,7 @@ hipError_t run_encode_generic(const EncodeLaunch& a, hipStream_t s) {
 
 hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
   if (a.groups == 0) return hipSuccess;
-  if (a.vec16) {
+  if (a.P >= kVecMinP) {
     if (a.off_kind == OffsetKind::kNone) {
       if (a.k == 10 && a.r == 3) return run_encode_v16<10, 3, 0, true>(a, 0, s);
       if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 0, true>(a, 0, s);
@@ -951,7 +972,7 @@ namespace {
 
 template <int K, int MAXE>
 hipError_t run_decode_v16(const DecodeLaunch& a, hipStream_t s) {
-  const uint32_t cpp = a.P / 16u;
+  const uint32_t cpp = (a.P + 15u) / 16u;
   const uint32_t passes = (a.r + MAXE - 1) / MAXE;  // e <= r
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t m0 = p * MAXE;
@@ -1025,7 +1046,9 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct) {
     return direct ? run_decode_fused<KK, RR, kNtStore, NMM, NTT, true>(a, s)                  \
                   : run_decode_fused<KK, RR, kNtStore, NMM, NTT, false>(a, s);
   QFEC_FUSED(10, 3, 1, 1)
+  QFEC_FUSED(10, 3, 1, 2)   // 1281..1536 B: 1350 / 1400 / 1452 / 1500-B packets
   QFEC_FUSED(20, 5, 1, 1)
+  QFEC_FUSED(20, 5, 1, 2)
   QFEC_FUSED(10, 1, 1, 1)
   QFEC_FUSED(4, 2, 0, 1)
 #undef QFEC_FUSED
@@ -1034,7 +1057,7 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct) {
 
 template <int K, int MAXE, int POL>
 hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s) {
-  const uint32_t cpp = a.P / 16u;
+  const uint32_t cpp = (a.P + 15u) / 16u;
   const uint32_t bs = (tile * cpp + 63) / 64 * 64;
   const uint64_t blocks = (a.groups + tile - 1) / tile;
   for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 30)) {
@@ -1062,7 +1085,7 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  if (!a.vec16) {
+  if (a.P < kVecMinP) {
     const uint64_t gchunk = kMaxThreadsPerLaunch / a.P;
     for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
       const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
@@ -1074,7 +1097,7 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     }
     return hipSuccess;
   }
-  const uint32_t tile = pick_tile(a.P / 16u, a.k, a.P);
+  const uint32_t tile = pick_tile((a.P + 15u) / 16u, a.k, a.P);
   const bool separate_out = a.out != nullptr && a.out != a.data;  // only decode_wave supports it
   if (!separate_out && tile > 0 && (a.variant == kDecodeTiledPlain || a.variant == kDecodeTiledNt)) {
     const bool nt = a.variant == kDecodeTiledNt;

@@ -11,6 +11,8 @@ namespace qfec {
 // Byte offsets of packets, when the data shards are not contiguous.
 enum class OffsetKind : int { kNone = 0, kU32 = 1, kU64 = 2 };
 
+// Packets of any size P >= 16 at any byte address run on the 16-byte-column kernels
+// (fec_kernels.hip header); shorter ones on the byte kernels.
 struct EncodeLaunch {
   const uint8_t* data;       // base of the data shards (device address)
   const void* offsets;       // device u32/u64 offsets (k per group) or nullptr
@@ -19,7 +21,6 @@ struct EncodeLaunch {
   uint64_t groups;
   uint32_t k, r, P;
   const void* tables;        // (r-1) x k CoefEntry (rows 1..r-1), device
-  bool vec16;                // P % 16 == 0 and every packet 16-byte aligned
   int waves_per_cu = 0;      // occupancy cap of the streaming kernel (0 = tuned default)
 };
 
@@ -76,7 +77,6 @@ struct DecodeLaunch {
   LevelMeta meta;
   uint64_t groups;
   uint32_t k, r, P;
-  bool vec16;
   int waves_per_cu = 0;      // occupancy cap of the decode kernel (0 = tuned default)
   bool rec_ready = false;    // rec_off already filled by the host (sparse plan): no classify
   int xcd_swizzle = -1;      // XCD-aware group order: -1 tuned default, 0 off, 1 on

@@ -346,8 +346,6 @@ int get_decode_plan(FECEncoderCtx* ctx, uint32_t k, uint32_t r, DecodePlan** out
   return FEC_OK;
 }
 
-bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-
 hipStream_t pick_stream(FECEncoderCtx* ctx, void* stream) {
   return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
 }
@@ -355,7 +353,7 @@ hipStream_t pick_stream(FECEncoderCtx* ctx, void* stream) {
 // Device-resident encode, contiguous layout.  Caller holds ctx->mu and the device.
 int encode_dev_locked(FECEncoderCtx* ctx, const uint8_t* d_data, const void* d_offsets,
                       qfec::OffsetKind ok, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
-                      uint8_t* d_parity, bool vec16, hipStream_t s) {
+                      uint8_t* d_parity, hipStream_t s) {
   const void* tables = nullptr;
   int rc = get_encode_plan(ctx, k, r, &tables);
   if (rc != FEC_OK) return rc;
@@ -369,14 +367,13 @@ int encode_dev_locked(FECEncoderCtx* ctx, const uint8_t* d_data, const void* d_o
   a.r = r;
   a.P = P;
   a.tables = tables;
-  a.vec16 = vec16;
   QFEC_HIP(qfec::launch_encode(a, s));
   return FEC_OK;
 }
 
 int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
                       const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
-                      uint8_t* d_status, bool vec16, hipStream_t s, DevBuf* rec = nullptr,
+                      uint8_t* d_status, hipStream_t s, DevBuf* rec = nullptr,
                       uint8_t* d_out = nullptr) {
   DecodePlan* plan = nullptr;
   int rc = get_decode_plan(ctx, k, r, &plan);
@@ -421,7 +418,6 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   a.k = k;
   a.r = r;
   a.P = P;
-  a.vec16 = vec16;
   QFEC_HIP(qfec::launch_decode(a, s));
   if (!plan->dense) QFEC_HIP(hipStreamSynchronize(s));  // the sparse records are reused next call
   return FEC_OK;
@@ -448,14 +444,13 @@ int encode_host_pipelined(FECEncoderCtx* ctx, const uint8_t* data, uint64_t G, u
     QFEC_HIP(p.in.ensure(cg * in_g));
     QFEC_HIP(p.par.ensure(cg * out_g));
   }
-  const bool vec16 = (P % 16u) == 0;
   uint64_t c = 0;
   for (uint64_t g0 = 0; g0 < G; g0 += cg, ++c) {
     PipeSlot& sl = ctx->pipe[c % kPipeSlots];
     const uint64_t n = (G - g0 < cg) ? G - g0 : cg;
     QFEC_HIP(hipMemcpyAsync(sl.in.ptr, data + g0 * in_g, n * in_g, hipMemcpyHostToDevice, sl.s));
     rc = encode_dev_locked(ctx, sl.in.as<uint8_t>(), nullptr, qfec::OffsetKind::kNone, n, k, r, P,
-                           sl.par.as<uint8_t>(), vec16, sl.s);
+                           sl.par.as<uint8_t>(), sl.s);
     if (rc != FEC_OK) return rc;
     QFEC_HIP(hipMemcpyAsync(parity_out + g0 * out_g, sl.par.ptr, n * out_g, hipMemcpyDeviceToHost, sl.s));
   }
@@ -476,7 +471,6 @@ int decode_host_pipelined(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
     QFEC_HIP(p.mask.ensure(cg * 8));
     QFEC_HIP(p.status.ensure(cg));
   }
-  const bool vec16 = (P % 16u) == 0;
   // Page-locked data: the kernel stores the rebuilt shards straight into host memory
   // (zero-copy PCIe writes of ~e*P bytes per group) instead of a D2H of the whole chunk.
   uint8_t* host_dev = nullptr;
@@ -496,7 +490,7 @@ int decode_host_pipelined(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
     QFEC_HIP(hipMemcpyAsync(sl.par.ptr, parity + g0 * par_g, n * par_g, hipMemcpyHostToDevice, sl.s));
     QFEC_HIP(hipMemcpyAsync(sl.mask.ptr, masks + g0, n * 8, hipMemcpyHostToDevice, sl.s));
     rc = decode_dev_locked(ctx, sl.in.as<uint8_t>(), sl.par.as<uint8_t>(), sl.mask.as<uint64_t>(), n, k, r, P,
-                           sl.status.as<uint8_t>(), vec16, sl.s, &sl.rec, host_dev ? host_dev + g0 * in_g : nullptr);
+                           sl.status.as<uint8_t>(), sl.s, &sl.rec, host_dev ? host_dev + g0 * in_g : nullptr);
     if (rc != FEC_OK) return rc;
     if (!host_dev)
       QFEC_HIP(hipMemcpyAsync(data + g0 * in_g, sl.in.ptr, n * in_g, hipMemcpyDeviceToHost, sl.s));
@@ -550,7 +544,6 @@ int decode_host_compacted(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
     sl.h_groups.clear();
     return FEC_OK;
   };
-  const bool vec16 = (P % 16u) == 0;
   uint64_t c = 0;
   for (uint64_t i0 = 0; i0 < N; i0 += cg, ++c) {
     PipeSlot& sl = ctx->pipe[c % kPipeSlots];
@@ -574,7 +567,7 @@ int decode_host_compacted(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
     QFEC_HIP(hipMemcpyAsync(sl.par.ptr, hp, n * par_g, hipMemcpyHostToDevice, sl.s));
     QFEC_HIP(hipMemcpyAsync(sl.mask.ptr, hm, n * 8, hipMemcpyHostToDevice, sl.s));
     rc = decode_dev_locked(ctx, sl.in.as<uint8_t>(), sl.par.as<uint8_t>(), sl.mask.as<uint64_t>(), n, k, r, P,
-                           nullptr, vec16, sl.s, &sl.rec);
+                           nullptr, sl.s, &sl.rec);
     if (rc != FEC_OK) return rc;
     QFEC_HIP(hipMemcpyAsync(hi, sl.in.ptr, n * in_g, hipMemcpyDeviceToHost, sl.s));
   }
@@ -621,9 +614,8 @@ void xor_packets_gpu(const uint8_t* packets[], size_t n, size_t packet_size, uin
       return;
     }
   }
-  const bool vec16 = (P % 16u) == 0;
   if (encode_dev_locked(ctx, ctx->d_in.as<uint8_t>(), nullptr, qfec::OffsetKind::kNone, 1,
-                        static_cast<uint32_t>(n), 1, P, ctx->d_out.as<uint8_t>(), vec16,
+                        static_cast<uint32_t>(n), 1, P, ctx->d_out.as<uint8_t>(),
                         ctx->stream) != FEC_OK)
     return;
   if (hipMemcpyAsync(repair, ctx->d_out.ptr, packet_size, hipMemcpyDefault, ctx->stream) != hipSuccess ||
@@ -690,9 +682,8 @@ QFEC_EXPORT int fec_encode_batch(FECEncoderCtx* ctx, const uint8_t* slab, const 
 
   const uint8_t* d_slab = slab;
   const uint32_t* d_offsets = offsets;
-  bool vec16 = (P % 16u) == 0;
   if (slab_mem != Mem::kDevice || off_mem != Mem::kDevice) {
-    // Host offsets: read them here to size the slab window and check alignment.
+    // Host offsets: read them here to size the slab window.
     std::vector<uint32_t> host_off;
     const uint32_t* hoff = offsets;
     if (off_mem == Mem::kDevice) {
@@ -706,7 +697,6 @@ QFEC_EXPORT int fec_encode_batch(FECEncoderCtx* ctx, const uint8_t* slab, const 
       hi = hoff[i] > hi ? hoff[i] : hi;
     }
     if (slab_mem == Mem::kDevice) {
-      for (uint64_t i = 0; i < noff && vec16; ++i) vec16 = aligned16(slab + hoff[i]);
       if (off_mem != Mem::kDevice) {
         QFEC_HIP(ctx->d_off.ensure(noff * 4));
         QFEC_HIP(hipMemcpyAsync(ctx->d_off.ptr, hoff, noff * 4, hipMemcpyHostToDevice, s));
@@ -716,10 +706,7 @@ QFEC_EXPORT int fec_encode_batch(FECEncoderCtx* ctx, const uint8_t* slab, const 
       // Copy the window [lo, hi + P) of the host slab; rebase offsets to it.
       const uint64_t span = uint64_t(hi) + P - lo;
       std::vector<uint32_t> rebased(noff);
-      for (uint64_t i = 0; i < noff; ++i) {
-        rebased[i] = hoff[i] - lo;
-        vec16 = vec16 && (rebased[i] % 16u) == 0;
-      }
+      for (uint64_t i = 0; i < noff; ++i) rebased[i] = hoff[i] - lo;
       QFEC_HIP(ctx->d_in.ensure(span));
       QFEC_HIP(ctx->d_off.ensure(noff * 4));
       QFEC_HIP(hipMemcpyAsync(ctx->d_in.ptr, slab + lo, span, hipMemcpyHostToDevice, s));
@@ -728,11 +715,6 @@ QFEC_EXPORT int fec_encode_batch(FECEncoderCtx* ctx, const uint8_t* slab, const 
       d_slab = ctx->d_in.as<uint8_t>();
       d_offsets = ctx->d_off.as<uint32_t>();
     }
-  } else {
-    // Both on the device: alignment of the packets is unknown without reading offsets.
-    std::vector<uint32_t> host_off(noff);
-    QFEC_HIP(hipMemcpy(host_off.data(), offsets, noff * 4, hipMemcpyDeviceToHost));
-    for (uint64_t i = 0; i < noff && vec16; ++i) vec16 = aligned16(slab + host_off[i]);
   }
   uint8_t* d_repair = repair_out;
   if (out_mem != Mem::kDevice) {
@@ -740,7 +722,7 @@ QFEC_EXPORT int fec_encode_batch(FECEncoderCtx* ctx, const uint8_t* slab, const 
     d_repair = ctx->d_out.as<uint8_t>();
   }
   const int rc = encode_dev_locked(ctx, d_slab, d_offsets, qfec::OffsetKind::kU32, num_groups,
-                                   kPackets, 1, packet_size, d_repair, vec16, s);
+                                   kPackets, 1, packet_size, d_repair, s);
   if (rc != FEC_OK) return rc;
   if (out_mem != Mem::kDevice)
     QFEC_HIP(hipMemcpyAsync(repair_out, d_repair, uint64_t(num_groups) * P, hipMemcpyDeviceToHost, s));
@@ -837,7 +819,6 @@ QFEC_EXPORT int fec_encode_batch_rs(FECEncoderCtx* ctx, const uint8_t* data, con
   const uint8_t* d_data = data;
   const void* d_off = nullptr;
   qfec::OffsetKind ok = qfec::OffsetKind::kNone;
-  bool vec16 = (P % 16u) == 0;
   std::vector<uint64_t> rebased;
   if (offsets) {
     ok = qfec::OffsetKind::kU64;
@@ -855,7 +836,6 @@ QFEC_EXPORT int fec_encode_batch_rs(FECEncoderCtx* ctx, const uint8_t* data, con
       hi = hoff[i] > hi ? hoff[i] : hi;
     }
     if (dmem == Mem::kDevice) {
-      for (uint64_t i = 0; i < nin && vec16; ++i) vec16 = aligned16(data + hoff[i]);
       if (offmem != Mem::kDevice) {
         QFEC_HIP(ctx->d_off.ensure(nin * 8));
         QFEC_HIP(hipMemcpyAsync(ctx->d_off.ptr, hoff, nin * 8, hipMemcpyHostToDevice, s));
@@ -867,10 +847,7 @@ QFEC_EXPORT int fec_encode_batch_rs(FECEncoderCtx* ctx, const uint8_t* data, con
     } else {
       const uint64_t span = hi + P - lo;
       rebased.resize(nin);
-      for (uint64_t i = 0; i < nin; ++i) {
-        rebased[i] = hoff[i] - lo;
-        vec16 = vec16 && (rebased[i] % 16u) == 0;
-      }
+      for (uint64_t i = 0; i < nin; ++i) rebased[i] = hoff[i] - lo;
       QFEC_HIP(ctx->d_in.ensure(span));
       QFEC_HIP(ctx->d_off.ensure(nin * 8));
       QFEC_HIP(hipMemcpyAsync(ctx->d_in.ptr, data + lo, span, hipMemcpyHostToDevice, s));
@@ -883,18 +860,14 @@ QFEC_EXPORT int fec_encode_batch_rs(FECEncoderCtx* ctx, const uint8_t* data, con
       QFEC_HIP(ctx->d_in.ensure(nin * P));
       QFEC_HIP(hipMemcpyAsync(ctx->d_in.ptr, data, nin * P, hipMemcpyHostToDevice, s));
       d_data = ctx->d_in.as<uint8_t>();
-    } else {
-      vec16 = vec16 && aligned16(data);
     }
   }
   uint8_t* d_par = parity_out;
   if (omem != Mem::kDevice) {
     QFEC_HIP(ctx->d_out.ensure(out_bytes));
     d_par = ctx->d_out.as<uint8_t>();
-  } else {
-    vec16 = vec16 && aligned16(parity_out);
   }
-  rc = encode_dev_locked(ctx, d_data, d_off, ok, G, k, r, P, d_par, vec16, s);
+  rc = encode_dev_locked(ctx, d_data, d_off, ok, G, k, r, P, d_par, s);
   if (rc != FEC_OK) return rc;
   if (omem != Mem::kDevice)
     QFEC_HIP(hipMemcpyAsync(parity_out, d_par, out_bytes, hipMemcpyDeviceToHost, s));
@@ -956,20 +929,15 @@ QFEC_EXPORT int fec_decode_batch_rs(FECEncoderCtx* ctx, uint8_t* data, const uin
   uint8_t* d_data = data;
   const uint8_t* d_par = parity;
   const uint64_t* d_masks = masks;
-  bool vec16 = (P % 16u) == 0;
   if (dmem != Mem::kDevice) {
     QFEC_HIP(ctx->d_in.ensure(data_bytes));
     QFEC_HIP(hipMemcpyAsync(ctx->d_in.ptr, data, data_bytes, hipMemcpyHostToDevice, s));
     d_data = ctx->d_in.as<uint8_t>();
-  } else {
-    vec16 = vec16 && aligned16(data);
   }
   if (pmem != Mem::kDevice) {
     QFEC_HIP(ctx->d_out.ensure(par_bytes));
     QFEC_HIP(hipMemcpyAsync(ctx->d_out.ptr, parity, par_bytes, hipMemcpyHostToDevice, s));
     d_par = ctx->d_out.as<uint8_t>();
-  } else {
-    vec16 = vec16 && aligned16(parity);
   }
   if (mmem != Mem::kDevice) {
     QFEC_HIP(ctx->d_mask.ensure(G * 8));
@@ -977,7 +945,7 @@ QFEC_EXPORT int fec_decode_batch_rs(FECEncoderCtx* ctx, uint8_t* data, const uin
     d_masks = ctx->d_mask.as<uint64_t>();
   }
   QFEC_HIP(ctx->d_status.ensure(G));
-  rc = decode_dev_locked(ctx, d_data, d_par, d_masks, G, k, r, P, ctx->d_status.as<uint8_t>(), vec16, s);
+  rc = decode_dev_locked(ctx, d_data, d_par, d_masks, G, k, r, P, ctx->d_status.as<uint8_t>(), s);
   if (rc != FEC_OK) return rc;
   if (dmem != Mem::kDevice)
     QFEC_HIP(hipMemcpyAsync(data, d_data, data_bytes, hipMemcpyDeviceToHost, s));
@@ -1001,8 +969,7 @@ QFEC_EXPORT int fec_encode_batch_rs_dev(FECEncoderCtx* ctx, const uint8_t* d_dat
   std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard dg(ctx->device);
   if (!dg.ok) return FEC_ERR_NODEV;
-  const bool vec16 = (P % 16u) == 0 && aligned16(d_data) && aligned16(d_parity);
-  return encode_dev_locked(ctx, d_data, nullptr, qfec::OffsetKind::kNone, G, k, r, P, d_parity, vec16,
+  return encode_dev_locked(ctx, d_data, nullptr, qfec::OffsetKind::kNone, G, k, r, P, d_parity,
                            pick_stream(ctx, stream));
 }
 
@@ -1016,8 +983,7 @@ QFEC_EXPORT int fec_decode_batch_rs_dev(FECEncoderCtx* ctx, uint8_t* d_data, con
   std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard dg(ctx->device);
   if (!dg.ok) return FEC_ERR_NODEV;
-  const bool vec16 = (P % 16u) == 0 && aligned16(d_data) && aligned16(d_parity);
-  return decode_dev_locked(ctx, d_data, d_parity, d_masks, G, k, r, P, d_status, vec16,
+  return decode_dev_locked(ctx, d_data, d_parity, d_masks, G, k, r, P, d_status,
                            pick_stream(ctx, stream));
 }
 

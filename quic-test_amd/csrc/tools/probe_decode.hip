@@ -114,7 +114,6 @@ int main(int argc, char** argv) {
   dl.k = k;
   dl.r = r;
   dl.P = P;
-  dl.vec16 = true;
   struct Var {
     std::string name;
     int variant;

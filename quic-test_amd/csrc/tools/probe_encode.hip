@@ -522,7 +522,6 @@ int main(int argc, char** argv) {
     el.r = r;
     el.P = P;
     el.tables = dtab;
-    el.vec16 = true;
     vars.push_back({"enc prod launch_encode", enc_bytes, [=] { CK(launch_encode(el, nullptr)); }, {}});
     for (int w : {5, 10, 15, 20, 40}) {
       EncodeLaunch e2 = el;

@@ -402,3 +402,73 @@ def test_full_size_c4_shard_encode(gpu_ctx, oracle_mod, torch_cuda):
     gpu_ctx.decode_dev(sub, par[:Gs * r * P], dm, Gs, k, r, P, stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert torch.equal(sub, orig)
+
+
+# ---------------- any packet size, any packet address ----------------
+#
+# P >= 16 runs on the 16-byte-column kernels whatever P % 16 and the packet alignment are:
+# the last column of a packet is shifted back to end at P (fec_kernels.hip header).  These
+# cases cover every encode form (compile-time k, runtime-k loop, gathered offsets) and every
+# decode form the library picks (fused with NT = 1..4 tail pieces, mask-addressed or not,
+# the runtime-k wave kernel), with sizes around the 16-B, 256-B and 1 KiB boundaries.
+
+ANY_P = [(10, 3, 1201), (10, 3, 1350), (10, 3, 1400), (10, 3, 1452), (10, 3, 1500), (10, 3, 1023),
+         (10, 3, 1025), (10, 3, 2047), (10, 3, 3001), (10, 3, 17), (10, 3, 31), (20, 5, 1399),
+         (20, 5, 1235), (10, 1, 1350), (4, 2, 250), (4, 2, 301), (7, 4, 1399), (12, 9, 70),
+         (3, 1, 18), (16, 16, 45)]
+
+
+@pytest.mark.parametrize("k,r,P", ANY_P)
+def test_any_packet_size_round_trip(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
+    torch = torch_cuda
+    G = 67
+    data = oracle_mod.splitmix_bytes(G * k * P, SEED + 901 + k * 7 + P)
+    exp_par = oracle_mod.rs_encode(data, G, k, r, P)
+    par = np.zeros(G * r * P, dtype=np.uint8)
+    gpu_ctx.encode(data, k, r, P, par, num_groups=G)
+    assert np.array_equal(par, exp_par)
+    rng = np.random.default_rng(P * 31 + k)
+    masks = _random_masks(rng, G, k, r, r + 1)
+    broken = _poison(data, masks, G, k, P)
+    exp = broken.copy()
+    bad_exp, st_exp = oracle_mod.rs_decode(exp, exp_par, masks, G, k, r, P)
+    got = broken.copy()
+    st = np.zeros(G, dtype=np.uint8)
+    assert gpu_ctx.decode(got, exp_par, masks, k, r, P, status_out=st) == bad_exp
+    assert np.array_equal(st, st_exp)
+    assert np.array_equal(got, exp)
+    # Device views at odd byte addresses (packet bases misaligned for every dword / 16-B access).
+    for shift_d, shift_p in [(1, 3), (5, 15), (8, 0)]:
+        bd = torch.zeros(G * k * P + 32, dtype=torch.uint8, device="cuda")
+        bp = torch.zeros(G * r * P + 32, dtype=torch.uint8, device="cuda")
+        dd = bd[shift_d:shift_d + G * k * P]
+        dp = bp[shift_p:shift_p + G * r * P]
+        dd.copy_(torch.from_numpy(data))
+        gpu_ctx.encode_dev(dd, G, k, r, P, dp)
+        gpu_ctx.synchronize()
+        assert np.array_equal(dp.cpu().numpy(), exp_par), (shift_d, shift_p)
+        # guard bytes around the views untouched
+        assert int(bp[:shift_p].sum().item()) == 0 and int(bp[shift_p + G * r * P:].sum().item()) == 0
+        dd.copy_(torch.from_numpy(broken))
+        dm = _dev(torch, masks.view(np.int64))
+        dst = torch.zeros(G, dtype=torch.uint8, device="cuda")
+        gpu_ctx.decode_dev(dd, dp, dm, G, k, r, P, dst)
+        gpu_ctx.synchronize()
+        assert np.array_equal(dd.cpu().numpy(), exp), (shift_d, shift_p)
+        assert np.array_equal(dst.cpu().numpy(), st_exp)
+        assert int(bd[:shift_d].sum().item()) == 0 and int(bd[shift_d + G * k * P:].sum().item()) == 0
+
+
+@pytest.mark.parametrize("P", [1201, 1350, 37])
+def test_any_packet_size_gather_offsets_odd(gpu_ctx, oracle_mod, P):
+    """u64 offsets at arbitrary (odd) byte positions of the slab."""
+    k, r, G = 10, 3, 29
+    rng = np.random.default_rng(P)
+    slab = oracle_mod.splitmix_bytes(G * k * (P + 7) + 64, 1234 + P)
+    offs = (np.arange(G * k, dtype=np.uint64) * np.uint64(P + 7) + np.uint64(3)).astype(np.uint64)
+    offs = offs[rng.permutation(G * k)]
+    contig = np.concatenate([slab[int(o):int(o) + P] for o in offs])
+    exp = oracle_mod.rs_encode(contig, G, k, r, P)
+    par = np.zeros(G * r * P, dtype=np.uint8)
+    gpu_ctx.encode(slab, k, r, P, par, num_groups=G, offsets=offs)
+    assert np.array_equal(par, exp)
