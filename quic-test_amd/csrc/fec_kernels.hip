@@ -708,14 +708,16 @@ __global__ __launch_bounds__(256) void decode_v16(uint8_t* __restrict__ data,
 // groups with different erasure patterns, so each lane reads its own record (header and
 // tables through the vector cache; lanes of one group read the same lines) and runs the
 // multiply for every coefficient, 0 and 1 included (their tables are the zero / identity
-// maps): no lane-divergent branches except the row count e.
+// maps): no lane-divergent branches except the row count e.  The library's form for
+// packets of <= 256 B, where one group per wave would leave most lanes idle (k=10 r=3,
+// 2 erasures: 64 B 3.4 vs 0.72 TB/s, 256 B 4.6 vs 3.7; profiles/r01_probe_decode_small.txt).
 template <int K, int MAXE, int POL = 0>
-__global__ __launch_bounds__(512) void decode_tiled(uint8_t* __restrict__ data,
+__global__ __launch_bounds__(512) void decode_tiled(const uint8_t* __restrict__ data,
                                                     const uint8_t* __restrict__ parity,
                                                     const uint32_t* __restrict__ rec_off,
                                                     const uint8_t* __restrict__ codebook,
                                                     uint64_t groups, uint32_t cpp, uint32_t P,
-                                                    uint32_t r, uint32_t tile) {
+                                                    uint32_t r, uint32_t tile, uint8_t* __restrict__ out) {
   const uint32_t lane = threadIdx.x;
   uint32_t gl = lane / cpp;
   const uint32_t col = lane - gl * cpp;
@@ -729,8 +731,9 @@ __global__ __launch_bounds__(512) void decode_tiled(uint8_t* __restrict__ data,
   const uint32_t* rw = reinterpret_cast<const uint32_t*>(recp);
   const uint32_t e = rw[24] & 0xFFu;
   const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
-  uint8_t* dg = data + g * K * static_cast<uint64_t>(P);
+  const uint8_t* dg = data + g * K * static_cast<uint64_t>(P);
   const uint8_t* pg = parity + g * r * static_cast<uint64_t>(P);
+  uint8_t* og = out + g * K * static_cast<uint64_t>(P);
   const size_t coff = col_off16(col, P);
   uint32_t sw[(K + 3) / 4];
 #pragma unroll
@@ -759,7 +762,7 @@ __global__ __launch_bounds__(512) void decode_tiled(uint8_t* __restrict__ data,
   for (int m = 0; m < MAXE; ++m) {
     if (static_cast<uint32_t>(m) < e) {
       const uint32_t eid = m < 4 ? (ew >> (8 * m)) & 0xFFu : rec_byte(rw, 64 + m);
-      st16<POL>(dg + eid * static_cast<uint64_t>(P) + coff, acc[m]);
+      st16<POL>(og + eid * static_cast<uint64_t>(P) + coff, acc[m]);
     }
   }
 }
@@ -1039,21 +1042,35 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
 }
 
 // The fused form for this (k, r, P), if instantiated; hipErrorNotSupported otherwise.
+// Instantiated for every P in (256, 2048] of the compiled (k, r) shapes: NM 16-B and NT 4-B
+// pieces per lane.  r <= 3 shapes only in the mask-addressed form (the one auto uses for
+// them), r > 3 only in the record-addressed one; k=10 r=3 1200 B in both (probes).
+// Measured at k=10 r=3, 2 erasures (tools/probe_decode.hip): 512 B 5.89 TB/s vs 3.12 for
+// the looped wave kernel, 768 B 5.49 vs 3.24 (profiles/r01_probe_decode_small.txt).
 hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct) {
   const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
-#define QFEC_FUSED(KK, RR, NMM, NTT)                                                          \
-  if (a.k == KK && a.r == RR && nm == NMM && nt == NTT)                                       \
-    return direct ? run_decode_fused<KK, RR, kNtStore, NMM, NTT, true>(a, s)                  \
-                  : run_decode_fused<KK, RR, kNtStore, NMM, NTT, false>(a, s);
-  QFEC_FUSED(10, 3, 1, 1)
-  QFEC_FUSED(10, 3, 1, 2)   // 1281..1536 B: 1350 / 1400 / 1452 / 1500-B packets
-  QFEC_FUSED(20, 5, 1, 1)
-  QFEC_FUSED(20, 5, 1, 2)
-  QFEC_FUSED(10, 1, 1, 1)
-  QFEC_FUSED(4, 2, 0, 1)
-#undef QFEC_FUSED
+#define QFEC_FUSED_D(KK, RR, NMM, NTT)                                                        \
+  if (direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                             \
+    return run_decode_fused<KK, RR, kNtStore, NMM, NTT, true>(a, s);
+#define QFEC_FUSED_R(KK, RR, NMM, NTT)                                                        \
+  if (!direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                            \
+    return run_decode_fused<KK, RR, kNtStore, NMM, NTT, false>(a, s);
+#define QFEC_FUSED_P(M, KK, RR)                                                               \
+  M(KK, RR, 0, 2) M(KK, RR, 0, 3) M(KK, RR, 0, 4) M(KK, RR, 1, 0) M(KK, RR, 1, 1)            \
+  M(KK, RR, 1, 2) M(KK, RR, 1, 3) M(KK, RR, 1, 4)
+  QFEC_FUSED_P(QFEC_FUSED_D, 10, 3)
+  QFEC_FUSED_R(10, 3, 1, 1)
+  QFEC_FUSED_P(QFEC_FUSED_R, 20, 5)
+  QFEC_FUSED_P(QFEC_FUSED_D, 10, 1)
+  QFEC_FUSED_P(QFEC_FUSED_D, 4, 2)
+#undef QFEC_FUSED_P
+#undef QFEC_FUSED_R
+#undef QFEC_FUSED_D
   return hipErrorNotSupported;
 }
+
+// Packets of at most this size decode in the tiled form (several groups per wave).
+constexpr uint32_t kTiledMaxP = 256;
 
 template <int K, int MAXE, int POL>
 hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s) {
@@ -1067,7 +1084,7 @@ hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s)
     hipLaunchKernelGGL((decode_tiled<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(bs), 0, s,
                        a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                        a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, cpp,
-                       a.P, a.r, tile);
+                       a.P, a.r, tile, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P));
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -1098,9 +1115,10 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     return hipSuccess;
   }
   const uint32_t tile = pick_tile((a.P + 15u) / 16u, a.k, a.P);
-  const bool separate_out = a.out != nullptr && a.out != a.data;  // only decode_wave supports it
-  if (!separate_out && tile > 0 && (a.variant == kDecodeTiledPlain || a.variant == kDecodeTiledNt)) {
-    const bool nt = a.variant == kDecodeTiledNt;
+  const bool separate_out = a.out != nullptr && a.out != a.data;  // decode_v16 lacks it
+  const bool tiled_auto = a.variant == kDecodeAuto && a.P <= kTiledMaxP;
+  if (tile > 0 && (tiled_auto || a.variant == kDecodeTiledPlain || a.variant == kDecodeTiledNt)) {
+    const bool nt = a.variant != kDecodeTiledPlain;
 #define QFEC_TILED(KK, RR)                                                                   \
   if (a.k == KK && a.r == RR)                                                                \
     return nt ? run_decode_tiled<KK, RR, kNtStore>(a, tile, s) : run_decode_tiled<KK, RR, 0>(a, tile, s);

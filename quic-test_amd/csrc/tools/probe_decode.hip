@@ -62,7 +62,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dtab, tab.size() * 32));
     CK(hipMemcpy(dtab, tab.data(), tab.size() * 32, hipMemcpyHostToDevice));
   }
-  EncodeLaunch el{data, nullptr, OffsetKind::kNone, par, G, k, r, P, dtab, true};
+  EncodeLaunch el{data, nullptr, OffsetKind::kNone, par, G, k, r, P, dtab};
   CK(launch_encode(el, nullptr));
   CK(hipMemcpy(orig, data, nd, hipMemcpyDeviceToDevice));
   // exactly `ners` erasures per group, uniform over the k + r shards
@@ -152,6 +152,16 @@ int main(int argc, char** argv) {
   PV("reads dense cap12", 12, kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)               \
   PV("reads dense cap16", 16, kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)               \
   PV("reads dense nt-load", -1, kNtLoad | kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)
+  if (P < 1024) vars.push_back({"tiled nt", kDecodeTiledNt, -1, -1, {}});
+#define PF(NAME, NT)                                                                             \
+  vars.push_back({NAME, kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {                \
+                    probe(a);                                                                    \
+                    return run_decode_fused<10, 3, kNtStore, 0, NT, true>(a, nullptr);           \
+                  }});
+  if (k == 10 && r == 3 && P <= 256) PF("fused direct 4B x1", 1)
+  if (k == 10 && r == 3 && P > 256 && P <= 512) PF("fused direct 4B x2", 2)
+  if (k == 10 && r == 3 && P > 512 && P <= 768) PF("fused direct 4B x3", 3)
+  if (k == 10 && r == 3 && P > 768 && P <= 1024) PF("fused direct 4B x4", 4)
   if (k == 10 && r == 3 && P == 1200) {
     PSET(1, 1)
   } else if (k == 10 && r == 3 && P == 1024) {

@@ -3,7 +3,7 @@
 # Each line: P, verified, encode ms and algorithmic GB/s, decode (2 erasures/group) ms and GB/s.
 # Usage (GPU box): bash scripts/size_sweep.sh [P ...] > gpurun_out/size_sweep.txt
 set -euo pipefail
-SIZES=${*:-"64 256 512 1024 1200 1201 1350 1400 1452 1472 1500 2048"}
+SIZES=${*:-"64 128 256 384 512 768 1024 1200 1201 1350 1400 1452 1472 1500 1800 2048"}
 for P in $SIZES; do
   G=$((12000000000 / (10 * P)))
   printf "P=%s " "$P"
