@@ -230,7 +230,8 @@ def cpu_baseline(cfg: dict, seconds: float = 8.0) -> dict:
 def e2e_pinned(ctx, d_data, d_parity, d_masks, G: int, cfg: dict, reps: int = 3) -> dict:
     """The path as the QUIC client/server sees it: packets start and end in host memory.
     Page-locked host buffers (the same allocator kind as fec_alloc_slab) go through the
-    synchronous API, which pipelines ~64 MB chunks H2D -> kernel -> D2H on 3 streams."""
+    synchronous API, whose kernels then read and write them in place over PCIe (zero-copy;
+    QUICFEC_SMALL_CALL_BYTES=0 selects the 3-stream H2D -> kernel -> D2H pipeline instead)."""
     import torch
     k, r, P = cfg["k"], cfg["r"], cfg["P"]
     h_data = torch.empty(d_data.numel(), dtype=torch.uint8, pin_memory=True)

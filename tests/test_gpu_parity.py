@@ -225,9 +225,12 @@ def test_single_loss_is_reference_xor_recovery(gpu_ctx, oracle_mod):
         assert np.array_equal(got[(g * k + mid) * P:(g * k + mid + 1) * P], rec)
 
 
-@pytest.mark.parametrize("pinned", [True, False])
-def test_host_pipeline_multi_chunk(gpu_ctx, oracle_mod, torch_cuda, pinned):
-    """Host-resident batches larger than one 64 MB pipeline chunk (5 chunks over 3 slots)."""
+@pytest.mark.parametrize("pinned,dma", [(True, False), (True, True), (False, False)])
+def test_host_pipeline_multi_chunk(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, pinned, dma):
+    """Host-resident batches larger than one 64 MB pipeline chunk (5 chunks over 3 slots);
+    page-locked buffers run zero-copy unless QUICFEC_SMALL_CALL_BYTES=0 forces the DMA path."""
+    if dma:
+        monkeypatch.setenv("QUICFEC_SMALL_CALL_BYTES", "0")
     k, r, P, G = 10, 3, 1200, 27_000
     data = oracle_mod.splitmix_bytes(G * k * P, SEED + 11)
     exp = oracle_mod.rs_encode(data, G, k, r, P, nthreads=8)
@@ -257,14 +260,16 @@ def test_host_pipeline_multi_chunk(gpu_ctx, oracle_mod, torch_cuda, pinned):
     assert np.array_equal(hb, ref)
 
 
-@pytest.mark.parametrize("k,r,P,pinned", [(10, 3, 1200, True), (10, 3, 1200, False), (20, 5, 96, False),
-                                          (10, 3, 100, True), (4, 2, 256, False)])
-def test_host_decode_compacted_sparse_loss(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, k, r, P, pinned):
+@pytest.mark.parametrize("k,r,P,pinned,dma", [(10, 3, 1200, True, True), (10, 3, 1200, True, False),
+                                              (10, 3, 1200, False, False), (20, 5, 96, False, False),
+                                              (10, 3, 100, True, True), (4, 2, 256, False, False)])
+def test_host_decode_compacted_sparse_loss(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, k, r, P, pinned, dma):
     """Host-resident decode under iid loss (satellite profile, network_profiles.go:78): at most
     half the groups need work, so only those cross PCIe (gathered, decoded, scattered back).
     Small pipeline chunks so the 3 slots rotate several times; some groups unrecoverable."""
     G = 6_000
     monkeypatch.setenv("QUICFEC_PIPE_CHUNK_BYTES", str(k * P * 97))
+    monkeypatch.setenv("QUICFEC_SMALL_CALL_BYTES", "0" if dma else "1000000000000" if pinned else "")
     data = oracle_mod.splitmix_bytes(G * k * P, SEED + 21 + k + P)
     par = oracle_mod.rs_encode(data, G, k, r, P, nthreads=8)
     rng = np.random.default_rng(k * 7 + P)
@@ -472,3 +477,63 @@ def test_any_packet_size_gather_offsets_odd(gpu_ctx, oracle_mod, P):
     par = np.zeros(G * r * P, dtype=np.uint8)
     gpu_ctx.encode(slab, k, r, P, par, num_groups=G, offsets=offs)
     assert np.array_equal(par, exp)
+
+
+# ---------------- small host-resident calls: zero-copy vs DMA ----------------
+#
+# Calls of at most QUICFEC_SMALL_CALL_BYTES (default 1 MiB) run the kernels directly on
+# page-locked host memory (the caller's, or the context's staging); 0 forces the DMA paths.
+
+@pytest.mark.parametrize("small", ["0", None])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_small_calls_zero_copy_and_dma(gpu_ctx, quicfec_mod, oracle_mod, xor_golden, manifest, torch_cuda,
+                                       monkeypatch, small, pinned):
+    import ctypes
+    if small is None:
+        monkeypatch.delenv("QUICFEC_SMALL_CALL_BYTES", raising=False)
+    else:
+        monkeypatch.setenv("QUICFEC_SMALL_CALL_BYTES", small)
+    torch = torch_cuda
+
+    def host(a):
+        return torch.from_numpy(np.ascontiguousarray(a)).pin_memory() if pinned else np.ascontiguousarray(a).copy()
+
+    def npy(a):
+        return a.numpy() if pinned else a
+
+    # legacy fec_encode_batch: golden fixture, and scattered offsets into a larger slab
+    c = next(c for c in manifest["cases"] if c["name"] == "batch_k10_p1200_g64")
+    G, P = c["G"], c["P"]
+    slab = host(oracle_mod.splitmix_bytes(G * 10 * P, c["seed"]))
+    offs = (np.arange(G * 10, dtype=np.uint32) * P).astype(np.uint32)
+    rep = host(np.zeros(G * P, dtype=np.uint8))
+    assert gpu_ctx.encode_batch_legacy(slab, offs, G, P, rep) == 0
+    assert np.array_equal(npy(rep), xor_golden["batch_k10_p1200_g64"])
+    c = next(c for c in manifest["cases"] if c["name"] == "batch_scattered_p100_g16")
+    slab = host(oracle_mod.splitmix_bytes(c["slab_bytes"], c["seed"]))
+    rep = host(np.zeros(c["G"] * c["P"], dtype=np.uint8))
+    assert gpu_ctx.encode_batch_legacy(slab, xor_golden["batch_scattered_p100_g16_offsets"], c["G"], c["P"], rep) == 0
+    assert np.array_equal(npy(rep), xor_golden["batch_scattered_p100_g16"])
+    # batch API, one group and a few, odd packet size
+    for k, r, P, G in [(10, 3, 1200, 1), (10, 3, 1201, 7), (20, 5, 1200, 3), (4, 2, 256, 40)]:
+        data = oracle_mod.splitmix_bytes(G * k * P, SEED + 5000 + G + P)
+        exp = oracle_mod.rs_encode(data, G, k, r, P)
+        hd, hp = host(data), host(np.zeros(G * r * P, dtype=np.uint8))
+        gpu_ctx.encode(hd, k, r, P, hp, num_groups=G)
+        assert np.array_equal(npy(hp), exp), (k, r, P, G)
+        rng = np.random.default_rng(G + P)
+        masks = _random_masks(rng, G, k, r, r + 1)
+        masks[0] = np.uint64(1)  # at least one rebuilt group
+        broken = _poison(data, masks, G, k, P)
+        ref = broken.copy()
+        bad_exp, st_exp = oracle_mod.rs_decode(ref, exp, masks, G, k, r, P)
+        hb = host(broken)
+        st = np.zeros(G, dtype=np.uint8)
+        assert gpu_ctx.decode(hb, hp, masks, k, r, P, status_out=st, num_groups=G) == bad_exp
+        assert np.array_equal(st, st_exp)
+        assert np.array_equal(npy(hb), ref), (k, r, P, G)
+    # xor_packets_* (context-free entry point): ten host packets
+    pk = [oracle_mod.splitmix_bytes(1200, 77 + i) for i in range(10)]
+    out = np.zeros(1200, dtype=np.uint8)
+    quicfec_mod.xor_packets(pk, 1200, out)
+    assert np.array_equal(out, oracle_mod.xor_packets(pk, 1200))
