@@ -217,6 +217,12 @@ Mem classify_ptr(const void* p, void** dev = nullptr) {
 // CPU memcpy and break even near 3 MB.  QUICFEC_SMALL_CALL_BYTES overrides both limits
 // (0 = always DMA).
 constexpr uint64_t kZeroCopyPinnedBytes = ~0ull;
+
+// Completion wait of the zero-copy calls.  The runtime's blocking wait: polling
+// hipStreamQuery from the calling thread measured slower (one group: 20 vs 15.5 us;
+// profiles/r01_latency_sweep.txt).
+hipError_t wait_stream(hipStream_t s) { return hipStreamSynchronize(s); }
+
 constexpr uint64_t kZeroCopyStagedBytes = 2ull << 20;
 uint64_t small_call_bytes(bool all_pinned) {  // read per call: tests switch paths in one process
   const char* v = std::getenv("QUICFEC_SMALL_CALL_BYTES");
@@ -643,7 +649,7 @@ int encode_host_zero_copy(FECEncoderCtx* ctx, const uint8_t* data, Mem dmem, voi
   if (rc == FEC_OK) rc = zc_view(ctx->z_out, parity_out, omem, odev, out_bytes, false, &dst, &out_staged);
   if (rc == FEC_OK) rc = encode_dev_locked(ctx, src, nullptr, qfec::OffsetKind::kNone, G, k, r, P, dst, ctx->stream);
   if (rc != FEC_OK) return rc;
-  QFEC_HIP(hipStreamSynchronize(ctx->stream));
+  QFEC_HIP(wait_stream(ctx->stream));
   if (out_staged) std::memcpy(parity_out, ctx->z_out.ptr, out_bytes);
   return FEC_OK;
 }
@@ -662,7 +668,7 @@ int decode_host_zero_copy(FECEncoderCtx* ctx, uint8_t* data, Mem dmem, void* dde
   std::memcpy(ctx->z_aux.ptr, masks, G * 8);
   rc = decode_dev_locked(ctx, d, p, ctx->z_aux.dev_as<uint64_t>(), G, k, r, P, nullptr, ctx->stream);
   if (rc != FEC_OK) return rc;
-  QFEC_HIP(hipStreamSynchronize(ctx->stream));
+  QFEC_HIP(wait_stream(ctx->stream));
   if (d_staged) {  // only erased data packets changed (unrecoverable groups: untouched bytes)
     const uint64_t kmask = (1ull << k) - 1;
     const uint8_t* z = ctx->z_in.as<uint8_t>();
@@ -712,7 +718,7 @@ void xor_packets_gpu(const uint8_t* packets[], size_t n, size_t packet_size, uin
       if (encode_dev_locked(ctx, ctx->z_in.dev_as<uint8_t>(), nullptr, qfec::OffsetKind::kNone, 1,
                             static_cast<uint32_t>(n), 1, P, ctx->z_out.dev_as<uint8_t>(), ctx->stream) != FEC_OK)
         return;
-      if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      if (wait_stream(ctx->stream) != hipSuccess) {
         set_error("xor_packets: kernel failed");
         return;
       }
@@ -839,7 +845,7 @@ QFEC_EXPORT int fec_encode_batch(FECEncoderCtx* ctx, const uint8_t* slab, const 
         rc = encode_dev_locked(ctx, zs, ctx->z_aux.dev_as<uint32_t>(), qfec::OffsetKind::kU32, num_groups, kPackets,
                                1, packet_size, zr, s);
       if (rc != FEC_OK) return rc;
-      QFEC_HIP(hipStreamSynchronize(s));
+      QFEC_HIP(wait_stream(s));
       if (out_staged) std::memcpy(repair_out, ctx->z_out.ptr, uint64_t(num_groups) * P);
       return 0;
     }

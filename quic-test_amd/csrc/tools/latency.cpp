@@ -1,7 +1,7 @@
 // latency.cpp — per-call latency of the host-resident C-ABI at small batch sizes, called
 // the way the reference's cgo wrapper calls it (fec_cgo.go:138: one fec_encode_batch per
-// EncodeBatch, today with a single group per call, encoder_hybrid.go:115).  Links only
-// libfec_hip.so.  Not part of the library.
+// EncodeBatch, today with a single group per call, encoder_hybrid.go:115).  Links
+// libfec_hip.so (and the HIP runtime for the device-resident floor).  Not part of the library.
 //
 //   latency [calls_per_point]   ->  one JSON object per line
 #include <algorithm>
@@ -11,6 +11,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "fec_hip.h"
 
@@ -66,6 +68,15 @@ int main(int argc, char** argv) {
   // fec_encode_batch with nothing to do: the cost of crossing the C-ABI alone
   run_point("fec_encode_batch (0 groups)", "-", 0, k, P, calls,
             [&] { return fec_encode_batch(ctx, slab, off.data(), 0, P, rep); });
+  // Floor: the same kernel on device-resident buffers (no PCIe), launch + synchronize.
+  void *d_in = nullptr, *d_out = nullptr;
+  if (hipMalloc(&d_in, k * P) == hipSuccess && hipMalloc(&d_out, r * P) == hipSuccess) {
+    run_point("fec_encode_batch_rs_dev r=3 + fec_synchronize", "device", 1, k, P, calls, [&] {
+      const int rc = fec_encode_batch_rs_dev(ctx, static_cast<uint8_t*>(d_in), 1, k, r, P, static_cast<uint8_t*>(d_out),
+                                             nullptr);
+      return rc != 0 ? rc : fec_synchronize(ctx);
+    });
+  }
   for (uint64_t G : {1ull, 4ull, 16ull, 64ull, 256ull, 1024ull, 4096ull, 16384ull}) {
     run_point("fec_encode_batch", "pinned", G, k, P, calls,
               [&] { return fec_encode_batch(ctx, slab, off.data(), static_cast<uint32_t>(G), P, rep); });
@@ -77,6 +88,8 @@ int main(int argc, char** argv) {
       return fec_decode_batch_rs(ctx, slab, rep, masks.data(), G, k, r, P, nullptr, nullptr);
     });
   }
+  (void)hipFree(d_in);
+  (void)hipFree(d_out);
   fec_free_slab(slab);
   fec_free_repair_buffer(rep);
   fec_encoder_free(ctx);
