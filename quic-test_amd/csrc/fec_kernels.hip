@@ -46,7 +46,7 @@ constexpr int kNtLoad = 1;        // non-temporal loads (data read once)
 constexpr int kNtStore = 2;       // non-temporal stores
 constexpr int kNoCoefBranch = 4;  // decode: multiply by every coefficient, no 0/1 branches
 constexpr int kProbeXorOnly = 8;   // probes only: decode_fused XORs instead of multiplying
-constexpr int kProbeNoStore = 16; // probes only: decode_fused never stores (read pattern alone)
+constexpr int kProbeNoStore = 16; // probes only: decode_fused never stores (read pattern alone, xor-only path too)
 constexpr int kProbeDense = 32;   // probes only: decode_fused reads data shards 0..K-1, no parity
 
 template <int POL>
@@ -530,6 +530,9 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
       load(shard(sid[s]), v);
 #pragma unroll
       for (int q = 0; q < NW; ++q) acc[q] ^= v[q];
+    }
+    if constexpr ((POL & kProbeNoStore) != 0) {
+      if (acc[0] != 0x9E3779B9u || acc[NW - 1] != 0x7F4A7C15u) return;
     }
     store(og + erased(0) * static_cast<uint64_t>(P), acc);
     return;
@@ -1046,12 +1049,15 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
 // pieces per lane.  r <= 3 shapes only in the mask-addressed form (the one auto uses for
 // them), r > 3 only in the record-addressed one; k=10 r=3 1200 B in both (probes).
 // Measured at k=10 r=3, 2 erasures (tools/probe_decode.hip): 512 B 5.89 TB/s vs 3.12 for
-// the looped wave kernel, 768 B 5.49 vs 3.24 (profiles/r01_probe_decode_small.txt).
+// the looped wave kernel, 768 B 5.49 vs 3.24 (profiles/r01_probe_decode_small.txt).  The
+// mask-addressed forms also load non-temporally (survivors are read once): +1.2..3.2% at
+// 512 / 768 / 1200 / 1400 B in one process (profiles/r01_probe_decode_ntload.txt); loads
+// alone without NT stores lose 14%.
 hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct) {
   const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
 #define QFEC_FUSED_D(KK, RR, NMM, NTT)                                                        \
   if (direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                             \
-    return run_decode_fused<KK, RR, kNtStore, NMM, NTT, true>(a, s);
+    return run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true>(a, s);
 #define QFEC_FUSED_R(KK, RR, NMM, NTT)                                                        \
   if (!direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                            \
     return run_decode_fused<KK, RR, kNtStore, NMM, NTT, false>(a, s);

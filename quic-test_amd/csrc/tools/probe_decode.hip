@@ -134,6 +134,8 @@ int main(int argc, char** argv) {
       if (v.name.rfind("auto", 0) == 0 || v.name.rfind("direct xcd", 0) == 0) keep.push_back(v);
     vars.swap(keep);
   }
+  uint8_t* oop = nullptr;  // separate output buffer for the out-of-place probe
+  CK(hipMalloc(&oop, nd));
   auto probe = [](const DecodeLaunch& a) -> hipError_t {
     hipLaunchKernelGGL(classify, dim3(blocks_for(a.groups)), dim3(256), 0, nullptr, a.masks, a.groups, a.k, a.r,
                        a.binom, a.meta, a.rec_off, a.status);
@@ -154,15 +156,47 @@ int main(int argc, char** argv) {
   PV("reads dense nt-load", -1, kNtLoad | kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)
   if (P < 1024) vars.push_back({"tiled nt", kDecodeTiledNt, -1, -1, {}});
 #define PF(NAME, NT)                                                                             \
+  {                                                                                              \
   vars.push_back({NAME, kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {                \
                     probe(a);                                                                    \
                     return run_decode_fused<10, 3, kNtStore, 0, NT, true>(a, nullptr);           \
-                  }});
+                  }});                                                                           \
+  vars.push_back({NAME " nt-load", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {     \
+                    probe(a);                                                                    \
+                    return run_decode_fused<10, 3, kNtStore | kNtLoad, 0, NT, true>(a, nullptr); \
+                  }});                                                                           \
+  }
   if (k == 10 && r == 3 && P <= 256) PF("fused direct 4B x1", 1)
   if (k == 10 && r == 3 && P > 256 && P <= 512) PF("fused direct 4B x2", 2)
   if (k == 10 && r == 3 && P > 512 && P <= 768) PF("fused direct 4B x3", 3)
   if (k == 10 && r == 3 && P > 768 && P <= 1024) PF("fused direct 4B x4", 4)
+#define PVD(NAME, CAP, POLF, NM, NT)                                                             \
+  vars.push_back({NAME, kDecodeFused, CAP, 1, {}, [probe](const DecodeLaunch& a) {               \
+                    probe(a);                                                                    \
+                    return run_decode_fused<10, 3, (POLF), NM, NT, true>(a, nullptr);            \
+                  }});
+  if (k == 10 && r == 3 && P > 1280 && P <= 1536) {
+    PVD("pol direct nt-store", -1, kNtStore, 1, 2)
+    PVD("pol direct nt-load+store", -1, kNtStore | kNtLoad, 1, 2)
+  }
   if (k == 10 && r == 3 && P == 1200) {
+    PVD("pol direct nt-store", -1, kNtStore, 1, 1)
+    PVD("pol direct nt-load+store", -1, kNtStore | kNtLoad, 1, 1)
+    PVD("pol direct nt-load", -1, kNtLoad, 1, 1)
+    PVD("pol direct plain", -1, 0, 1, 1)
+    PVD("pol direct nt-load+store cap12", 12, kNtStore | kNtLoad, 1, 1)
+    PVD("pol direct reads-only", -1, kProbeNoStore | kProbeXorOnly, 1, 1)
+    PVD("pol direct reads-only nt-load", -1, kNtLoad | kProbeNoStore | kProbeXorOnly, 1, 1)
+    PVD("pol dense reads-only", -1, kProbeNoStore | kProbeXorOnly | kProbeDense, 1, 1)
+    vars.push_back({"pol encode (same buffers)", kDecodeFused, -1, 1, {}, [el](const DecodeLaunch&) {
+                      return launch_encode(el, nullptr);  // rewrites identical parity
+                    }});
+    vars.push_back({"pol out-of-place", kDecodeFused, -1, 1, {}, [probe, oop](const DecodeLaunch& a) {
+                      probe(a);
+                      DecodeLaunch b = a;
+                      b.out = oop;
+                      return run_decode_fused<10, 3, kNtStore, 1, 1, true>(b, nullptr);
+                    }});
     PSET(1, 1)
   } else if (k == 10 && r == 3 && P == 1024) {
     PSET(1, 0)
