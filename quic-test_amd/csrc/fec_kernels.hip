@@ -25,6 +25,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "fec_kernels.hpp"
 
@@ -48,6 +49,13 @@ constexpr int kNoCoefBranch = 4;  // decode: multiply by every coefficient, no 0
 constexpr int kProbeXorOnly = 8;   // probes only: decode_fused XORs instead of multiplying
 constexpr int kProbeNoStore = 16; // probes only: decode_fused never stores (read pattern alone, xor-only path too)
 constexpr int kProbeDense = 32;   // probes only: decode_fused reads data shards 0..K-1, no parity
+// decode_fused: coefficient tables through LDS.  A record-addressed wave reads e*K 32-B
+// table entries of its group's record.  For large codebooks (k=20 r=5: 53,130 records,
+// 143 MB) the records miss the scalar cache, and one scalar load per coefficient — a few
+// in flight at a time — stalls the wave for several memory round trips per group.  With
+// this bit the wave fetches its rows with vector loads issued next to its survivor loads
+// (one round trip) and reads them from a per-wave LDS slice.
+constexpr int kLdsTabs = 64;
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
@@ -290,6 +298,39 @@ __global__ __launch_bounds__(256) void classify(const uint64_t* __restrict__ mas
   if (status) status[g] = st;
 }
 
+// C(n, t) for t = 1..3 without the table (the mask-addressed decode ranks inline; its
+// shapes have r <= 3, so e <= 3).  n < t gives 0 like the table.
+__device__ __forceinline__ uint64_t choose_small(uint32_t n, uint32_t t) {
+  const uint64_t a = n, b = n - 1u, c = n - 2u;
+  return t == 1u ? a : t == 2u ? (a * b) >> 1 : (a * b * c) / 6u;
+}
+
+// Per-wave LDS slice of N coefficient entries (decode_fused with kLdsTabs; 4 waves per
+// workgroup).  Only instantiated by the kernels that use it.
+template <int N>
+__device__ __forceinline__ Tab* wave_tabs_lds() {
+  __shared__ __attribute__((aligned(16))) Tab t[4 * N];
+  return t + (threadIdx.x >> 6) * N;
+}
+
+// f(std::integral_constant<int, n>) for a wave-uniform n in [1, N]: one straight-line body
+// per row count.
+template <int N, typename F>
+__device__ __forceinline__ void for_row_count(uint32_t n, F& f) {
+  if constexpr (N >= 1) {
+    if (n == static_cast<uint32_t>(N)) {
+      f(std::integral_constant<int, N>{});
+      return;
+    }
+    for_row_count<N - 1>(n, f);
+  }
+}
+
+// Codebook levels e = 1..3 for the inline classify of the mask-addressed decode.
+struct RankMeta {
+  uint64_t base[4], stride[4], count_r[4];
+};
+
 __device__ __forceinline__ uint32_t rec_byte(const uint32_t* __restrict__ w, uint32_t i) {
   return (w[i >> 2] >> (8u * (i & 3u))) & 0xFFu;
 }
@@ -421,14 +462,21 @@ __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, co
 // read only for its coefficient tables, behind the data loads.  Same ids in the same order
 // as the record (gf256.hpp build_record: surviving data ascending, then the e lowest
 // surviving parity rows; erased data ascending).
-template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false>
+//
+// INLINE (mask-addressed only, e <= 3): the kernel classifies its group itself — status
+// byte, colex ranks of the erased data set and of the parity rows used, record offset,
+// exactly as `classify` does — so no classify launch (and no rec_off round trip through
+// HBM) precedes it.  One launch per decode call instead of two.
+template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false, bool INLINE = DIRECT>
 __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ data,
                                                     const uint8_t* __restrict__ parity,
                                                     const uint32_t* __restrict__ rec_off,
                                                     const uint8_t* __restrict__ codebook,
                                                     uint64_t groups, uint32_t P, uint32_t r, uint32_t m0,
                                                     uint8_t* __restrict__ out, uint32_t never, uint32_t swz,
-                                                    const uint64_t* __restrict__ masks) {
+                                                    const uint64_t* __restrict__ masks, RankMeta rm,
+                                                    uint8_t* __restrict__ status) {
+  static_assert(!INLINE || (DIRECT && MAXE <= 3), "inline classify: mask-addressed forms with r <= 3");
   extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];  // see encode_v16
   if (never) occupancy_lds[threadIdx.x] = 0;
   constexpr int NW = 4 * NM + NT;  // dwords per lane and survivor
@@ -436,17 +484,40 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   if (gw >= groups) return;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t rec = __builtin_amdgcn_readfirstlane(rec_off[gw]);
-  if (rec >= kRecBad) return;
-  const uint8_t* recp = codebook + static_cast<uint64_t>(rec) * 32u;
+  constexpr uint64_t kmask = (1ull << K) - 1;
+  const uint64_t m = DIRECT ? masks[gw] : 0;
+  uint64_t rec_byte_off;
+  if constexpr (INLINE) {
+    uint64_t dm = m & kmask;
+    const uint64_t rmask = (1ull << r) - 1;
+    const uint64_t pm = (m >> K) & rmask;
+    const uint32_t ne = static_cast<uint32_t>(__popcll(dm));
+    const bool bad = ne > r - static_cast<uint32_t>(__popcll(pm));
+    if (status != nullptr && lane == 0) status[gw] = bad ? 1 : 0;
+    if (ne == 0 || bad) return;
+    uint64_t rank_e = 0, rank_r = 0;
+    for (uint32_t t = 0; dm; ++t) {
+      rank_e += choose_small(static_cast<uint32_t>(__builtin_ctzll(dm)), t + 1u);
+      dm &= dm - 1;
+    }
+    uint64_t sp = ~pm & rmask;
+    for (uint32_t t = 0; t < ne; ++t) {
+      rank_r += choose_small(static_cast<uint32_t>(__builtin_ctzll(sp)), t + 1u);
+      sp &= sp - 1;
+    }
+    rec_byte_off = rm.base[ne] + (rank_e * rm.count_r[ne] + rank_r) * rm.stride[ne];
+  } else {
+    const uint32_t rec = __builtin_amdgcn_readfirstlane(rec_off[gw]);
+    if (rec >= kRecBad) return;
+    rec_byte_off = static_cast<uint64_t>(rec) * 32u;
+  }
+  const uint8_t* recp = codebook + rec_byte_off;
   const uint32_t* rw = reinterpret_cast<const uint32_t*>(recp);
   uint32_t e;
   bool xor_only;
   // DIRECT: survivor ids (ascending bits of `surv`) and erased ids (bits of `lost`).
   uint64_t surv = 0, lost = 0;
   if constexpr (DIRECT) {
-    const uint64_t m = masks[gw];
-    constexpr uint64_t kmask = (1ull << K) - 1;
     lost = m & kmask;
     e = static_cast<uint32_t>(__popcll(lost));
     uint64_t alive = ~(m >> K) & ((r >= 64 ? 0ull : (1ull << r)) - 1);
@@ -537,9 +608,89 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
     store(og + erased(0) * static_cast<uint64_t>(P), acc);
     return;
   }
+  // kLdsTabs: the wave's coefficient rows [m0, m0 + MAXE) come in with vector loads issued
+  // next to the survivor loads and are read back from LDS, instead of one scalar load per
+  // coefficient (records of large codebooks miss the scalar cache; see kLdsTabs).
+  constexpr bool kLds = (POL & kLdsTabs) != 0;
+  constexpr int kTabPieces = MAXE * K * 2;  // 16-B pieces of MAXE rows of K entries
+  constexpr int kTabIter = kLds ? (kTabPieces + 63) / 64 : 1;
+  const uint32_t tab_pieces = (e - m0 < MAXE ? e - m0 : MAXE) * K * 2u;
+  // the slice holds kTabIter whole wave-loads (16 B per lane), so no load writes past it
+  constexpr int kSliceTabs = kTabIter * 64 / 2;
+  if constexpr (kLds) {
+    // direct-to-LDS loads (global_load_lds_dwordx4: LDS address = wave base + lane * 16, no
+    // VGPR destination); pieces past the rows re-read the last piece into unused slots
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(tabs + m0 * K);
+    uint8_t* dst = reinterpret_cast<uint8_t*>(wave_tabs_lds<kSliceTabs>());
+#pragma unroll
+    for (int i = 0; i < kTabIter; ++i) {
+      uint32_t idx = lane + 64u * i;
+      if (idx >= tab_pieces) idx = tab_pieces - 1u;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + idx * 16u),
+                                       (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+    }
+  }
+  // kLds: survivors stream through a window of kWin loads in flight (survivor s + kWin is
+  // loaded as survivor s is consumed), so K = 20 needs ~half the data VGPRs and the wave
+  // keeps 4 waves per SIMD; the first window is in flight with the table loads.
+  constexpr int kWin = kLds ? (K < 10 ? K : 10) : K;
   uint32_t x[K][NW];
 #pragma unroll
-  for (int s = 0; s < K; ++s) load(shard(sid[s]), x[s]);
+  for (int s = 0; s < kWin; ++s) load(shard(sid[s]), x[s]);
+  const Tab* rt = tabs + m0 * K;  // rows of this pass: entry (m, s) at rt[m * K + s]
+  if constexpr (kLds) {
+    // Wait for every load so far (vmcnt(0): the compiler may order the survivor loads
+    // around the LDS loads, so no counted wait), then keep LDS reads below the wait.
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const Tab* lt = wave_tabs_lds<kSliceTabs>();
+    // Straight-line body per row count NR (no branch on the row index or the coefficient:
+    // table values are VGPRs here, and the 0 / 1 entries are the zero / identity maps).
+    auto rebuild = [&](auto nr_c) __attribute__((always_inline)) {
+      constexpr int NR = decltype(nr_c)::value;
+      uint32_t acc[NR][NW];
+#pragma unroll
+      for (int m = 0; m < NR; ++m)
+#pragma unroll
+        for (int q = 0; q < NW; ++q) acc[m][q] = 0;
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        // survivor s's selectors, table reads and the next window load stay in its
+        // iteration (the compiler otherwise hoists them all: 472 VGPRs + AGPRs, one wave
+        // per SIMD)
+#pragma unroll
+        for (int q = 0; q < NW; ++q) __asm__ volatile("" : "+v"(x[s][q]));
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + kWin < K) load(shard(sid[s + kWin]), x[s + kWin]);  // folded when unrolled
+        uint32_t s0[NW], s1[NW], s2[NW];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          s0[q] = x[s][q] & 0x07070707u;
+          s1[q] = (x[s][q] >> 3) & 0x07070707u;
+          s2[q] = (x[s][q] >> 6) & 0x03030303u;
+        }
+#pragma unroll
+        for (int m = 0; m < NR; ++m) {
+          const Tab t = lt[m * K + s];
+#pragma unroll
+          for (int q = 0; q < NW; ++q) {
+            acc[m][q] ^= gmul(s0[q], s1[q], s2[q], t);
+            // pin the accumulation order: reassociating the K-term XOR chains into trees
+            // keeps every survivor's products live at once (spills)
+            __asm__ volatile("" : "+v"(acc[m][q]));
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < NR; ++m) store(og + erased(m0 + m) * static_cast<uint64_t>(P), acc[m]);
+    };
+    for_row_count<MAXE>(e - m0 < MAXE ? e - m0 : MAXE, rebuild);
+    return;
+  } else {
+#pragma unroll
+    for (int s = kWin; s < K; ++s) load(shard(sid[s]), x[s]);
+  }
   uint32_t acc[MAXE][NW];
 #pragma unroll
   for (int m = 0; m < MAXE; ++m)
@@ -557,7 +708,7 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
 #pragma unroll
     for (int m = 0; m < MAXE; ++m) {
       if (m0 + m < e) {
-        const Tab& t = tabs[(m0 + m) * K + s];
+        const Tab& t = rt[m * K + s];
         if (((POL & kProbeXorOnly) != 0) || t.coef == 1u) {
 #pragma unroll
           for (int q = 0; q < NW; ++q) acc[m][q] ^= x[s][q];
@@ -1021,10 +1172,16 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
   return hipSuccess;
 }
 
-template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false>
+template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false, bool INLINE = DIRECT>
 hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
   const uint32_t passes = (a.r + MAXE - 1) / MAXE;
   const uint32_t smem = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_DECODE_WAVES", kDecodeWavesPerCU), 4);
+  RankMeta rm{};
+  for (int e = 1; e <= 3; ++e) {
+    rm.base[e] = a.meta.base[e];
+    rm.stride[e] = a.meta.stride[e];
+    rm.count_r[e] = a.meta.count_r[e];
+  }
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t m0 = p * MAXE;
     const uint64_t blocks = (a.groups + 3) / 4;
@@ -1032,11 +1189,12 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
       const uint64_t bn = (blocks - b0 < (1u << 24)) ? blocks - b0 : (1u << 24);
       const uint64_t g0 = b0 * 4;
       const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
-      hipLaunchKernelGGL((decode_fused<K, MAXE, POL, NM, NT, DIRECT>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
+      hipLaunchKernelGGL((decode_fused<K, MAXE, POL, NM, NT, DIRECT, INLINE>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                          a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
                          a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u,
-                         decode_swizzle(a, kDecodeFusedXcdSwizzle), DIRECT ? a.masks + g0 : nullptr);
+                         decode_swizzle(a, kDecodeFusedXcdSwizzle), DIRECT ? a.masks + g0 : nullptr, rm,
+                         INLINE && a.status ? a.status + g0 : nullptr);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
@@ -1052,7 +1210,10 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
 // the looped wave kernel, 768 B 5.49 vs 3.24 (profiles/r01_probe_decode_small.txt).  The
 // mask-addressed forms also load non-temporally (survivors are read once): +1.2..3.2% at
 // 512 / 768 / 1200 / 1400 B in one process (profiles/r01_probe_decode_ntload.txt); loads
-// alone without NT stores lose 14%.
+// alone without NT stores lose 14%.  The r > 3 record-addressed forms stage their tables
+// through LDS (kLdsTabs): k=20 r=5, 5 erasures, 1200 B: 2.27 -> 4.44 TB/s
+// (profiles/r01_probe_decode_ldstabs_k20.txt); at k=10 r=3, whose 286 records stay in the
+// scalar cache, it gains nothing (profiles/r01_probe_decode_inline_k10.txt).
 hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct) {
   const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
 #define QFEC_FUSED_D(KK, RR, NMM, NTT)                                                        \
@@ -1061,15 +1222,19 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct) {
 #define QFEC_FUSED_R(KK, RR, NMM, NTT)                                                        \
   if (!direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                            \
     return run_decode_fused<KK, RR, kNtStore, NMM, NTT, false>(a, s);
+#define QFEC_FUSED_L(KK, RR, NMM, NTT)                                                        \
+  if (!direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                            \
+    return run_decode_fused<KK, RR, kNtStore | kLdsTabs, NMM, NTT, false>(a, s);
 #define QFEC_FUSED_P(M, KK, RR)                                                               \
   M(KK, RR, 0, 2) M(KK, RR, 0, 3) M(KK, RR, 0, 4) M(KK, RR, 1, 0) M(KK, RR, 1, 1)            \
   M(KK, RR, 1, 2) M(KK, RR, 1, 3) M(KK, RR, 1, 4)
   QFEC_FUSED_P(QFEC_FUSED_D, 10, 3)
   QFEC_FUSED_R(10, 3, 1, 1)
-  QFEC_FUSED_P(QFEC_FUSED_R, 20, 5)
+  QFEC_FUSED_P(QFEC_FUSED_L, 20, 5)
   QFEC_FUSED_P(QFEC_FUSED_D, 10, 1)
   QFEC_FUSED_P(QFEC_FUSED_D, 4, 2)
 #undef QFEC_FUSED_P
+#undef QFEC_FUSED_L
 #undef QFEC_FUSED_R
 #undef QFEC_FUSED_D
   return hipErrorNotSupported;
@@ -1101,6 +1266,17 @@ hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s)
 
 hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
   if (a.groups == 0) return hipSuccess;
+  const uint32_t tile = a.P >= kVecMinP ? pick_tile((a.P + 15u) / 16u, a.k, a.P) : 0u;
+  const bool tiled = tile > 0 && ((a.variant == kDecodeAuto && a.P <= kTiledMaxP) ||
+                                  a.variant == kDecodeTiledPlain || a.variant == kDecodeTiledNt);
+  // Mask-addressed fused form (r <= 3): +1.2% at k=10 r=3 (tools/probe_decode.hip,
+  // r01_probe_decode_direct.txt); at k=20 r=5 its extra VGPRs cost a wave per SIMD (-30%), so
+  // auto takes it for r <= 3 only.  It classifies inline: one launch, no classify kernel.
+  if (a.P >= kVecMinP && !tiled && a.masks != nullptr && !a.rec_ready &&
+      (a.variant == kDecodeFusedDirect || (a.variant == kDecodeAuto && a.r <= 3))) {
+    const hipError_t e = try_decode_fused(a, s, true);
+    if (e != hipErrorNotSupported) return e;
+  }
   for (uint64_t g0 = 0; !a.rec_ready && g0 < a.groups; g0 += kMaxThreadsPerLaunch) {
     const uint64_t gn = (a.groups - g0 < kMaxThreadsPerLaunch) ? a.groups - g0 : kMaxThreadsPerLaunch;
     hipLaunchKernelGGL(classify, dim3(blocks_for(gn)), dim3(256), 0, s, a.masks + g0, gn, a.k, a.r,
@@ -1120,10 +1296,8 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     }
     return hipSuccess;
   }
-  const uint32_t tile = pick_tile((a.P + 15u) / 16u, a.k, a.P);
   const bool separate_out = a.out != nullptr && a.out != a.data;  // decode_v16 lacks it
-  const bool tiled_auto = a.variant == kDecodeAuto && a.P <= kTiledMaxP;
-  if (tile > 0 && (tiled_auto || a.variant == kDecodeTiledPlain || a.variant == kDecodeTiledNt)) {
+  if (tiled) {
     const bool nt = a.variant != kDecodeTiledPlain;
 #define QFEC_TILED(KK, RR)                                                                   \
   if (a.k == KK && a.r == RR)                                                                \
@@ -1137,12 +1311,9 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
   // Fused passes win where many rows share each survivor (k=20 r=5, 5 losses: +21%); with
   // the XCD-aware order they also win at r = 3 (+2.6%; tools/probe_decode.hip), so auto
   // takes them wherever they are instantiated.
+  // (the mask-addressed forms were tried above, before classify)
   if (a.variant == kDecodeFused || a.variant == kDecodeAuto || a.variant == kDecodeFusedDirect) {
-    // Mask-addressed survivors: +1.2% at k=10 r=3 (tools/probe_decode.hip, r01_probe_decode_direct.txt);
-    // at k=20 r=5 its extra VGPRs cost a wave per SIMD (-30%), so auto takes it for r <= 3 only.
-    const bool direct = (a.variant == kDecodeFusedDirect || (a.variant == kDecodeAuto && a.r <= 3)) &&
-                        a.masks != nullptr && !a.rec_ready;
-    const hipError_t e = try_decode_fused(a, s, direct);
+    const hipError_t e = try_decode_fused(a, s, false);
     if (e != hipErrorNotSupported) return e;
   }
   if (a.variant == kDecodeWaveNoBranch && !separate_out) {

@@ -182,6 +182,13 @@ int main(int argc, char** argv) {
   if (k == 10 && r == 3 && P == 1200) {
     PVD("pol direct nt-store", -1, kNtStore, 1, 1)
     PVD("pol direct nt-load+store", -1, kNtStore | kNtLoad, 1, 1)
+    vars.push_back({"pol direct classify-launch", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {
+                      probe(a);  // the previous form: classify kernel, then rec_off
+                      return run_decode_fused<10, 3, kNtStore | kNtLoad, 1, 1, true, false>(a, nullptr);
+                    }});
+    vars.push_back({"pol direct inline-only", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
+                      return run_decode_fused<10, 3, kNtStore | kNtLoad, 1, 1, true, true>(a, nullptr);
+                    }});
     PVD("pol direct nt-load", -1, kNtLoad, 1, 1)
     PVD("pol direct plain", -1, 0, 1, 1)
     PVD("pol direct nt-load+store cap12", 12, kNtStore | kNtLoad, 1, 1)
@@ -203,6 +210,24 @@ int main(int argc, char** argv) {
   } else if (k == 10 && r == 3 && P == 2048) {
     PSET(2, 0)
   }
+  // record-addressed fused form with the coefficient tables staged through LDS (kLdsTabs)
+#define PLDS(KK, RR, NMM, NTT)                                                                    \
+  if (k == KK && r == RR && P / 1024 == NMM && (P % 1024 + 255) / 256 == NTT) {                   \
+    vars.push_back({"lds-tabs", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {         \
+                      probe(a);                                                                   \
+                      return run_decode_fused<KK, RR, kNtStore | kLdsTabs, NMM, NTT, false>(a, nullptr); \
+                    }});                                                                          \
+    vars.push_back({"lds-tabs nt-load", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) { \
+                      probe(a);                                                                   \
+                      return run_decode_fused<KK, RR, kNtStore | kNtLoad | kLdsTabs, NMM, NTT, false>(a, nullptr); \
+                    }});                                                                          \
+    vars.push_back({"lds-tabs xcd0", kDecodeFused, -1, 0, {}, [probe](const DecodeLaunch& a) {    \
+                      probe(a);                                                                   \
+                      return run_decode_fused<KK, RR, kNtStore | kLdsTabs, NMM, NTT, false>(a, nullptr); \
+                    }});                                                                          \
+  }
+  PLDS(20, 5, 1, 1)
+  PLDS(10, 3, 1, 1)
   if (std::getenv("PROBE_FILTER")) {  // keep variants whose name contains one of '|'-separated words
     const std::string f = std::getenv("PROBE_FILTER");
     std::vector<Var> keep;
@@ -219,12 +244,12 @@ int main(int argc, char** argv) {
     vars.swap(keep);
   }
   for (auto& v : vars) {
-    if (v.fn) continue;
+    // custom launches are checked too (probe-only forms that skip stores or math mismatch by design)
     dl.variant = v.variant;
     dl.waves_per_cu = v.waves;
     dl.xcd_swizzle = v.swz;
     poison<<<uint32_t((nd + 255) / 256), 256>>>(data, masks, G, k, P);
-    CK(launch_decode(dl, nullptr));
+    CK(v.fn ? v.fn(dl) : launch_decode(dl, nullptr));
     CK(hipDeviceSynchronize());
     std::vector<uint8_t> a(nd), b(nd);
     CK(hipMemcpy(a.data(), data, nd, hipMemcpyDeviceToHost));

@@ -31,7 +31,7 @@ def collect(d: Path, counter: str):
 
 
 def short(name: str) -> str:
-    for key in ("encode_v16", "decode_wave", "decode_v16", "classify", "fill_words", "encode_bytes", "decode_bytes"):
+    for key in ("encode_v16", "decode_fused", "decode_wave", "decode_v16", "decode_tiled", "classify", "fill_words", "encode_bytes", "decode_bytes"):
         if key in name:
             return key
     return name[:40]
@@ -56,7 +56,7 @@ def main():
             entry["hbm_read_bytes_per_launch"] = int(fk * 1024 * 2)
             entry["hbm_write_bytes_per_launch"] = int(wk * 1024)
             entry["hbm_bytes_per_launch"] = entry["hbm_read_bytes_per_launch"] + entry["hbm_write_bytes_per_launch"]
-        key = {"encode_v16": "encode", "decode_wave": "decode", "decode_v16": "decode"}.get(s, s)
+        key = {"encode_v16": "encode", "decode_fused": "decode", "decode_tiled": "decode", "decode_wave": "decode", "decode_v16": "decode"}.get(s, s)
         res[key] = entry
     out.write_text(json.dumps(res, indent=1))
     print(json.dumps(res, indent=1))

@@ -66,6 +66,14 @@ int main() {
       if (gmul(w, e) != uint32_t(qfec::gf().mul(uint8_t(c), uint8_t(x))) * 0x01010101u) return fail("gmul", c, x, 0);
     }
   }
+  // decode_fused<..., INLINE>: choose_small (fec_kernels.hip, the inline classify's C(n, t)
+  // for t <= 3, same unsigned wrap-around for n < t) against the binomial table classify reads
+  for (uint32_t n = 0; n < 64; ++n)
+    for (uint32_t t = 1; t <= 3; ++t) {
+      const uint64_t a = n, b = n - 1u, c = n - 2u;
+      const uint64_t v = t == 1u ? a : t == 2u ? (a * b) >> 1 : (a * b * c) / 6u;
+      if (v != qfec::binom().c[n][t]) return fail("choose_small", int(n), int(t), 0);
+    }
   const uint32_t shapes[][3] = {{4, 2, 256}, {10, 3, 1200}, {10, 1, 64}, {20, 5, 96}, {7, 4, 32}, {3, 8, 16}, {1, 1, 8}, {16, 16, 16}, {32, 8, 8}};
   for (const auto& sh : shapes) {
     const uint32_t k = sh[0], r = sh[1], P = sh[2];

@@ -420,7 +420,10 @@ def test_full_size_c4_shard_encode(gpu_ctx, oracle_mod, torch_cuda):
 ANY_P = [(10, 3, 1201), (10, 3, 1350), (10, 3, 1400), (10, 3, 1452), (10, 3, 1500), (10, 3, 1023),
          (10, 3, 1025), (10, 3, 2047), (10, 3, 3001), (10, 3, 17), (10, 3, 31), (20, 5, 1399),
          (20, 5, 1235), (10, 1, 1350), (4, 2, 250), (4, 2, 301), (7, 4, 1399), (12, 9, 70),
-         (3, 1, 18), (16, 16, 45)]
+         (3, 1, 18), (16, 16, 45),
+         # k=20 r=5 fused forms with LDS-staged tables: every (NM, NT) piece layout
+         (20, 5, 300), (20, 5, 700), (20, 5, 1000), (20, 5, 1024), (20, 5, 1500), (20, 5, 1600),
+         (20, 5, 1800)]
 
 
 @pytest.mark.parametrize("k,r,P", ANY_P)
