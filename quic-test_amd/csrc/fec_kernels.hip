@@ -740,8 +740,10 @@ __global__ __launch_bounds__(256) void decode_wave(uint8_t* __restrict__ data,
                                                    const uint8_t* __restrict__ codebook,
                                                    uint64_t groups, uint32_t P, uint32_t k_rt, uint32_t r,
                                                    uint32_t m0, uint8_t* __restrict__ out, uint32_t never,
-                                                   uint32_t swz) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];  // see encode_v16
+                                                   uint32_t swz, uint32_t lds_slice) {
+  // Dynamic LDS: an occupancy cap, or (kLdsTabs) 4 per-wave slices of `lds_slice` bytes
+  // holding the wave's coefficient rows (see kLdsTabs and decode_fused).
+  extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];
   if (never) occupancy_lds[threadIdx.x] = 0;
   const uint64_t gw = static_cast<uint64_t>(swz ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * 4u +
                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
@@ -756,6 +758,27 @@ __global__ __launch_bounds__(256) void decode_wave(uint8_t* __restrict__ data,
   const bool xor_only = ((rw[24] >> 8) & 0xFFu) != 0;
   if (m0 >= e) return;
   const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
+  if constexpr ((POL & kLdsTabs) != 0) {
+    if (!xor_only) {
+      // rows [m0, m0 + min(e - m0, MAXE)) of the record into this wave's slice, by
+      // direct-to-LDS loads (LDS address = wave base + lane * 16); every pass over the
+      // packet then reads them from LDS instead of re-reading them through the scalar cache
+      const uint32_t pieces = (e - m0 < MAXE ? e - m0 : MAXE) * k * 2u;
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(tabs + m0 * k);
+      uint8_t* slice = occupancy_lds + (threadIdx.x >> 6) * lds_slice;
+      for (uint32_t i = 0; i * 64u < pieces; ++i) {
+        uint32_t idx = lane + 64u * i;
+        if (idx >= pieces) idx = pieces - 1u;  // slots past the rows: unused, inside the slice
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + idx * 16u),
+                                         (__attribute__((address_space(3))) void*)(slice + i * 1024u), 16, 0, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // decode_piece indexes rows from m0
+      tabs = reinterpret_cast<const Tab*>(slice) - static_cast<ptrdiff_t>(m0) * k;
+    }
+  }
   const uint8_t* dg = data + gw * k * static_cast<uint64_t>(P);
   const uint8_t* pg = parity + gw * r * static_cast<uint64_t>(P);
   uint8_t* og = out + gw * k * static_cast<uint64_t>(P);
@@ -1152,9 +1175,13 @@ hipError_t run_decode_v16(const DecodeLaunch& a, hipStream_t s) {
 template <int K, int MAXE, int POL>
 hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
   const uint32_t passes = (a.r + MAXE - 1) / MAXE;  // e <= r
-  const uint32_t smem = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_DECODE_WAVES", kDecodeWavesPerCU), 4);
+  const uint32_t cap = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_DECODE_WAVES", kDecodeWavesPerCU), 4);
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t m0 = p * MAXE;
+    // kLdsTabs: per-wave slice of whole 1 KiB wave-loads covering this pass's rows
+    const uint32_t rows = a.r - m0 < MAXE ? a.r - m0 : MAXE;
+    const uint32_t slice = (POL & kLdsTabs) != 0 ? (rows * a.k * 2u + 63u) / 64u * 1024u : 0u;
+    const uint32_t smem = cap > 4 * slice ? cap : 4 * slice;
     const uint64_t blocks = (a.groups + 3) / 4;
     for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 24)) {
       const uint64_t bn = (blocks - b0 < (1u << 24)) ? blocks - b0 : (1u << 24);
@@ -1164,7 +1191,7 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                          a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
                          a.k, a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u,
-                         decode_swizzle(a, kDecodeWaveXcdSwizzle));
+                         decode_swizzle(a, kDecodeWaveXcdSwizzle), slice);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
@@ -1333,7 +1360,12 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     QFEC_WAVE(20, 5)
     QFEC_WAVE(4, 2)
 #undef QFEC_WAVE
-    return nt ? run_decode_wave<0, 8, kNtStore>(a, s) : run_decode_wave<0, 8, 0>(a, s);
+    // Runtime k: multiplying by every coefficient (no branches on 0 / 1) wins at every shape
+    // measured (tools/probe_decode.hip, profiles/r01_probe_decode_runtime_k.txt): k=10 r=2
+    // 4.13 -> 4.79 TB/s, 12+6 2.62 -> 3.20, 16+4 2.67 -> 3.40.  Its tables staged through
+    // LDS (kLdsTabs) lose here (2.2-2.8 TB/s): the records of these codebooks are hit often
+    // enough in the scalar cache, and the wait for the tables precedes the survivor loads.
+    return nt ? run_decode_wave<0, 8, kNtStore | kNoCoefBranch>(a, s) : run_decode_wave<0, 8, 0>(a, s);
   }
   if (a.k == 10 && a.r == 3) return run_decode_v16<10, 3>(a, s);
   if (a.k == 10 && a.r == 1) return run_decode_v16<10, 1>(a, s);

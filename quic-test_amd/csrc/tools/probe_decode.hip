@@ -228,6 +228,19 @@ int main(int argc, char** argv) {
   }
   PLDS(20, 5, 1, 1)
   PLDS(10, 3, 1, 1)
+  // runtime-k wave kernel (any k, r): tables through the scalar cache vs through LDS
+  vars.push_back({"wave0 scalar", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {
+                    probe(a);
+                    return run_decode_wave<0, 8, kNtStore>(a, nullptr);
+                  }});
+  vars.push_back({"wave0 nobranch", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {
+                    probe(a);
+                    return run_decode_wave<0, 8, kNtStore | kNoCoefBranch>(a, nullptr);
+                  }});
+  vars.push_back({"wave0 lds", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {
+                    probe(a);
+                    return run_decode_wave<0, 8, kNtStore | kNoCoefBranch | kLdsTabs>(a, nullptr);
+                  }});
   if (std::getenv("PROBE_FILTER")) {  // keep variants whose name contains one of '|'-separated words
     const std::string f = std::getenv("PROBE_FILTER");
     std::vector<Var> keep;
