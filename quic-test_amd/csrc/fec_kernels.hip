@@ -56,6 +56,8 @@ constexpr int kProbeDense = 32;   // probes only: decode_fused reads data shards
 // this bit the wave fetches its rows with vector loads issued next to its survivor loads
 // (one round trip) and reads them from a per-wave LDS slice.
 constexpr int kLdsTabs = 64;
+constexpr int kProbeWin10 = 128;  // probes only: kLdsTabs survivor window of 10 (default 6)
+constexpr int kProbeWin14 = 256;  // probes only: window of 14
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
@@ -631,9 +633,12 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
     }
   }
   // kLds: survivors stream through a window of kWin loads in flight (survivor s + kWin is
-  // loaded as survivor s is consumed), so K = 20 needs ~half the data VGPRs and the wave
-  // keeps 4 waves per SIMD; the first window is in flight with the table loads.
-  constexpr int kWin = kLds ? (K < 10 ? K : 10) : K;
+  // loaded as survivor s is consumed), so K = 20 needs a third of the data VGPRs: 114 VGPRs,
+  // 4 waves per SIMD at 1200 B (window 10: 153, 3 waves; 5-erasure decode 4.73 vs 4.28-4.50
+  // TB/s, profiles/r01_probe_decode_window.txt).  The first window is in flight with the
+  // table loads.
+  constexpr int kWinW = (POL & kProbeWin10) != 0 ? 10 : (POL & kProbeWin14) != 0 ? 14 : 6;
+  constexpr int kWin = kLds ? (K < kWinW ? K : kWinW) : K;
   uint32_t x[K][NW];
 #pragma unroll
   for (int s = 0; s < kWin; ++s) load(shard(sid[s]), x[s]);

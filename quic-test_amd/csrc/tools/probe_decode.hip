@@ -221,6 +221,14 @@ int main(int argc, char** argv) {
                       probe(a);                                                                   \
                       return run_decode_fused<KK, RR, kNtStore | kNtLoad | kLdsTabs, NMM, NTT, false>(a, nullptr); \
                     }});                                                                          \
+    vars.push_back({"lds-tabs win10", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {    \
+                      probe(a);                                                                   \
+                      return run_decode_fused<KK, RR, kNtStore | kLdsTabs | kProbeWin10, NMM, NTT, false>(a, nullptr); \
+                    }});                                                                          \
+    vars.push_back({"lds-tabs win14", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {   \
+                      probe(a);                                                                   \
+                      return run_decode_fused<KK, RR, kNtStore | kLdsTabs | kProbeWin14, NMM, NTT, false>(a, nullptr); \
+                    }});                                                                          \
     vars.push_back({"lds-tabs xcd0", kDecodeFused, -1, 0, {}, [probe](const DecodeLaunch& a) {    \
                       probe(a);                                                                   \
                       return run_decode_fused<KK, RR, kNtStore | kLdsTabs, NMM, NTT, false>(a, nullptr); \
