@@ -58,6 +58,7 @@ constexpr int kProbeDense = 32;   // probes only: decode_fused reads data shards
 constexpr int kLdsTabs = 64;
 constexpr int kProbeWin10 = 128;  // probes only: kLdsTabs survivor window of 10 (default 6)
 constexpr int kProbeWin14 = 256;  // probes only: window of 14
+constexpr int kProbeWindowed = 512;  // probes only: windowed body, tables from the record
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
@@ -637,19 +638,25 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
   // 4 waves per SIMD at 1200 B (window 10: 153, 3 waves; 5-erasure decode 4.73 vs 4.28-4.50
   // TB/s, profiles/r01_probe_decode_window.txt).  The first window is in flight with the
   // table loads.
+  // kProbeWindowed: the same windowed straight-line body with the tables read from the
+  // record (scalar loads) instead of LDS (probes).
+  constexpr bool kWinPath = kLds || (POL & kProbeWindowed) != 0;
   constexpr int kWinW = (POL & kProbeWin10) != 0 ? 10 : (POL & kProbeWin14) != 0 ? 14 : 6;
-  constexpr int kWin = kLds ? (K < kWinW ? K : kWinW) : K;
+  constexpr int kWin = kWinPath ? (K < kWinW ? K : kWinW) : K;
   uint32_t x[K][NW];
 #pragma unroll
   for (int s = 0; s < kWin; ++s) load(shard(sid[s]), x[s]);
   const Tab* rt = tabs + m0 * K;  // rows of this pass: entry (m, s) at rt[m * K + s]
-  if constexpr (kLds) {
-    // Wait for every load so far (vmcnt(0): the compiler may order the survivor loads
-    // around the LDS loads, so no counted wait), then keep LDS reads below the wait.
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const Tab* lt = wave_tabs_lds<kSliceTabs>();
+  if constexpr (kWinPath) {
+    const Tab* lt = rt;
+    if constexpr (kLds) {
+      // Wait for every load so far (vmcnt(0): the compiler may order the survivor loads
+      // around the LDS loads, so no counted wait), then keep LDS reads below the wait.
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      lt = wave_tabs_lds<kSliceTabs>();
+    }
     // Straight-line body per row count NR (no branch on the row index or the coefficient:
     // table values are VGPRs here, and the 0 / 1 entries are the zero / identity maps).
     auto rebuild = [&](auto nr_c) __attribute__((always_inline)) {
@@ -1243,7 +1250,7 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
 // mask-addressed forms also load non-temporally (survivors are read once): +1.2..3.2% at
 // 512 / 768 / 1200 / 1400 B in one process (profiles/r01_probe_decode_ntload.txt); loads
 // alone without NT stores lose 14%.  The r > 3 record-addressed forms stage their tables
-// through LDS (kLdsTabs): k=20 r=5, 5 erasures, 1200 B: 2.27 -> 4.44 TB/s
+// through LDS (kLdsTabs): k=20 r=5, 5 erasures, 1200 B: 2.27 -> 4.73-4.92 TB/s
 // (profiles/r01_probe_decode_ldstabs_k20.txt); at k=10 r=3, whose 286 records stay in the
 // scalar cache, it gains nothing (profiles/r01_probe_decode_inline_k10.txt).
 hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct) {

@@ -236,6 +236,24 @@ int main(int argc, char** argv) {
   }
   PLDS(20, 5, 1, 1)
   PLDS(10, 3, 1, 1)
+  // windowed straight-line body (6-deep survivor window) with tables from the record
+  if (k == 10 && r == 3 && P == 1200) {
+    vars.push_back({"winbody direct w6", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
+                      return run_decode_fused<10, 3, kNtStore | kNtLoad | kProbeWindowed, 1, 1, true>(a, nullptr);
+                    }});
+    vars.push_back({"winbody direct w10", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
+                      return run_decode_fused<10, 3, kNtStore | kNtLoad | kProbeWindowed | kProbeWin10, 1, 1, true>(a, nullptr);
+                    }});
+    vars.push_back({"winbody direct w6 lds", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
+                      return run_decode_fused<10, 3, kNtStore | kNtLoad | kLdsTabs, 1, 1, true>(a, nullptr);
+                    }});
+  }
+  if (k == 20 && r == 5 && P == 1200) {
+    vars.push_back({"winbody scalar-tabs", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {
+                      probe(a);
+                      return run_decode_fused<20, 5, kNtStore | kProbeWindowed, 1, 1, false>(a, nullptr);
+                    }});
+  }
   // runtime-k wave kernel (any k, r): tables through the scalar cache vs through LDS
   vars.push_back({"wave0 scalar", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {
                     probe(a);
