@@ -184,7 +184,8 @@ def test_rs_decode_matches_oracle(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
     assert np.array_equal(got, exp)
     # device-resident API
     dd, dpar, dm = _dev(torch_cuda, broken), _dev(torch_cuda, par), _dev(torch_cuda, masks.view(np.int64))
-    dst = torch_cuda.zeros(G, dtype=torch_cuda.uint8, device="cuda")
+    # 0xAA: every status byte must be written by the device (inline classify included)
+    dst = torch_cuda.full((G,), 0xAA, dtype=torch_cuda.uint8, device="cuda")
     gpu_ctx.decode_dev(dd, dpar, dm, G, k, r, P, dst)
     gpu_ctx.synchronize()
     assert np.array_equal(dd.cpu().numpy(), exp)
@@ -459,7 +460,7 @@ def test_any_packet_size_round_trip(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
         assert int(bp[:shift_p].sum().item()) == 0 and int(bp[shift_p + G * r * P:].sum().item()) == 0
         dd.copy_(torch.from_numpy(broken))
         dm = _dev(torch, masks.view(np.int64))
-        dst = torch.zeros(G, dtype=torch.uint8, device="cuda")
+        dst = torch.full((G,), 0xAA, dtype=torch.uint8, device="cuda")  # every byte written
         gpu_ctx.decode_dev(dd, dp, dm, G, k, r, P, dst)
         gpu_ctx.synchronize()
         assert np.array_equal(dd.cpu().numpy(), exp), (shift_d, shift_p)
