@@ -47,6 +47,109 @@ CONFIGS = {
 }
 
 
+# ----------------------------------------------------------------------------- launch
+def dist_backend() -> str:
+    """RCCL ("nccl") unless QUICFEC_DIST_BACKEND overrides it (gloo: multi-rank rehearsal
+    on a one-GPU box, where several ranks share the card)."""
+    return os.environ.get("QUICFEC_DIST_BACKEND", "nccl")
+
+
+def launch_plan(gpus: int, env) -> tuple[str, int]:
+    """How this process runs `--gpus N`:
+      ("run", W)   this process is one rank of W (WORLD_SIZE from torch.distributed.run, or
+                   W = 1 for a plain single-GPU run);
+      ("spawn", N) no WORLD_SIZE and N > 1: start N rank processes here (spawn_ranks).
+    A WORLD_SIZE that disagrees with --gpus is an error, never silently one of the two."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    w = env.get("WORLD_SIZE")
+    if w is not None and w != "":
+        world = int(w)
+        if world != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} disagrees with WORLD_SIZE={world} from the launcher")
+        return "run", world
+    return ("run", 1) if gpus == 1 else ("spawn", gpus)
+
+
+def visible_gpus() -> int:
+    """Visible GPU count without initialising the GPU in this process (on this image
+    torch.cuda.device_count() does not create a HIP context)."""
+    import torch
+    return int(torch.cuda.device_count())
+
+
+def bind_local_device(local: int, world: int, ndev: int) -> int:
+    """The device of local rank `local`: one process per GPU.  Ranks beyond the visible
+    devices are an error under RCCL; the gloo rehearsal shares the card (local % ndev)."""
+    if ndev <= 0:
+        raise SystemExit("bench.py: no GPU visible")
+    if local < ndev:
+        return local
+    if dist_backend() == "gloo":
+        return local % ndev
+    raise SystemExit(f"bench.py: local rank {local} of {world} needs GPU {local}, only {ndev} visible")
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str], check_devices: bool = True) -> int:
+    """`bench.py --gpus N` run directly (no torch.distributed.run): start N rank processes
+    of this script on 127.0.0.1, one per GPU, and return the worst exit code.  This parent
+    makes no GPU call (children bind their device before RCCL init); only rank 0 prints."""
+    import subprocess
+    if check_devices and dist_backend() != "gloo":
+        ndev = visible_gpus()
+        if n > ndev:
+            raise SystemExit(f"bench.py: --gpus {n} but only {ndev} GPU(s) visible")
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            code = p.wait()
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:          # a failed rank would leave the others in a collective
+                    if q.poll() is None:
+                        q.terminate()
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 1
+
+
+def launch_selftest(args) -> int:
+    """CPU-only check of the launch path (tests/test_distributed.py): every rank joins a
+    gloo group, reduces like the bench does, and rank 0 prints one JSON line."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="gloo", init_method="env://")
+    G = 1000
+    g0, g1 = shard_range(G * world, rank, world)
+    mx = reduce_max(0.25 * (rank + 1))
+    total = reduce_sum(float(g1 - g0))
+    barrier()
+    if rank == 0:
+        print(json.dumps({"selftest": True, "n_gpus": world, "gpus_arg": args.gpus, "max_elapsed": mx,
+                          "total_groups": total}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 # ----------------------------------------------------------------------------- helpers
 def shard_range(total_groups: int, rank: int, world: int) -> tuple[int, int]:
     """Contiguous [g0, g1) slice of the global group stream owned by `rank`."""
@@ -157,55 +260,107 @@ def decode_algorithmic_bytes(masks, k: int, r: int, P: int) -> int:
     return int(((k + e[ok]) * P).sum())
 
 
-def cpu_baseline(cfg: dict, seconds: float = 8.0) -> dict:
-    """The oracle restatement (oracle/, test infrastructure) timed on this host: the same
-    workload (encode + 2-erasure decode at k, r, P) on a bounded sample of groups."""
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup v2 quota (cpu.max), or None when unlimited/unknown."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def host_threads() -> int:
+    """Every core this process may run on: the sched_getaffinity set, bounded by the cgroup
+    CPU quota when one is set (more threads than the quota only time-slice)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    q = cgroup_cpu_quota()
+    return max(1, min(aff, q) if q else aff)
+
+
+def _rate(fn, nbytes: int, seconds: float) -> float:
+    """GiB/s of `nbytes` per call of fn(), repeated for about `seconds`."""
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return reps * nbytes / dt / 2**30
+
+
+def _threaded(n: int, G: int, body) -> None:
+    """body(g0, g1) over n Python threads on disjoint group ranges; the ctypes calls inside
+    release the GIL, so the threads run the C code in parallel."""
+    import threading
+    th = [threading.Thread(target=body, args=(G * t // n, G * (t + 1) // n)) for t in range(1, n)]
+    for t in th:
+        t.start()
+    body(0, G // n)
+    for t in th:
+        t.join()
+
+
+def cpu_baseline(cfg: dict, seconds: float = 10.0) -> dict:
+    """The same workload on this host's CPU cores, timed on a bounded sample (test
+    infrastructure, oracle/; never the product path).
+
+    value: the GF(2^8) restatement in its fast form (oracle_rs_encode_fast /
+    oracle_rs_decode_fast: GFNI affine multiply, 64 B per instruction with AVX-512,
+    recovery rows cached per erasure pattern -- how a tuned CPU library does it), byte-equal
+    to the table restatement (tests/test_oracle_golden.py), on every core of this process's
+    affinity.  The reference itself has no GF(2^8) code, so the reference
+    numbers beside it are its XOR row only: the reference library (oracle/_ref, compiled from
+    /root/reference's fec_xor_simd.cpp) fec_encode_batch single-threaded as written, and on
+    every core over disjoint group ranges, plus the AVX2 restatement."""
     import numpy as np
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle
     k, r, P = cfg["k"], cfg["r"], cfg["P"]
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
-    G = 20_000
+    threads = host_threads()
+    G = min(200_000, max(20_000, 1250 * threads))   # ~15 MB of data per thread: out of cache
     data = oracle.splitmix_bytes(G * k * P, SEED + 2)
     masks = make_masks(cfg, G, SEED + 3) if cfg["decode"] else None
-    done, t_total = 0, 0.0
-    while t_total < seconds and done < 2_000_000:
+    par = oracle.rs_encode_fast(data, G, k, r, P, nthreads=threads)
+    done, t_enc, t_dec = 0, 0.0, 0.0
+    while t_enc + t_dec < seconds:
         t0 = time.perf_counter()
-        par = oracle.rs_encode(data, G, k, r, P, nthreads=threads)
+        oracle.rs_encode_fast(data, G, k, r, P, nthreads=threads)
+        t1 = time.perf_counter()
         if cfg["decode"]:
-            oracle.rs_decode(data, par, masks, G, k, r, P, nthreads=threads)
-        t_total += time.perf_counter() - t0
+            oracle.rs_decode_fast(data, par, masks, G, k, r, P, nthreads=threads)
+        t_enc += t1 - t0
+        t_dec += time.perf_counter() - t1
         done += G
-    value = done * k * P / t_total / 2**30
-    # The reference's own computation (XOR row only, AVX2 restatement) on the same host.
-    reps = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < 2.0:
-        oracle.xor_encode_contig(data, G, k, P, nthreads=1)
-        reps += 1
-    xor1 = reps * G * k * P / (time.perf_counter() - t0) / 2**30
-    reps = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < 2.0:
-        oracle.xor_encode_contig(data, G, k, P, nthreads=threads)
-        reps += 1
-    xorn = reps * G * k * P / (time.perf_counter() - t0) / 2**30
-    # The reference library itself (oracle/_ref: /root/reference's fec_xor_simd.cpp compiled
-    # in this repo's build container), fec_encode_batch, single thread as it is written.
-    ref_gib_s = None
+    value = done * k * P / (t_enc + t_dec) / 2**30
+    leg = max(1.0, seconds / 5)
+    port_1 = _rate(lambda: oracle.rs_encode_fast(data[: 2000 * k * P], 2000, k, r, P, nthreads=1),
+                   2000 * k * P, leg)
+    xor1 = _rate(lambda: oracle.xor_encode_contig(data, G, k, P, nthreads=1), G * k * P, leg)
+    xorn = _rate(lambda: oracle.xor_encode_contig(data, G, k, P, nthreads=threads), G * k * P, leg)
+    ref_block = None
     ref = oracle.ref_lib()
     if ref is not None:
-        import numpy as np
-        offs = (np.arange(G * 10, dtype=np.uint32) * P).astype(np.uint32)
-        rep = np.zeros(G * P, dtype=np.uint8)
+        # fec_encode_batch takes 10 packets per group (fec_xor_simd.cpp:580): the slab read
+        # as G*k/10 groups of ten 1200-B packets, the same bytes
+        Gr = G * k // 10
+        offs = (np.arange(Gr * 10, dtype=np.uint64) * P).astype(np.uint32)
+        rep = np.zeros(Gr * P, dtype=np.uint8)
         h = ref.fec_encoder_new(0.10, 1024)
-        reps = 0
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < 2.0:
-            ref.fec_encode_batch(h, data.ctypes.data, offs.ctypes.data, G * k // 10, P, rep.ctypes.data)
-            reps += 1
-        ref_gib_s = round(reps * G * k * P / (time.perf_counter() - t0) / 2**30, 3)
+
+        def ref_range(g0, g1):
+            if g1 > g0:
+                ref.fec_encode_batch(h, data.ctypes.data, offs[g0 * 10:].ctypes.data, g1 - g0, P,
+                                     rep[g0 * P:].ctypes.data)
+
+        ref1 = _rate(lambda: ref_range(0, Gr), Gr * 10 * P, leg)
+        refn = _rate(lambda: _threaded(threads, Gr, ref_range), Gr * 10 * P, leg)
         ref.fec_encoder_free(h)
+        ref_block = {"threads_1": round(ref1, 3), f"threads_{threads}": round(refn, 3),
+                     "note": "oracle/_ref: /root/reference internal/fec/fec_xor_simd.cpp compiled by "
+                             "oracle/Makefile; fec_encode_batch (XOR parity row 0 only, the reference's "
+                             "whole computation), one call per thread over disjoint group ranges"}
     cpu_model = ""
     try:
         for ln in open("/proc/cpuinfo"):
@@ -214,16 +369,24 @@ def cpu_baseline(cfg: dict, seconds: float = 8.0) -> dict:
                 break
     except OSError:
         pass
+    isa = {2: "AVX-512+GFNI", 1: "AVX2+GFNI", 0: "scalar tables"}[oracle.fast_isa()]
     return {
         "value": round(value, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "sample": f"{done} groups ({G} per pass) of k={k} r={r} P={P}: oracle rs_encode"
-                  + (f" + rs_decode ({cfg['erasures']} erasures/group)" if cfg["decode"] else "")
-                  + f", {threads} threads, {t_total:.1f} s",
-        "cpu_model": cpu_model,
+        "sample": f"{done} groups ({G} per pass) of k={k} r={r} P={P}: GF(2^8) restatement, fast form "
+                  f"({isa}) rs_encode_fast"
+                  + (f" + rs_decode_fast ({'iid loss p=%g' % cfg['loss'] if cfg.get('loss') else '%d erasures/group' % cfg['erasures']})"
+                     if cfg["decode"] else "")
+                  + f", {threads} threads, {t_enc + t_dec:.1f} s",
+        "encode_GiBps": round(done * k * P / t_enc / 2**30, 3),
+        "decode_GiBps": round(done * k * P / t_dec / 2**30, 3) if cfg["decode"] else None,
+        "port_encode_threads_1_GiBps": round(port_1, 3),
+        "cpu_model": cpu_model, "nproc": os.cpu_count(),
+        "affinity_cores": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+        "cgroup_cpu_quota": cgroup_cpu_quota(),
+        "reference_fec_encode_batch_gib_s": ref_block,
         "xor_avx2_row0_gib_s": {"threads_1": round(xor1, 3), f"threads_{threads}": round(xorn, 3),
-                                "note": "reference computation only (XOR parity row 0, AVX2 restatement "
-                                        "bit-identical to fec_xor_simd.cpp:74-204)"},
-        "reference_fec_encode_batch_gib_s": ref_gib_s,
+                                "note": "AVX2 restatement of xor_packets_avx2 (fec_xor_simd.cpp:74-204), "
+                                        "bit-identical to it (tests/test_oracle_golden.py)"},
     }
 
 
@@ -300,7 +463,14 @@ def main() -> int:
                     help="k,r,P override of the config's code shape (tuning sweeps; not the headline)")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-resident path (pinned buffers, H2D -> kernel -> D2H)")
+    ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    mode, n = launch_plan(args.gpus, os.environ)
+    if mode == "spawn":
+        return spawn_ranks(n, sys.argv[1:])
+    if args.launch_selftest:
+        return launch_selftest(args)
 
     import numpy as np
     import torch
@@ -310,12 +480,11 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; bind the GPU before RCCL creates its communicator.  The modulo
-    # and the gloo override only exist to rehearse several ranks on a one-GPU box.
-    local = local % max(1, torch.cuda.device_count())
+    # one process per GPU; bind the GPU before RCCL creates its communicator.
+    local = bind_local_device(local, world, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group(backend=os.environ.get("QUICFEC_DIST_BACKEND", "nccl"), init_method="env://")
+        dist.init_process_group(backend=dist_backend(), init_method="env://")
     cfg = dict(CONFIGS[args.config])
     if args.loss is not None:
         cfg["loss"] = args.loss

@@ -44,8 +44,17 @@ extern "C" {
 /* Number of visible HIP devices (0 when none or the runtime is unusable). */
 int fec_hip_device_count(void);
 
-/* Last error message of the calling thread ("" if none). */
+/* Message of the calling thread's last failing call ("" if none; entry points taking a
+ * context clear it on entry). */
 const char* fec_hip_last_error(void);
+
+/* Message of the last failing call on `ctx`, whichever thread made it (Go: a goroutine may
+ * move to another OS thread between the failing call and the read, so the thread-local
+ * text above may be empty or another call's).  Copies at most buflen-1 bytes plus a NUL
+ * into buf (when buf != NULL and buflen > 0) and returns the message's full length; 0 for
+ * a NULL context or no failure yet.  Replaces the cgo wrapper's code-only message
+ * (fec_cgo.go:147-149). */
+size_t fec_ctx_last_error(FECEncoderCtx* ctx, char* buf, size_t buflen);
 
 /* fec_encoder_new on an explicit device ordinal (shards of a multi-GPU job). */
 FECEncoderCtx* fec_encoder_new_device(double redundancy, uint32_t max_groups, int device);

@@ -38,8 +38,11 @@ FECEncoderCtx* fec_encoder_new(double redundancy, uint32_t max_groups);
  * Here: page-locked (pinned) host memory, so H2D/D2H copies run at DMA rate. */
 void* fec_alloc_slab(size_t size);
 
-/* Reference fec_xor_simd.h:37 / .cpp:486-510.  Pinned host memory; numa_node is
- * advisory (pinned pages are placed by the HIP runtime). */
+/* Reference fec_xor_simd.h:37 / .cpp:486-510.  numa_node >= 0: page-aligned anonymous
+ * memory bound to that node with mbind(MPOL_BIND, MPOL_MF_MOVE) -- best effort, as in the
+ * reference -- then page-locked with hipHostRegister (so the pages fault in on the node);
+ * without a usable GPU it stays pageable, which is what the reference returns.
+ * numa_node < 0: fec_alloc_slab.  Free with fec_free_slab. */
 void* fec_alloc_slab_numa(size_t size, int numa_node);
 
 /* Reference fec_xor_simd.h:44 / .cpp:512-514: same allocator as fec_alloc_slab. */

@@ -301,6 +301,262 @@ int64_t oracle_rs_decode(uint8_t* data, const uint8_t* parity, const uint64_t* e
 }
 
 /* ------------------------------------------------------------------------- */
+/* Fast CPU comparator (bench.py cpu_baseline): GFNI affine multiply           */
+/* ------------------------------------------------------------------------- */
+/* x -> c*x is linear over GF(2): output bit i = parity(row_i & x) with row_i bit j =
+ * bit i of c*2^j.  VGF2P8AFFINEQB takes row_i from byte 7-i of the 64-bit matrix. */
+uint64_t oracle_gf_affine(uint8_t c) {
+    gf_init();
+    uint64_t A = 0;
+    for (int i = 0; i < 8; ++i) {
+        unsigned row = 0;
+        for (int j = 0; j < 8; ++j) row |= ((unsigned)(gf_mul_tab[c][1u << j] >> i) & 1u) << j;
+        A |= (uint64_t)row << (8 * (7 - i));
+    }
+    return A;
+}
+
+#include <cpuid.h>
+int oracle_fast_isa(void) {
+    unsigned a, b, c, d;
+    if (!__get_cpuid_count(7, 0, &a, &b, &c, &d)) return 0;
+    const int gfni = (c >> 8) & 1, avx2 = (b >> 5) & 1, avx512bw = (b >> 30) & 1, avx512f = (b >> 16) & 1;
+    if (!gfni || !avx2) return 0;
+    return (avx512f && avx512bw) ? 2 : 1;
+}
+
+#define FAST_MAXK 32u
+#define FAST_MAXE 8u
+#define FAST_TAB  512u   /* per-thread recovery-row cache entries (direct mapped) */
+
+/* Rows for the 64-byte (AVX-512) or 32-byte (AVX2) column step of one group.
+ * n_out rows; row o = sum over s < n_in of coef[o][s] * in_s.  coef 1 = plain XOR. */
+typedef struct {
+    uint32_t n_in, n_out;
+    const uint8_t* in[FAST_MAXK > 64 ? FAST_MAXK : 64];
+    uint8_t* out[FAST_MAXE];
+    const uint64_t* A;     /* n_out x n_in affine matrices, row-major */
+    const uint8_t* coef;   /* n_out x n_in coefficients */
+} fast_job;
+
+__attribute__((target("avx512f,avx512bw,gfni"), always_inline))
+static inline void fast_rows512(const fast_job* jb, uint32_t P, const uint32_t NO) {
+    for (uint32_t c = 0; c < P; c += 64) {
+        const uint32_t n = P - c < 64 ? P - c : 64;
+        const __mmask64 m = n == 64 ? ~0ULL : ((1ULL << n) - 1);
+        __m512i acc[FAST_MAXE];
+        for (uint32_t o = 0; o < NO; ++o) acc[o] = _mm512_setzero_si512();
+        for (uint32_t s = 0; s < jb->n_in; ++s) {
+            const __m512i x = _mm512_maskz_loadu_epi8(m, jb->in[s] + c);
+            for (uint32_t o = 0; o < NO; ++o) {
+                const uint32_t t = o * jb->n_in + s;
+                if (jb->coef[t] == 1) acc[o] = _mm512_xor_si512(acc[o], x);
+                else if (jb->coef[t] != 0)
+                    acc[o] = _mm512_xor_si512(acc[o], _mm512_gf2p8affine_epi64_epi8(x, _mm512_set1_epi64((long long)jb->A[t]), 0));
+            }
+        }
+        for (uint32_t o = 0; o < NO; ++o) _mm512_mask_storeu_epi8(jb->out[o] + c, m, acc[o]);
+    }
+}
+
+__attribute__((target("avx512f,avx512bw,gfni")))
+static void fast_run512(const fast_job* jb, uint32_t P) {
+    switch (jb->n_out) {
+        case 1: fast_rows512(jb, P, 1); break;
+        case 2: fast_rows512(jb, P, 2); break;
+        case 3: fast_rows512(jb, P, 3); break;
+        case 4: fast_rows512(jb, P, 4); break;
+        case 5: fast_rows512(jb, P, 5); break;
+        case 6: fast_rows512(jb, P, 6); break;
+        case 7: fast_rows512(jb, P, 7); break;
+        default: fast_rows512(jb, P, 8); break;
+    }
+}
+
+__attribute__((target("avx2,gfni"), always_inline))
+static inline void fast_rows256(const fast_job* jb, uint32_t P, const uint32_t NO) {
+    uint8_t tail[FAST_MAXE][32];
+    for (uint32_t c = 0; c < P; c += 32) {
+        const uint32_t n = P - c < 32 ? P - c : 32;
+        __m256i acc[FAST_MAXE];
+        for (uint32_t o = 0; o < NO; ++o) acc[o] = _mm256_setzero_si256();
+        for (uint32_t s = 0; s < jb->n_in; ++s) {
+            __m256i x;
+            if (n == 32) {
+                x = _mm256_loadu_si256((const __m256i*)(jb->in[s] + c));
+            } else {
+                uint8_t b[32] = {0};
+                memcpy(b, jb->in[s] + c, n);
+                x = _mm256_loadu_si256((const __m256i*)b);
+            }
+            for (uint32_t o = 0; o < NO; ++o) {
+                const uint32_t t = o * jb->n_in + s;
+                if (jb->coef[t] == 1) acc[o] = _mm256_xor_si256(acc[o], x);
+                else if (jb->coef[t] != 0)
+                    acc[o] = _mm256_xor_si256(acc[o], _mm256_gf2p8affine_epi64_epi8(x, _mm256_set1_epi64x((long long)jb->A[t]), 0));
+            }
+        }
+        for (uint32_t o = 0; o < NO; ++o) {
+            if (n == 32) {
+                _mm256_storeu_si256((__m256i*)(jb->out[o] + c), acc[o]);
+            } else {
+                _mm256_storeu_si256((__m256i*)tail[o], acc[o]);
+                memcpy(jb->out[o] + c, tail[o], n);
+            }
+        }
+    }
+}
+
+__attribute__((target("avx2,gfni")))
+static void fast_run256(const fast_job* jb, uint32_t P) {
+    switch (jb->n_out) {
+        case 1: fast_rows256(jb, P, 1); break;
+        case 2: fast_rows256(jb, P, 2); break;
+        case 3: fast_rows256(jb, P, 3); break;
+        case 4: fast_rows256(jb, P, 4); break;
+        case 5: fast_rows256(jb, P, 5); break;
+        case 6: fast_rows256(jb, P, 6); break;
+        case 7: fast_rows256(jb, P, 7); break;
+        default: fast_rows256(jb, P, 8); break;
+    }
+}
+
+static void fast_run(int isa, const fast_job* jb, uint32_t P) {
+    if (isa == 2) fast_run512(jb, P);
+    else fast_run256(jb, P);
+}
+
+typedef struct {
+    const uint8_t* data; uint32_t k, r, P; int isa;
+    const uint64_t* A; const uint8_t* coef; uint8_t* parity;
+} fenc_arg;
+
+static void fenc_range(void* p, uint64_t g0, uint64_t g1) {
+    fenc_arg* a = (fenc_arg*)p;
+    const uint32_t k = a->k, r = a->r, P = a->P;
+    fast_job jb;
+    jb.n_in = k;
+    for (uint64_t g = g0; g < g1; ++g) {
+        for (uint32_t j = 0; j < k; ++j) jb.in[j] = a->data + (g * k + j) * (uint64_t)P;
+        for (uint32_t i0 = 0; i0 < r; i0 += FAST_MAXE) {   /* passes of up to 8 parity rows */
+            jb.n_out = r - i0 < FAST_MAXE ? r - i0 : FAST_MAXE;
+            for (uint32_t o = 0; o < jb.n_out; ++o) jb.out[o] = a->parity + (g * r + i0 + o) * (uint64_t)P;
+            jb.A = a->A + (uint64_t)i0 * k;
+            jb.coef = a->coef + (uint64_t)i0 * k;
+            fast_run(a->isa, &jb, P);
+        }
+    }
+}
+
+int oracle_rs_encode_fast(const uint8_t* data, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
+                          uint8_t* parity, int nthreads) {
+    const int isa = oracle_fast_isa();
+    if (isa == 0 || k > 64) return oracle_rs_encode(data, G, k, r, P, parity, nthreads);
+    if (k == 0 || r == 0 || k + r > 256) return -1;
+    gf_init();
+    uint8_t* M = (uint8_t*)malloc((size_t)k * r);
+    uint64_t* A = (uint64_t*)malloc((size_t)k * r * 8);
+    oracle_parity_matrix(k, r, M);
+    for (uint32_t t = 0; t < k * r; ++t) A[t] = oracle_gf_affine(M[t]);
+    fenc_arg a = {data, k, r, P, isa, A, M, parity};
+    run_ranges(fenc_range, &a, G, nthreads);
+    free(M); free(A);
+    return 0;
+}
+
+/* Recovery rows of one erasure pattern (same survivor rule and inversion as dec_range). */
+typedef struct {
+    uint64_t mask; int valid, ok;
+    uint32_t e;
+    uint8_t surv[FAST_MAXK], erased[FAST_MAXE];
+    uint8_t coef[FAST_MAXE * FAST_MAXK];
+    uint64_t A[FAST_MAXE * FAST_MAXK];
+} fast_rec;
+
+static void fast_rec_build(fast_rec* R, uint64_t m, uint32_t k, uint32_t r, const uint8_t* M) {
+    uint8_t Gs[FAST_MAXK * FAST_MAXK], Inv[FAST_MAXK * FAST_MAXK];
+    uint32_t surv[64], erased[64], ns = 0, ne = 0;
+    R->mask = m; R->valid = 1; R->ok = 0; R->e = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+        if ((m >> j) & 1) erased[ne++] = j;
+        else surv[ns++] = j;
+    }
+    for (uint32_t i = 0; i < r && ns < k; ++i)
+        if (!((m >> (k + i)) & 1)) surv[ns++] = k + i;
+    if (ns < k || ne > FAST_MAXE) return;
+    for (uint32_t s = 0; s < k; ++s)
+        for (uint32_t j = 0; j < k; ++j)
+            Gs[s * k + j] = surv[s] < k ? (uint8_t)(surv[s] == j) : M[(surv[s] - k) * k + j];
+    if (gf_invert(Gs, Inv, k) != 0) return;
+    R->ok = 1; R->e = ne;
+    for (uint32_t s = 0; s < k; ++s) R->surv[s] = (uint8_t)surv[s];
+    for (uint32_t o = 0; o < ne; ++o) {
+        R->erased[o] = (uint8_t)erased[o];
+        for (uint32_t s = 0; s < k; ++s) {
+            R->coef[o * k + s] = Inv[erased[o] * k + s];
+            R->A[o * k + s] = oracle_gf_affine(Inv[erased[o] * k + s]);
+        }
+    }
+}
+
+typedef struct {
+    uint8_t* data; const uint8_t* parity; const uint64_t* masks;
+    uint32_t k, r, P; int isa; const uint8_t* M; uint8_t* status; int64_t bad;
+    pthread_mutex_t mu;
+} fdec_arg;
+
+static void fdec_range(void* p, uint64_t g0, uint64_t g1) {
+    fdec_arg* a = (fdec_arg*)p;
+    const uint32_t k = a->k, r = a->r, P = a->P;
+    const uint64_t kmask = (1ULL << k) - 1;
+    fast_rec* cache = (fast_rec*)calloc(FAST_TAB, sizeof(fast_rec));
+    fast_job jb;
+    jb.n_in = k;
+    int64_t bad = 0;
+    for (uint64_t g = g0; g < g1; ++g) {
+        const uint64_t m = a->masks[g];
+        if (a->status) a->status[g] = 0;
+        if ((m & kmask) == 0) continue;
+        fast_rec* R = &cache[(m * 0x9E3779B97F4A7C15ULL) >> 55];   /* 9 bits: FAST_TAB */
+        if (!R->valid || R->mask != m) fast_rec_build(R, m, k, r, a->M);
+        if (!R->ok) { if (a->status) a->status[g] = 1; ++bad; continue; }
+        uint8_t* d = a->data + g * k * (uint64_t)P;
+        const uint8_t* par = a->parity + g * r * (uint64_t)P;
+        for (uint32_t s = 0; s < k; ++s)
+            jb.in[s] = R->surv[s] < k ? d + (uint64_t)R->surv[s] * P : par + (uint64_t)(R->surv[s] - k) * P;
+        jb.n_out = R->e;
+        for (uint32_t o = 0; o < R->e; ++o) jb.out[o] = d + (uint64_t)R->erased[o] * P;
+        jb.A = R->A;
+        jb.coef = R->coef;
+        /* in place: erased shards are never survivors, and each column step reads all its
+         * inputs before it stores */
+        fast_run(a->isa, &jb, P);
+    }
+    free(cache);
+    pthread_mutex_lock(&a->mu); a->bad += bad; pthread_mutex_unlock(&a->mu);
+}
+
+int64_t oracle_rs_decode_fast(uint8_t* data, const uint8_t* parity, const uint64_t* erasure_masks,
+                              uint64_t G, uint32_t k, uint32_t r, uint32_t P, uint8_t* status,
+                              int nthreads) {
+    const int isa = oracle_fast_isa();
+    if (isa == 0 || k > FAST_MAXK || r > FAST_MAXE)
+        return oracle_rs_decode(data, parity, erasure_masks, G, k, r, P, status, nthreads);
+    if (k == 0 || r == 0 || k + r > 64) return -1;
+    gf_init();
+    uint8_t* M = (uint8_t*)malloc((size_t)k * r);
+    oracle_parity_matrix(k, r, M);
+    fdec_arg a;
+    a.data = data; a.parity = parity; a.masks = erasure_masks; a.k = k; a.r = r; a.P = P;
+    a.isa = isa; a.M = M; a.status = status; a.bad = 0;
+    pthread_mutex_init(&a.mu, NULL);
+    run_ranges(fdec_range, &a, G, nthreads);
+    pthread_mutex_destroy(&a.mu);
+    free(M);
+    return a.bad;
+}
+
+/* ------------------------------------------------------------------------- */
 /* Go-path semantics                                                          */
 /* ------------------------------------------------------------------------- */
 /* encoder.go:113-163: maxSize over the group, zero-padded XOR (:133-143), header

@@ -74,6 +74,21 @@ int64_t oracle_rs_decode(uint8_t* data, const uint8_t* parity, const uint64_t* e
                          uint64_t G, uint32_t k, uint32_t r, uint32_t P, uint8_t* status,
                          int nthreads);
 
+/* ---- Fast CPU comparator (bench.py cpu_baseline leg) ----
+ * Same results as oracle_rs_encode / oracle_rs_decode (tests check byte equality), computed
+ * the way a tuned CPU library (ISA-L style) does: multiplication by a constant is an 8x8
+ * GF(2) bit matrix applied with GFNI's affine instruction (VGF2P8AFFINEQB), 64 bytes per
+ * instruction with AVX-512 (32 with AVX2+GFNI), recovery rows cached per erasure pattern.
+ * Falls back to the table code above when the CPU lacks GFNI or the shape exceeds
+ * k <= 32, e <= 8.  oracle_fast_isa(): 2 = AVX-512+GFNI, 1 = AVX2+GFNI, 0 = tables. */
+int oracle_fast_isa(void);
+uint64_t oracle_gf_affine(uint8_t c);  /* the affine matrix of x -> c*x */
+int oracle_rs_encode_fast(const uint8_t* data, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
+                          uint8_t* parity, int nthreads);
+int64_t oracle_rs_decode_fast(uint8_t* data, const uint8_t* parity, const uint64_t* erasure_masks,
+                              uint64_t G, uint32_t k, uint32_t r, uint32_t P, uint8_t* status,
+                              int nthreads);
+
 /* ---- Go-path semantics ---- */
 /* encoder.go:113-163.  Writes 11 + maxLen bytes into out (cap checked).  Returns the
  * length, -1 for "no packets in group", -2 for "empty packets", -3 if cap too small. */

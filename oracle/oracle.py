@@ -42,6 +42,10 @@ def lib() -> ctypes.CDLL:
             "oracle_parity_matrix": (_int, [_u32, _u32, _vp]),
             "oracle_rs_encode": (_int, [_vp, _u64, _u32, _u32, _u32, _vp, _int]),
             "oracle_rs_decode": (ctypes.c_int64, [_vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp, _int]),
+            "oracle_fast_isa": (_int, []),
+            "oracle_gf_affine": (_u64, [ctypes.c_uint8]),
+            "oracle_rs_encode_fast": (_int, [_vp, _u64, _u32, _u32, _u32, _vp, _int]),
+            "oracle_rs_decode_fast": (ctypes.c_int64, [_vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp, _int]),
             "oracle_go_generate_redundancy": (ctypes.c_int64, [ctypes.POINTER(_vp), ctypes.POINTER(_sz), _sz, _u64, _vp, _sz]),
             "oracle_go_recover_single": (ctypes.c_int64, [ctypes.POINTER(_vp), ctypes.POINTER(_sz), _vp, _sz, _vp, _sz, _sz, _vp]),
         }
@@ -106,6 +110,28 @@ def rs_decode(data: np.ndarray, parity: np.ndarray, masks: np.ndarray, G: int, k
     st = np.zeros(G, dtype=np.uint8)
     bad = lib().oracle_rs_decode(data.ctypes.data, parity.ctypes.data, masks.ctypes.data, G, k, r, P,
                                  st.ctypes.data, nthreads)
+    assert bad >= 0
+    return int(bad), st
+
+
+def fast_isa() -> int:
+    """2 = AVX-512 + GFNI, 1 = AVX2 + GFNI, 0 = table fallback (oracle_rs_*_fast)."""
+    return int(lib().oracle_fast_isa())
+
+
+def rs_encode_fast(data: np.ndarray, G: int, k: int, r: int, P: int, nthreads: int = 1) -> np.ndarray:
+    """The GFNI comparator (bench.py cpu_baseline); same bytes as rs_encode."""
+    par = np.zeros(G * r * P, dtype=np.uint8)
+    assert lib().oracle_rs_encode_fast(data.ctypes.data, G, k, r, P, par.ctypes.data, nthreads) == 0
+    return par
+
+
+def rs_decode_fast(data: np.ndarray, parity: np.ndarray, masks: np.ndarray, G: int, k: int, r: int, P: int,
+                   nthreads: int = 1):
+    """The GFNI comparator of rs_decode (in place).  Returns (unrecoverable_count, status)."""
+    st = np.zeros(G, dtype=np.uint8)
+    bad = lib().oracle_rs_decode_fast(data.ctypes.data, parity.ctypes.data, masks.ctypes.data, G, k, r, P,
+                                      st.ctypes.data, nthreads)
     assert bad >= 0
     return int(bad), st
 

@@ -1018,6 +1018,9 @@ __global__ __launch_bounds__(256) void fill_bytes(uint8_t* __restrict__ dst, uin
 }
 
 constexpr uint32_t kMaxThreadsPerLaunch = 1u << 30;
+// Wave-per-group decode launches: 256-thread workgroups, so at most 2^22 of them keep the
+// grid's work-item count (blocks * 256) inside 32 bits with room to spare.
+constexpr uint64_t kMaxWaveBlocks = kMaxThreadsPerLaunch / 256u;
 constexpr uint32_t kVecMinP = 16;  // shorter packets take the byte kernels
 
 inline uint32_t blocks_for(uint64_t n) { return static_cast<uint32_t>((n + 255) / 256); }
@@ -1169,8 +1172,8 @@ hipError_t run_decode_v16(const DecodeLaunch& a, hipStream_t s) {
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t m0 = p * MAXE;
     const uint64_t blocks = (a.groups + 3) / 4;
-    for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 24)) {
-      const uint64_t bn = (blocks - b0 < (1u << 24)) ? blocks - b0 : (1u << 24);
+    for (uint64_t b0 = 0; b0 < blocks; b0 += kMaxWaveBlocks) {
+      const uint64_t bn = (blocks - b0 < kMaxWaveBlocks) ? blocks - b0 : kMaxWaveBlocks;
       const uint64_t g0 = b0 * 4;
       const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
       hipLaunchKernelGGL((decode_v16<K, MAXE>), dim3(static_cast<uint32_t>(bn)), dim3(256), 0, s,
@@ -1195,8 +1198,8 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
     const uint32_t slice = (POL & kLdsTabs) != 0 ? (rows * a.k * 2u + 63u) / 64u * 1024u : 0u;
     const uint32_t smem = cap > 4 * slice ? cap : 4 * slice;
     const uint64_t blocks = (a.groups + 3) / 4;
-    for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 24)) {
-      const uint64_t bn = (blocks - b0 < (1u << 24)) ? blocks - b0 : (1u << 24);
+    for (uint64_t b0 = 0; b0 < blocks; b0 += kMaxWaveBlocks) {
+      const uint64_t bn = (blocks - b0 < kMaxWaveBlocks) ? blocks - b0 : kMaxWaveBlocks;
       const uint64_t g0 = b0 * 4;
       const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
       hipLaunchKernelGGL((decode_wave<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
@@ -1224,8 +1227,8 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t m0 = p * MAXE;
     const uint64_t blocks = (a.groups + 3) / 4;
-    for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 24)) {
-      const uint64_t bn = (blocks - b0 < (1u << 24)) ? blocks - b0 : (1u << 24);
+    for (uint64_t b0 = 0; b0 < blocks; b0 += kMaxWaveBlocks) {
+      const uint64_t bn = (blocks - b0 < kMaxWaveBlocks) ? blocks - b0 : kMaxWaveBlocks;
       const uint64_t g0 = b0 * 4;
       const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
       hipLaunchKernelGGL((decode_fused<K, MAXE, POL, NM, NT, DIRECT, INLINE>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
@@ -1253,17 +1256,18 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
 // through LDS (kLdsTabs): k=20 r=5, 5 erasures, 1200 B: 2.27 -> 4.73-4.92 TB/s
 // (profiles/r01_probe_decode_ldstabs_k20.txt); at k=10 r=3, whose 286 records stay in the
 // scalar cache, it gains nothing (profiles/r01_probe_decode_inline_k10.txt).
-hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct) {
+// dry: only report whether a form exists (hipSuccess) without launching it.
+hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, bool dry = false) {
   const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
 #define QFEC_FUSED_D(KK, RR, NMM, NTT)                                                        \
   if (direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                             \
-    return run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true>(a, s);
+    return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true>(a, s);
 #define QFEC_FUSED_R(KK, RR, NMM, NTT)                                                        \
   if (!direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                            \
-    return run_decode_fused<KK, RR, kNtStore, NMM, NTT, false>(a, s);
+    return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore, NMM, NTT, false>(a, s);
 #define QFEC_FUSED_L(KK, RR, NMM, NTT)                                                        \
   if (!direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                            \
-    return run_decode_fused<KK, RR, kNtStore | kLdsTabs, NMM, NTT, false>(a, s);
+    return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore | kLdsTabs, NMM, NTT, false>(a, s);
 #define QFEC_FUSED_P(M, KK, RR)                                                               \
   M(KK, RR, 0, 2) M(KK, RR, 0, 3) M(KK, RR, 0, 4) M(KK, RR, 1, 0) M(KK, RR, 1, 1)            \
   M(KK, RR, 1, 2) M(KK, RR, 1, 3) M(KK, RR, 1, 4)
@@ -1287,8 +1291,9 @@ hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s)
   const uint32_t cpp = (a.P + 15u) / 16u;
   const uint32_t bs = (tile * cpp + 63) / 64 * 64;
   const uint64_t blocks = (a.groups + tile - 1) / tile;
-  for (uint64_t b0 = 0; b0 < blocks; b0 += (1u << 30)) {
-    const uint64_t bn = (blocks - b0 < (1u << 30)) ? blocks - b0 : (1u << 30);
+  const uint64_t max_blocks = kMaxThreadsPerLaunch / bs;  // blocks * bs stays a 32-bit grid
+  for (uint64_t b0 = 0; b0 < blocks; b0 += max_blocks) {
+    const uint64_t bn = (blocks - b0 < max_blocks) ? blocks - b0 : max_blocks;
     const uint64_t g0 = b0 * tile;
     const uint64_t gn = (a.groups - g0 < bn * tile) ? a.groups - g0 : bn * tile;
     hipLaunchKernelGGL((decode_tiled<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(bs), 0, s,
@@ -1301,21 +1306,31 @@ hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s)
   return hipSuccess;
 }
 
+bool decode_tiled_form(const DecodeLaunch& a) {
+  const uint32_t tile = a.P >= kVecMinP ? pick_tile((a.P + 15u) / 16u, a.k, a.P) : 0u;
+  return tile > 0 && ((a.variant == kDecodeAuto && a.P <= kTiledMaxP) || a.variant == kDecodeTiledPlain ||
+                      a.variant == kDecodeTiledNt);
+}
+
+// Mask-addressed fused form (r <= 3): +1.2% at k=10 r=3 (tools/probe_decode.hip,
+// r01_probe_decode_direct.txt); at k=20 r=5 its extra VGPRs cost a wave per SIMD (-30%), so
+// auto takes it for r <= 3 only.  It classifies inline: one launch, no classify kernel.
+bool decode_direct_form(const DecodeLaunch& a) {
+  return a.P >= kVecMinP && !decode_tiled_form(a) && a.masks != nullptr && !a.rec_ready &&
+         (a.variant == kDecodeFusedDirect || (a.variant == kDecodeAuto && a.r <= 3)) &&
+         try_decode_fused(a, nullptr, true, /*dry=*/true) == hipSuccess;
+}
+
 }  // namespace
+
+bool decode_needs_rec_off(const DecodeLaunch& a) { return a.groups > 0 && !decode_direct_form(a); }
 
 hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
   if (a.groups == 0) return hipSuccess;
   const uint32_t tile = a.P >= kVecMinP ? pick_tile((a.P + 15u) / 16u, a.k, a.P) : 0u;
-  const bool tiled = tile > 0 && ((a.variant == kDecodeAuto && a.P <= kTiledMaxP) ||
-                                  a.variant == kDecodeTiledPlain || a.variant == kDecodeTiledNt);
-  // Mask-addressed fused form (r <= 3): +1.2% at k=10 r=3 (tools/probe_decode.hip,
-  // r01_probe_decode_direct.txt); at k=20 r=5 its extra VGPRs cost a wave per SIMD (-30%), so
-  // auto takes it for r <= 3 only.  It classifies inline: one launch, no classify kernel.
-  if (a.P >= kVecMinP && !tiled && a.masks != nullptr && !a.rec_ready &&
-      (a.variant == kDecodeFusedDirect || (a.variant == kDecodeAuto && a.r <= 3))) {
-    const hipError_t e = try_decode_fused(a, s, true);
-    if (e != hipErrorNotSupported) return e;
-  }
+  const bool tiled = decode_tiled_form(a);
+  if (decode_direct_form(a)) return try_decode_fused(a, s, true);
+  if (a.rec_off == nullptr) return hipErrorInvalidValue;  // every other form reads rec_off
   for (uint64_t g0 = 0; !a.rec_ready && g0 < a.groups; g0 += kMaxThreadsPerLaunch) {
     const uint64_t gn = (a.groups - g0 < kMaxThreadsPerLaunch) ? a.groups - g0 : kMaxThreadsPerLaunch;
     hipLaunchKernelGGL(classify, dim3(blocks_for(gn)), dim3(256), 0, s, a.masks + g0, gn, a.k, a.r,

@@ -87,6 +87,9 @@ constexpr int kDecodeWaveXcdSwizzle = 1;
 
 hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s);
 hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s);
+// Whether launch_decode(a) uses the rec_off workspace (every form but the mask-addressed
+// one, which classifies inline).  The caller then provides a workspace private to the call.
+bool decode_needs_rec_off(const DecodeLaunch& a);
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);
 

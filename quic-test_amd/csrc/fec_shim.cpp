@@ -10,7 +10,11 @@
 // call (Go goroutines migrate between OS threads and the HIP current device is
 // thread-local), restoring the caller's device afterwards.
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -260,11 +264,16 @@ struct FECEncoderCtx {
   hipStream_t stream = nullptr;
   std::mutex mu;
   // staging / workspace buffers
-  DevBuf d_in, d_off, d_out, d_mask, d_status, d_rec, d_binom;
+  DevBuf d_in, d_off, d_out, d_mask, d_status, d_binom;
   HostBuf z_in, z_out, z_aux;           // zero-copy staging of small host-resident calls
   PipeSlot pipe[kPipeSlots];
   std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<EncodePlan>> enc_plans;
   std::map<std::pair<uint32_t, uint32_t>, std::unique_ptr<DecodePlan>> dec_plans;
+  // Message of the last failing call on this context (fec_ctx_last_error): callers whose
+  // threads migrate between the failing call and the read (Go goroutines) cannot rely on the
+  // thread-local fec_hip_last_error.  Own lock: readable while a call holds `mu`.
+  std::mutex err_mu;
+  std::string last_error;
 
   ~FECEncoderCtx() {
     DeviceGuard g(device);
@@ -276,7 +285,6 @@ struct FECEncoderCtx {
     d_out.release();
     d_mask.release();
     d_status.release();
-    d_rec.release();
     d_binom.release();
     z_in.release();
     z_out.release();
@@ -335,6 +343,10 @@ FECEncoderCtx* make_ctx(double redundancy, uint32_t max_groups, int device) {
 }
 
 int get_encode_plan(FECEncoderCtx* ctx, uint32_t k, uint32_t r, const void** tables) {
+  if (r == 1) {  // the XOR row alone needs no coefficients, so any number of packets works
+    *tables = nullptr;
+    return k > 0 ? FEC_OK : FEC_ERR_RANGE;
+  }
   auto key = std::make_pair(k, r);
   auto it = ctx->enc_plans.find(key);
   if (it == ctx->enc_plans.end()) {
@@ -415,6 +427,36 @@ int encode_dev_locked(FECEncoderCtx* ctx, const uint8_t* d_data, const void* d_o
   return FEC_OK;
 }
 
+// Per-call record-offset workspace, ordered on the call's stream: allocated before the
+// launch and released behind it with the stream-ordered allocator, so decodes in flight on
+// different streams never share one (the context-wide buffer they used to share could be
+// overwritten by the next call's classify before the previous call's decode read it).
+struct StreamScratch {
+  void* ptr = nullptr;
+  hipStream_t s = nullptr;
+  bool async = false;
+  hipError_t alloc(size_t bytes, hipStream_t stream) {
+    s = stream;
+    hipError_t e = hipMallocAsync(&ptr, bytes, s);
+    if (e == hipSuccess) {
+      async = true;
+      return e;
+    }
+    (void)hipGetLastError();  // no memory pools: a plain allocation, released after a sync
+    ptr = nullptr;
+    return hipMalloc(&ptr, bytes);
+  }
+  ~StreamScratch() {
+    if (!ptr) return;
+    if (async) {
+      (void)hipFreeAsync(ptr, s);
+    } else {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(ptr);
+    }
+  }
+};
+
 int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
                       const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
                       uint8_t* d_status, hipStream_t s, DevBuf* rec = nullptr,
@@ -422,35 +464,14 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   DecodePlan* plan = nullptr;
   int rc = get_decode_plan(ctx, k, r, &plan);
   if (rc != FEC_OK) return rc;
-  DevBuf& ws = rec ? *rec : ctx->d_rec;
-  QFEC_HIP(ws.ensure(G * sizeof(uint32_t)));
   qfec::DecodeLaunch a;
   a.data = d_data;
   a.parity = d_parity;
   a.masks = d_masks;
-  a.rec_off = ws.as<uint32_t>();
+  a.rec_off = nullptr;
   a.out = d_out;
   a.status = d_status;
   a.codebook = plan->codebook.as<uint8_t>();
-  if (!plan->dense) {
-    // Sparse plan: the masks come to the host (after the stream's earlier work), records
-    // are built for the patterns present, and the call completes synchronously.
-    std::vector<uint64_t> hm(G);
-    QFEC_HIP(hipStreamSynchronize(s));
-    QFEC_HIP(hipMemcpy(hm.data(), d_masks, G * 8, hipMemcpyDefault));
-    std::vector<uint8_t> book, st;
-    std::vector<uint32_t> ro;
-    if (!qfec::build_sparse_plan(k, r, plan->M, hm.data(), G, qfec::kRecNone, qfec::kRecBad, book, ro, st)) {
-      set_error("decode: sparse plan failed for k=%u r=%u", k, r);
-      return FEC_ERR_RANGE;
-    }
-    QFEC_HIP(plan->sparse_book.ensure(book.size() + 32));
-    if (!book.empty()) QFEC_HIP(hipMemcpy(plan->sparse_book.ptr, book.data(), book.size(), hipMemcpyHostToDevice));
-    QFEC_HIP(hipMemcpy(ws.ptr, ro.data(), G * 4, hipMemcpyHostToDevice));
-    if (d_status) QFEC_HIP(hipMemcpy(d_status, st.data(), G, hipMemcpyDefault));
-    a.codebook = plan->sparse_book.as<uint8_t>();
-    a.rec_ready = true;
-  }
   a.binom = ctx->d_binom.as<uint64_t>();
   std::memset(&a.meta, 0, sizeof(a.meta));
   for (uint32_t e = 1; e <= 32; ++e) {
@@ -462,8 +483,41 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   a.k = k;
   a.r = r;
   a.P = P;
+  a.rec_ready = !plan->dense;
+  // Workspace: the caller's slot buffer (pipeline slots: private stream, calls serialised
+  // by the context lock), else one private to this call.
+  StreamScratch scratch;
+  if (!plan->dense || qfec::decode_needs_rec_off(a)) {
+    if (rec) {
+      QFEC_HIP(rec->ensure(G * sizeof(uint32_t)));
+      a.rec_off = rec->as<uint32_t>();
+    } else {
+      QFEC_HIP(scratch.alloc(G * sizeof(uint32_t), s));
+      a.rec_off = static_cast<uint32_t*>(scratch.ptr);
+    }
+  }
+  std::vector<uint8_t> book, st;
+  std::vector<uint32_t> ro;
+  if (!plan->dense) {
+    // Sparse plan: the masks come to the host (after the stream's earlier work), records
+    // are built for the patterns present, and the call completes synchronously.
+    std::vector<uint64_t> hm(G);
+    QFEC_HIP(hipStreamSynchronize(s));
+    QFEC_HIP(hipMemcpy(hm.data(), d_masks, G * 8, hipMemcpyDefault));
+    if (!qfec::build_sparse_plan(k, r, plan->M, hm.data(), G, qfec::kRecNone, qfec::kRecBad, book, ro, st)) {
+      set_error("decode: sparse plan failed for k=%u r=%u", k, r);
+      return FEC_ERR_RANGE;
+    }
+    QFEC_HIP(plan->sparse_book.ensure(book.size() + 32));
+    if (!book.empty())
+      QFEC_HIP(hipMemcpyAsync(plan->sparse_book.ptr, book.data(), book.size(), hipMemcpyHostToDevice, s));
+    QFEC_HIP(hipMemcpyAsync(a.rec_off, ro.data(), G * 4, hipMemcpyHostToDevice, s));
+    if (d_status) QFEC_HIP(hipMemcpyAsync(d_status, st.data(), G, hipMemcpyDefault, s));
+    a.codebook = plan->sparse_book.as<uint8_t>();
+  }
   QFEC_HIP(qfec::launch_decode(a, s));
-  if (!plan->dense) QFEC_HIP(hipStreamSynchronize(s));  // the sparse records are reused next call
+  // sparse: the records (and the host vectors above) are reused / freed after this call
+  if (!plan->dense) QFEC_HIP(hipStreamSynchronize(s));
   return FEC_OK;
 }
 
@@ -748,6 +802,15 @@ void xor_packets_gpu(const uint8_t* packets[], size_t n, size_t packet_size, uin
   }
 }
 
+// Non-zero codes copy the thread's message into the context (fec_ctx_last_error).
+int record_ctx_error(FECEncoderCtx* ctx, int rc) {
+  if (rc != FEC_OK && ctx != nullptr) {
+    std::lock_guard<std::mutex> lk(ctx->err_mu);
+    ctx->last_error = g_last_error.empty() ? "error code " + std::to_string(rc) : g_last_error;
+  }
+  return rc;
+}
+
 }  // namespace
 
 // =====================================================================================
@@ -772,20 +835,71 @@ QFEC_EXPORT void* fec_alloc_slab(size_t size) {
   return p;
 }
 
+namespace {
+
+// NUMA-placed slabs (fec_alloc_slab_numa): mmap'd, mbind'd, then registered with HIP.
+// fec_free_slab looks pointers up here to undo exactly what was done.
+struct NumaSlab {
+  size_t len;
+  bool registered;
+};
+std::mutex g_numa_mu;
+std::map<void*, NumaSlab> g_numa_slabs;
+
+}  // namespace
+
 QFEC_EXPORT void* fec_alloc_slab_numa(size_t size, int numa_node) {
-  (void)numa_node;  // placement of pinned pages is left to the HIP runtime
-  return fec_alloc_slab(size);
+  if (numa_node < 0) return fec_alloc_slab(size);
+  const size_t page = static_cast<size_t>(sysconf(_SC_PAGESIZE));
+  const size_t len = ((size == 0 ? 1 : size) + page - 1) / page * page;
+  void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) {
+    set_error("fec_alloc_slab_numa(%zu): mmap: %s", size, std::strerror(errno));
+    return nullptr;
+  }
+  // Bind before the first touch so every page is allocated on the node (fec_xor_simd.cpp:
+  // 497-502 binds with MPOL_MF_MOVE and ignores failure; so does this -- e.g. a node the
+  // machine does not have leaves the default policy).  The range is page-aligned, which
+  // mbind requires.
+  constexpr int kMaxNodes = 1024;
+  unsigned long mask[kMaxNodes / (8 * sizeof(unsigned long))] = {};
+  if (numa_node < kMaxNodes) {
+    mask[numa_node / (8 * sizeof(unsigned long))] |= 1ul << (numa_node % (8 * sizeof(unsigned long)));
+    constexpr int kMpolBind = 2, kMpolMfMove = 1 << 1;
+    (void)syscall(SYS_mbind, p, len, kMpolBind, mask, static_cast<unsigned long>(kMaxNodes + 1), kMpolMfMove);
+  }
+  // Page-lock for DMA / zero-copy kernel access; pinning faults the pages in under the
+  // policy above.  Without a GPU the memory stays pageable (the reference's behaviour).
+  bool registered = false;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0)
+    registered = hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess;
+  (void)hipGetLastError();
+  std::lock_guard<std::mutex> lk(g_numa_mu);
+  g_numa_slabs[p] = NumaSlab{len, registered};
+  return p;
 }
 
 QFEC_EXPORT void* fec_alloc_repair_buffer(size_t size) { return fec_alloc_slab(size); }
 
 QFEC_EXPORT void fec_free_slab(void* ptr) {
-  if (ptr) (void)hipHostFree(ptr);
+  if (!ptr) return;
+  {
+    std::lock_guard<std::mutex> lk(g_numa_mu);
+    auto it = g_numa_slabs.find(ptr);
+    if (it != g_numa_slabs.end()) {
+      if (it->second.registered) (void)hipHostUnregister(ptr);
+      (void)munmap(ptr, it->second.len);
+      g_numa_slabs.erase(it);
+      return;
+    }
+  }
+  (void)hipHostFree(ptr);
 }
 
 QFEC_EXPORT void fec_free_repair_buffer(void* ptr) { fec_free_slab(ptr); }
 
-QFEC_EXPORT int fec_encode_batch(FECEncoderCtx* ctx, const uint8_t* slab, const uint32_t* offsets,
+static int fec_encode_batch_impl(FECEncoderCtx* ctx, const uint8_t* slab, const uint32_t* offsets,
                                  uint32_t num_groups, uint32_t packet_size, uint8_t* repair_out) {
   // fec_xor_simd.cpp:564-570, same order
   if (ctx == nullptr || slab == nullptr || offsets == nullptr || repair_out == nullptr) return -1;
@@ -882,6 +996,12 @@ QFEC_EXPORT int fec_encode_batch(FECEncoderCtx* ctx, const uint8_t* slab, const 
   return 0;
 }
 
+QFEC_EXPORT int fec_encode_batch(FECEncoderCtx* ctx, const uint8_t* slab, const uint32_t* offsets,
+                                 uint32_t num_groups, uint32_t packet_size, uint8_t* repair_out) {
+  g_last_error.clear();
+  return record_ctx_error(ctx, fec_encode_batch_impl(ctx, slab, offsets, num_groups, packet_size, repair_out));
+}
+
 QFEC_EXPORT xor_impl_fn fec_select_xor_impl(void) { return xor_packets_gpu; }
 
 QFEC_EXPORT void xor_packets_scalar(const uint8_t* packets[], size_t n, size_t packet_size,
@@ -915,6 +1035,17 @@ QFEC_EXPORT int fec_hip_device_count(void) {
 }
 
 QFEC_EXPORT const char* fec_hip_last_error(void) { return g_last_error.c_str(); }
+
+QFEC_EXPORT size_t fec_ctx_last_error(FECEncoderCtx* ctx, char* buf, size_t buflen) {
+  if (!ctx) return 0;
+  std::lock_guard<std::mutex> lk(ctx->err_mu);
+  if (buf && buflen > 0) {
+    const size_t n = ctx->last_error.size() < buflen - 1 ? ctx->last_error.size() : buflen - 1;
+    std::memcpy(buf, ctx->last_error.data(), n);
+    buf[n] = '\0';
+  }
+  return ctx->last_error.size();
+}
 
 QFEC_EXPORT FECEncoderCtx* fec_encoder_new_device(double redundancy, uint32_t max_groups, int device) {
   if (device < 0) {
@@ -952,7 +1083,7 @@ int check_shape(uint64_t G, uint32_t k, uint32_t r, uint32_t P, bool decode) {
 
 }  // namespace
 
-QFEC_EXPORT int fec_encode_batch_rs(FECEncoderCtx* ctx, const uint8_t* data, const uint64_t* offsets,
+static int fec_encode_batch_rs_impl(FECEncoderCtx* ctx, const uint8_t* data, const uint64_t* offsets,
                                     uint64_t G, uint32_t k, uint32_t r, uint32_t P, uint8_t* parity_out) {
   if (!ctx || !data || !parity_out) return FEC_ERR_NULL;
   int rc = check_shape(G, k, r, P, false);
@@ -1031,7 +1162,13 @@ QFEC_EXPORT int fec_encode_batch_rs(FECEncoderCtx* ctx, const uint8_t* data, con
   return FEC_OK;
 }
 
-QFEC_EXPORT int fec_decode_batch_rs(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* parity,
+QFEC_EXPORT int fec_encode_batch_rs(FECEncoderCtx* ctx, const uint8_t* data, const uint64_t* offsets,
+                                    uint64_t G, uint32_t k, uint32_t r, uint32_t P, uint8_t* parity_out) {
+  g_last_error.clear();
+  return record_ctx_error(ctx, fec_encode_batch_rs_impl(ctx, data, offsets, G, k, r, P, parity_out));
+}
+
+static int fec_decode_batch_rs_impl(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* parity,
                                     const uint64_t* masks, uint64_t G, uint32_t k, uint32_t r,
                                     uint32_t P, uint8_t* status_out, uint64_t* unrecoverable_out) {
   if (!ctx || !data || !parity || !masks) return FEC_ERR_NULL;
@@ -1120,7 +1257,14 @@ QFEC_EXPORT int fec_decode_batch_rs(FECEncoderCtx* ctx, uint8_t* data, const uin
   return FEC_OK;
 }
 
-QFEC_EXPORT int fec_encode_batch_rs_dev(FECEncoderCtx* ctx, const uint8_t* d_data, uint64_t G,
+QFEC_EXPORT int fec_decode_batch_rs(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* parity,
+                                    const uint64_t* masks, uint64_t G, uint32_t k, uint32_t r,
+                                    uint32_t P, uint8_t* status_out, uint64_t* unrecoverable_out) {
+  g_last_error.clear();
+  return record_ctx_error(ctx, fec_decode_batch_rs_impl(ctx, data, parity, masks, G, k, r, P, status_out, unrecoverable_out));
+}
+
+static int fec_encode_batch_rs_dev_impl(FECEncoderCtx* ctx, const uint8_t* d_data, uint64_t G,
                                         uint32_t k, uint32_t r, uint32_t P, uint8_t* d_parity,
                                         void* stream) {
   if (!ctx || !d_data || !d_parity) return FEC_ERR_NULL;
@@ -1134,7 +1278,14 @@ QFEC_EXPORT int fec_encode_batch_rs_dev(FECEncoderCtx* ctx, const uint8_t* d_dat
                            pick_stream(ctx, stream));
 }
 
-QFEC_EXPORT int fec_decode_batch_rs_dev(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
+QFEC_EXPORT int fec_encode_batch_rs_dev(FECEncoderCtx* ctx, const uint8_t* d_data, uint64_t G,
+                                        uint32_t k, uint32_t r, uint32_t P, uint8_t* d_parity,
+                                        void* stream) {
+  g_last_error.clear();
+  return record_ctx_error(ctx, fec_encode_batch_rs_dev_impl(ctx, d_data, G, k, r, P, d_parity, stream));
+}
+
+static int fec_decode_batch_rs_dev_impl(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
                                         const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r,
                                         uint32_t P, uint8_t* d_status, void* stream) {
   if (!ctx || !d_data || !d_parity || !d_masks) return FEC_ERR_NULL;
@@ -1148,7 +1299,14 @@ QFEC_EXPORT int fec_decode_batch_rs_dev(FECEncoderCtx* ctx, uint8_t* d_data, con
                            pick_stream(ctx, stream));
 }
 
-QFEC_EXPORT int fec_decode_prepare(FECEncoderCtx* ctx, uint32_t k, uint32_t r, uint64_t* bytes_out) {
+QFEC_EXPORT int fec_decode_batch_rs_dev(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
+                                        const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r,
+                                        uint32_t P, uint8_t* d_status, void* stream) {
+  g_last_error.clear();
+  return record_ctx_error(ctx, fec_decode_batch_rs_dev_impl(ctx, d_data, d_parity, d_masks, G, k, r, P, d_status, stream));
+}
+
+static int fec_decode_prepare_impl(FECEncoderCtx* ctx, uint32_t k, uint32_t r, uint64_t* bytes_out) {
   if (!ctx) return FEC_ERR_NULL;
   int rc = check_shape(1, k, r, 1, true);
   if (rc != FEC_OK) return rc;
@@ -1162,7 +1320,12 @@ QFEC_EXPORT int fec_decode_prepare(FECEncoderCtx* ctx, uint32_t k, uint32_t r, u
   return FEC_OK;
 }
 
-QFEC_EXPORT int fec_fill_random_dev(FECEncoderCtx* ctx, uint8_t* d_dst, uint64_t nbytes, uint64_t seed,
+QFEC_EXPORT int fec_decode_prepare(FECEncoderCtx* ctx, uint32_t k, uint32_t r, uint64_t* bytes_out) {
+  g_last_error.clear();
+  return record_ctx_error(ctx, fec_decode_prepare_impl(ctx, k, r, bytes_out));
+}
+
+static int fec_fill_random_dev_impl(FECEncoderCtx* ctx, uint8_t* d_dst, uint64_t nbytes, uint64_t seed,
                                     uint64_t byte_offset, void* stream) {
   if (!ctx || !d_dst) return FEC_ERR_NULL;
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1170,6 +1333,12 @@ QFEC_EXPORT int fec_fill_random_dev(FECEncoderCtx* ctx, uint8_t* d_dst, uint64_t
   if (!dg.ok) return FEC_ERR_NODEV;
   QFEC_HIP(qfec::launch_fill_splitmix(d_dst, nbytes, seed, byte_offset, pick_stream(ctx, stream)));
   return FEC_OK;
+}
+
+QFEC_EXPORT int fec_fill_random_dev(FECEncoderCtx* ctx, uint8_t* d_dst, uint64_t nbytes, uint64_t seed,
+                                    uint64_t byte_offset, void* stream) {
+  g_last_error.clear();
+  return record_ctx_error(ctx, fec_fill_random_dev_impl(ctx, d_dst, nbytes, seed, byte_offset, stream));
 }
 
 QFEC_EXPORT int fec_synchronize(FECEncoderCtx* ctx) {

@@ -38,7 +38,7 @@ REFERENCE_SYMBOLS = (
     "xor_packets_neon",
 )
 HIP_SYMBOLS = (
-    "fec_hip_device_count", "fec_hip_last_error", "fec_encoder_new_device", "fec_encoder_device",
+    "fec_hip_device_count", "fec_hip_last_error", "fec_ctx_last_error", "fec_encoder_new_device", "fec_encoder_device",
     "fec_hip_version", "fec_parity_matrix", "fec_encode_batch_rs", "fec_decode_batch_rs",
     "fec_encode_batch_rs_dev", "fec_decode_batch_rs_dev", "fec_decode_prepare",
     "fec_fill_random_dev", "fec_synchronize",
@@ -99,6 +99,7 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
         "fec_hip_device_count": (_int, []),
         "fec_hip_last_error": (ctypes.c_char_p, []),
         "fec_hip_version": (ctypes.c_char_p, []),
+        "fec_ctx_last_error": (_sz, [_vp, ctypes.c_char_p, _sz]),
         "fec_parity_matrix": (_int, [_u32, _u32, _vp]),
         "fec_encode_batch_rs": (_int, [_vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp]),
         "fec_decode_batch_rs": (_int, [_vp, _vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp]),
@@ -171,6 +172,13 @@ class Context:
         if not h:
             raise FecError("fec_encoder_new", FEC_ERR_NODEV, last_error())
         self.handle = h
+
+    def last_error(self) -> str:
+        """Message of the last failing call on this context, from any thread."""
+        n = int(self.lib.fec_ctx_last_error(self.handle, None, 0))
+        buf = ctypes.create_string_buffer(n + 1)
+        self.lib.fec_ctx_last_error(self.handle, buf, n + 1)
+        return buf.value.decode(errors="replace")
 
     @property
     def device(self) -> int:

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "fec.hpp"
+#include "fec_hip.h"
 
 extern "C" {
 int64_t oracle_go_generate_redundancy(const uint8_t* const*, const size_t*, size_t, uint64_t, uint8_t*, size_t);
@@ -510,7 +511,31 @@ static void TestRSDecoderPartialAndShort() {
   CHECK(d.GetPacket(0, 0) == padded(data[0], 260) && d.GetPacket(0, 2) == padded(data[2], 260));
 }
 
+// fec_ctx_last_error: a call fails on one thread and the message is read on another, as a
+// Go goroutine does when it moves to another OS thread between the call and the read
+// (fec_hip_rs.go; the reference maps a failure to a code-only error, fec_cgo.go:147-149).
+static void TestContextErrorAcrossThreads() {
+  FECEncoderCtx* ctx = fec_encoder_new(0.10, 16);
+  CHECK(ctx != nullptr);
+  if (!ctx) return;
+  int rc = 0;
+  std::thread t([&] {
+    Bytes d(16 * 300), p(16 * 300);
+    rc = fec_encode_batch_rs(ctx, d.data(), nullptr, 1, 200, 100, 16, p.data());
+  });
+  t.join();
+  CHECK(rc == FEC_ERR_RANGE);
+  CHECK(std::string(fec_hip_last_error()).empty());  // this thread made no failing call
+  char buf[256];
+  const size_t n = fec_ctx_last_error(ctx, buf, sizeof(buf));
+  CHECK(n > 0 && std::string(buf).find("k=200 r=100") != std::string::npos);
+  char small[8];
+  CHECK(fec_ctx_last_error(ctx, small, sizeof(small)) == n && std::strlen(small) == 7);
+  fec_encoder_free(ctx);
+}
+
 int main() {
+  TestContextErrorAcrossThreads();
   TestNewFECEncoder();
   TestAddPacket();
   TestFECEncoderFullGroup();

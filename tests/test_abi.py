@@ -107,3 +107,47 @@ def test_kernel_arithmetic_emulation(tmp_path, oracle_mod):
                     f"-Wl,-rpath,{oracle_mod.ORACLE_DIR}", "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and out.stdout.startswith("OK"), out.stdout + out.stderr
+
+
+def test_ctx_last_error_null_context(quicfec_mod):
+    lib = quicfec_mod.load_library()
+    import ctypes
+    buf = ctypes.create_string_buffer(16)
+    assert lib.fec_ctx_last_error(None, buf, 16) == 0
+
+
+def _vma_policy(addr: int):
+    """(mode, nodemask word 0) of the mapping at addr: get_mempolicy(MPOL_F_ADDR)."""
+    import ctypes
+    libc = ctypes.CDLL(None, use_errno=True)
+    mode = ctypes.c_int(-1)
+    mask = (ctypes.c_ulong * 16)()
+    SYS_get_mempolicy, MPOL_F_ADDR = 239, 1 << 1
+    rc = libc.syscall(SYS_get_mempolicy, ctypes.byref(mode), mask, ctypes.c_ulong(1024 + 1),
+                      ctypes.c_void_p(addr), ctypes.c_ulong(MPOL_F_ADDR))
+    if rc != 0:
+        pytest.skip(f"get_mempolicy unavailable (errno {ctypes.get_errno()})")
+    return mode.value, mask[0]
+
+
+def test_alloc_slab_numa_binds_node(quicfec_mod):
+    """fec_alloc_slab_numa(size, node) binds the pages to the node (fec_xor_simd.cpp:486-510
+    mbinds with MPOL_BIND); read the policy back with get_mempolicy."""
+    import ctypes
+    lib = quicfec_mod.load_library()
+    size = 3 * 4096 + 100
+    p = lib.fec_alloc_slab_numa(size, 0)
+    assert p, quicfec_mod.last_error()
+    try:
+        assert p % 4096 == 0
+        ctypes.memset(p, 0xA5, size)              # usable memory, every byte
+        assert ctypes.string_at(p + size - 1, 1) == b"\xa5"
+        mode, nodes = _vma_policy(p)
+        MPOL_BIND = 2
+        assert mode == MPOL_BIND and nodes & 1, (mode, nodes)
+    finally:
+        lib.fec_free_slab(p)
+    # node < 0: the plain allocator (NULL without a GPU, as fec_alloc_slab)
+    q = lib.fec_alloc_slab_numa(64, -1)
+    if q:
+        lib.fec_free_slab(q)

@@ -60,6 +60,60 @@ def test_group_sharding_and_reductions(world):
         assert off == g0 * 12000
 
 
+def test_launch_plan_gpus_vs_world_size():
+    sys.path.insert(0, str(REPO))
+    import bench
+    assert bench.launch_plan(1, {}) == ("run", 1)
+    assert bench.launch_plan(8, {}) == ("spawn", 8)
+    assert bench.launch_plan(4, {"WORLD_SIZE": "4"}) == ("run", 4)
+    assert bench.launch_plan(1, {"WORLD_SIZE": "1"}) == ("run", 1)
+    with pytest.raises(SystemExit, match="disagrees"):
+        bench.launch_plan(8, {"WORLD_SIZE": "2"})
+    with pytest.raises(SystemExit, match="disagrees"):
+        bench.launch_plan(1, {"WORLD_SIZE": "8"})
+    with pytest.raises(SystemExit):
+        bench.launch_plan(0, {})
+
+
+def test_bind_local_device(monkeypatch):
+    sys.path.insert(0, str(REPO))
+    import bench
+    monkeypatch.setenv("QUICFEC_DIST_BACKEND", "nccl")
+    assert bench.bind_local_device(3, 8, 8) == 3
+    with pytest.raises(SystemExit, match="only 1 visible"):
+        bench.bind_local_device(1, 2, 1)
+    with pytest.raises(SystemExit):
+        bench.bind_local_device(0, 1, 0)
+    monkeypatch.setenv("QUICFEC_DIST_BACKEND", "gloo")      # one-GPU rehearsal shares the card
+    assert bench.bind_local_device(1, 2, 1) == 0
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_bench_gpus_n_spawns_n_ranks(world):
+    """`python bench.py --gpus N` with no WORLD_SIZE starts N ranks itself (gloo, CPU)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["QUICFEC_DIST_BACKEND"] = "gloo"
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", str(world), "--launch-selftest"],
+                         env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout                       # rank 0 only
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == world and rec["gpus_arg"] == world
+    assert rec["max_elapsed"] == pytest.approx(0.25 * world)
+    assert rec["total_groups"] == pytest.approx(1000 * world)
+
+
+def test_bench_gpus_disagreeing_world_size_fails():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "4", "--launch-selftest"],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "disagrees" in out.stderr
+
+
 def test_shard_range_single():
     sys.path.insert(0, str(REPO))
     import bench

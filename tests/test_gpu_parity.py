@@ -541,3 +541,64 @@ def test_small_calls_zero_copy_and_dma(gpu_ctx, quicfec_mod, oracle_mod, xor_gol
     out = np.zeros(1200, dtype=np.uint8)
     quicfec_mod.xor_packets(pk, 1200, out)
     assert np.array_equal(out, oracle_mod.xor_packets(pk, 1200))
+
+
+# ---------------- round-2 fixes ----------------
+
+@pytest.mark.parametrize("n", [255, 256, 300, 1000])
+def test_xor_packets_many_packets(quicfec_mod, oracle_mod, n):
+    """xor_packets_* XOR any number of packets like xor_packets_scalar
+    (fec_xor_simd.cpp:411-427): the XOR row needs no GF matrix, so n >= 256 works."""
+    P = 1200
+    pk = [oracle_mod.splitmix_bytes(P, 0xA000 + i) for i in range(n)]
+    out = np.full(P, 0xCC, dtype=np.uint8)
+    quicfec_mod.xor_packets(pk, P, out)
+    assert quicfec_mod.last_error() == ""
+    assert np.array_equal(out, oracle_mod.xor_packets(pk, P, avx2=False))
+
+
+@pytest.mark.parametrize("k,r,P,erasures", [(20, 5, 1200, 5), (10, 3, 200, 2), (6, 4, 1000, 3)])
+def test_concurrent_decodes_on_two_streams(gpu_ctx, oracle_mod, torch_cuda, k, r, P, erasures):
+    """Two decodes in flight at once on two streams of one context, each with its own
+    record-offset workspace (forms that classify first: record-addressed k=20 r=5, tiled
+    P <= 256, runtime k).  Each must rebuild its own batch exactly."""
+    torch = torch_cuda
+    G = 4096
+    batches = []
+    for b in range(2):
+        data = oracle_mod.splitmix_bytes(G * k * P, SEED + 77 + b)
+        par = oracle_mod.rs_encode(data, G, k, r, P, nthreads=4)
+        rng = np.random.default_rng(100 + b)
+        pos = np.argsort(rng.random((G, k + r)), axis=1)[:, :erasures].astype(np.uint64)
+        masks = np.left_shift(np.uint64(1), pos).sum(axis=1, dtype=np.uint64)
+        lost = ((masks[:, None] >> np.arange(k, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+        broken = data.copy().reshape(G, k, P)
+        broken[lost] = 0xEE
+        batches.append((data, _dev(torch, broken.reshape(-1)), _dev(torch, par), _dev(torch, masks.view(np.int64))))
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    sts = [torch.full((G,), 7, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    for rep in range(3):                        # several rounds, no host sync between streams
+        for b in range(2):
+            _, dd, dp, dm = batches[b]
+            gpu_ctx.decode_dev(dd, dp, dm, G, k, r, P, sts[b], stream=streams[b].cuda_stream)
+    torch.cuda.synchronize()
+    for b in range(2):
+        data, dd, _, _ = batches[b]
+        assert int(sts[b].sum().item()) == 0
+        assert np.array_equal(dd.cpu().numpy(), data), b
+
+
+def test_ctx_last_error_set_on_failure(gpu_ctx, quicfec_mod):
+    lib = quicfec_mod.load_library()
+    buf = np.zeros(1200 * 4, dtype=np.uint8)
+    rc = lib.fec_encode_batch_rs(gpu_ctx.handle, buf.ctypes.data, None, 1, 200, 100, 16, buf.ctypes.data)
+    assert rc == quicfec_mod.FEC_ERR_RANGE
+    assert "k=200 r=100" in gpu_ctx.last_error()
+    # read from another thread: the context keeps the text
+    import threading
+    seen = []
+    t = threading.Thread(target=lambda: seen.append(gpu_ctx.last_error()))
+    t.start()
+    t.join()
+    assert "k=200 r=100" in seen[0]

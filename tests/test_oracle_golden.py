@@ -175,3 +175,38 @@ def test_mds_round_trip(oracle_mod, k, r, P, seed, data):
     broken = broken.reshape(-1)
     bad, st_ = oracle_mod.rs_decode(broken, par, masks, G, k, r, P)
     assert bad == 0 and np.array_equal(broken, d)
+
+
+def test_gf_affine_matrices(oracle_mod):
+    """oracle_gf_affine(c) applied as VGF2P8AFFINEQB does (output bit i = parity of matrix
+    byte 7-i AND x) is multiplication by c."""
+    xs = np.arange(256)
+    for c in range(256):
+        A = int(oracle_mod.lib().oracle_gf_affine(c))
+        rows = [(A >> (8 * (7 - i))) & 0xFF for i in range(8)]
+        for x in xs[:: 7 if c % 5 else 1]:
+            y = sum((bin(rows[i] & int(x)).count("1") & 1) << i for i in range(8))
+            assert y == oracle_mod.gf_mul(c, int(x)), (c, int(x))
+
+
+@pytest.mark.parametrize("k,r,P,G", [(10, 3, 1200, 300), (20, 5, 1200, 60), (4, 2, 256, 200), (10, 3, 1201, 90),
+                                     (7, 9, 33, 80), (30, 8, 100, 40), (10, 1, 1200, 50), (12, 12, 17, 40),
+                                     (3, 2, 1, 20)])
+def test_fast_comparator_equals_restatement(oracle_mod, k, r, P, G):
+    """The bench's CPU comparator (GFNI form) produces the restatement's bytes, statuses and
+    unrecoverable counts (tails, every parity-row pass, unrecoverable groups)."""
+    rng = np.random.default_rng(k * 1000 + r * 10 + P)
+    data = oracle_mod.splitmix_bytes(G * k * P, 0x5EED + k + r)
+    par = oracle_mod.rs_encode(data, G, k, r, P)
+    assert np.array_equal(oracle_mod.rs_encode_fast(data, G, k, r, P, nthreads=3), par)
+    masks = np.zeros(G, dtype=np.uint64)
+    for g in range(G):
+        for s in rng.permutation(k + r)[: rng.integers(0, r + 2)]:
+            masks[g] |= np.uint64(1) << np.uint64(int(s))
+    lost = ((masks[:, None] >> np.arange(k, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+    a = data.copy().reshape(G, k, P)
+    a[lost] = 0xEE
+    b = a.copy()
+    bad_a, st_a = oracle_mod.rs_decode(a.reshape(-1), par, masks, G, k, r, P)
+    bad_b, st_b = oracle_mod.rs_decode_fast(b.reshape(-1), par, masks, G, k, r, P, nthreads=2)
+    assert bad_a == bad_b and np.array_equal(st_a, st_b) and np.array_equal(a, b)
