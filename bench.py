@@ -41,6 +41,10 @@ CONFIGS = {
                  workload="C2 encode + C3 decode: k=10 r=3, 1200 B packets, 1M groups/GPU, 2 erasures/group"),
     "c4": dict(k=20, r=5, P=1200, groups=1_000_000, erasures=0, decode=False,
                workload="C4 encode: k=20 r=5, 1200 B packets, 1M groups/GPU (8M over 8 GPUs)"),
+    # k=20 r=5 with 5 erasures per group (the C4 shape's worst recoverable decode; evidence
+    # config, not a BASELINE line)
+    "c4d": dict(k=20, r=5, P=1200, groups=500_000, erasures=5, decode=True,
+                workload="C4 shape encode + 5-erasure decode: k=20 r=5, 1200 B packets, 500k groups/GPU"),
     # satellite profile: iid loss 0.01 per packet (internal/network_profiles.go:78)
     "c5": dict(k=10, r=3, P=1200, groups=1_000_000, erasures=0, loss=0.01, decode=True,
                workload="C5 encode + decode, satellite loss (iid p=0.01 per shard): k=10 r=3, 1200 B, 1M groups/GPU"),
@@ -435,16 +439,27 @@ def e2e_pinned(ctx, d_data, d_parity, d_masks, G: int, cfg: dict, reps: int = 3)
     return out
 
 
+def lib_sha256() -> str:
+    """Hash of the libfec_hip.so this process loads (the build being timed)."""
+    import hashlib
+    import quicfec
+    return hashlib.sha256(Path(quicfec.LIB_PATH).read_bytes()).hexdigest()
+
+
 def load_pmc_traffic(config: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/pmc_<config>.json),
-    if one exists for this build; else None."""
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/pmc_<config>.json,
+    scripts/gpu_pmc.sh), used only when they were measured on this very library build (the
+    file's lib_sha256 equals the loaded .so's).  Returns (pmc dict or None, note)."""
     p = REPO / "profiles" / f"pmc_{config}.json"
     if not p.exists():
-        return None
+        return None, f"no profiles/pmc_{config}.json"
     try:
-        return json.loads(p.read_text())
+        pmc = json.loads(p.read_text())
     except (OSError, ValueError):
-        return None
+        return None, f"unreadable profiles/pmc_{config}.json"
+    if pmc.get("lib_sha256") != lib_sha256():
+        return None, f"profiles/pmc_{config}.json was measured on another build of libfec_hip.so"
+    return pmc, f"profiles/pmc_{config}.json (rocprofv3 PMC on this build, lib_sha256 {pmc['lib_sha256'][:16]})"
 
 
 # ----------------------------------------------------------------------------- main
@@ -512,6 +527,9 @@ def main() -> int:
         dec_bytes = decode_algorithmic_bytes(masks_h, k, r, P)
         masks = torch.from_numpy(masks_h.view(np.int64)).to("cuda")
         ctx.decode_prepare(k, r)
+        if cfg.get("loss"):
+            # the receiver knows its loss profile: share of groups that lose a data shard
+            ctx.decode_loss_hint(1.0 - (1.0 - cfg["loss"]) ** k)
     torch.cuda.synchronize()
 
     verified = None
@@ -585,13 +603,35 @@ def main() -> int:
         kernels["decode"] = {"ms": round(dec_ms, 4), "algorithmic_bytes": dec_bytes,
                              "achieved_GBps": round(dec_gbs, 1),
                              "payload_GiBps": round(k * P * G / (dec_ms * 1e-3) / 2**30, 2)}
+    # Each kernel alone, back to back (decode is idempotent on rebuilt data): its own time,
+    # without the write-back of the other kernel's output still draining from the caches
+    # when it starts (which the in-step times above include).
+    reps = max(5, args.steps // 4)
+    iso = {}
+    for name in kernels:
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+        evs[0].record(stream)
+        for i in range(reps):
+            if name == "encode":
+                ctx.encode_dev(data, G, k, r, P, parity, stream=sp)
+            else:
+                ctx.decode_dev(data, parity, masks, G, k, r, P, None, stream=sp)
+            evs[i + 1].record(stream)
+        torch.cuda.synchronize()
+        ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(reps))[reps // 2]
+        iso[name] = {"ms_median": round(ms, 4),
+                     "achieved_GBps": round(kernels[name]["algorithmic_bytes"] / (ms * 1e-3) / 1e9, 1)}
+    for name in kernels:
+        kernels[name]["isolated"] = iso[name]
     dom = max(kernels, key=lambda n: kernels[n]["ms"])
-    pmc = load_pmc_traffic(args.config) or {}
+    pmc, pmc_note = load_pmc_traffic(args.config)
+    pmc = pmc or {}
     roofline = {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["achieved_GBps"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(kernels[dom]["achieved_GBps"] / HBM_PEAK_GBS, 4),
                 "traffic": pmc.get(dom, {}).get("hbm_bytes_per_launch"),
                 "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes"],
+                "traffic_source": pmc_note,
                 "timing": "torch.cuda.Event on the launch stream, averaged over the timed steps"}
 
     e2e = None

@@ -101,6 +101,14 @@ int fec_decode_batch_rs_dev(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* 
  * then 0.  FEC_ERR_RANGE if k + r > 64. */
 int fec_decode_prepare(FECEncoderCtx* ctx, uint32_t k, uint32_t r, uint64_t* bytes_out);
 
+/* Expected share (0..1) of groups that lost data shards in this context's device-resident
+ * decode calls, e.g. 1 - (1 - p)^k for iid loss p (the receiver knows its network profile;
+ * satellite p = 0.01, k = 10: ~0.10).  Below 0.25 the decode checks several groups per
+ * wave instead of dispatching one wave per group, which saves the waves that would find
+ * nothing to do; results are identical either way.  share < 0 or > 1: unknown (default,
+ * treated as dense loss).  The host-pointer calls measure the share from the masks. */
+int fec_decode_loss_hint(FECEncoderCtx* ctx, double share);
+
 /* ---- utilities for benchmarks and tests ---- */
 /* Fill d_dst with the counter-based splitmix64 stream (byte i of the stream at
  * byte_offset + i), asynchronously on stream. */

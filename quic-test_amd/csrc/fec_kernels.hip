@@ -470,25 +470,21 @@ __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, co
 // byte, colex ranks of the erased data set and of the parity rows used, record offset,
 // exactly as `classify` does — so no classify launch (and no rec_off round trip through
 // HBM) precedes it.  One launch per decode call instead of two.
-template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false, bool INLINE = DIRECT>
-__global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ data,
-                                                    const uint8_t* __restrict__ parity,
-                                                    const uint32_t* __restrict__ rec_off,
-                                                    const uint8_t* __restrict__ codebook,
-                                                    uint64_t groups, uint32_t P, uint32_t r, uint32_t m0,
-                                                    uint8_t* __restrict__ out, uint32_t never, uint32_t swz,
-                                                    const uint64_t* __restrict__ masks, RankMeta rm,
-                                                    uint8_t* __restrict__ status) {
-  static_assert(!INLINE || (DIRECT && MAXE <= 3), "inline classify: mask-addressed forms with r <= 3");
-  extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];  // see encode_v16
-  if (never) occupancy_lds[threadIdx.x] = 0;
+//
+// SCAN > 0 (mask-addressed inline forms): one wave per SCAN consecutive groups (see the
+// kernel).
+//
+// One group of decode_fused (below): `m` is the group's erasure mask (DIRECT forms; wave-
+// uniform), `lane` the lane in the wave.
+template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT, bool INLINE>
+__device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t lane, const uint8_t* __restrict__ data,
+                                            const uint8_t* __restrict__ parity,
+                                            const uint32_t* __restrict__ rec_off,
+                                            const uint8_t* __restrict__ codebook, uint32_t P, uint32_t r,
+                                            uint32_t m0, uint8_t* __restrict__ out, const RankMeta& rm,
+                                            uint8_t* __restrict__ status) {
   constexpr int NW = 4 * NM + NT;  // dwords per lane and survivor
-  const uint64_t gw = static_cast<uint64_t>(swz ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * 4u +
-                      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
-  if (gw >= groups) return;
-  const uint32_t lane = threadIdx.x & 63u;
   constexpr uint64_t kmask = (1ull << K) - 1;
-  const uint64_t m = DIRECT ? masks[gw] : 0;
   uint64_t rec_byte_off;
   if constexpr (INLINE) {
     uint64_t dm = m & kmask;
@@ -737,6 +733,57 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
 #pragma unroll
   for (int m = 0; m < MAXE; ++m)
     if (m0 + m < e) store(og + erased(m0 + m) * static_cast<uint64_t>(P), acc[m]);
+}
+
+template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false, bool INLINE = DIRECT, int SCAN = 0>
+__global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ data,
+                                                    const uint8_t* __restrict__ parity,
+                                                    const uint32_t* __restrict__ rec_off,
+                                                    const uint8_t* __restrict__ codebook,
+                                                    uint64_t groups, uint32_t P, uint32_t r, uint32_t m0,
+                                                    uint8_t* __restrict__ out, uint32_t never, uint32_t swz,
+                                                    const uint64_t* __restrict__ masks, RankMeta rm,
+                                                    uint8_t* __restrict__ status) {
+  static_assert(!INLINE || (DIRECT && MAXE <= 3), "inline classify: mask-addressed forms with r <= 3");
+  static_assert(SCAN == 0 || (DIRECT && INLINE && SCAN <= 64), "scan: mask-addressed inline forms, <= 64 groups");
+  extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];  // see encode_v16
+  if (never) occupancy_lds[threadIdx.x] = 0;
+  const uint64_t wv = static_cast<uint64_t>(swz ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * 4u +
+                      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+  const uint32_t lane = threadIdx.x & 63u;
+  if constexpr (SCAN == 0) {
+    if (wv >= groups) return;
+    const uint64_t m = DIRECT ? masks[wv] : 0;
+    fused_group<K, MAXE, POL, NM, NT, DIRECT, INLINE>(wv, m, lane, data, parity, rec_off, codebook, P, r, m0, out, rm,
+                                                      status);
+  } else {
+    // SCAN groups per wave: lanes 0..SCAN-1 read the masks with one vector load and write
+    // the status bytes; the groups with lost, recoverable data shards (a ballot) are then
+    // rebuilt one after another by the whole wave.  Sparse loss (C5: ~10% of groups) costs
+    // one wave per SCAN groups instead of one per group.
+    const uint64_t g0 = wv * SCAN;
+    if (g0 >= groups) return;
+    uint64_t mv = 0;
+    bool need = false;
+    if (lane < static_cast<uint32_t>(SCAN) && g0 + lane < groups) {
+      mv = masks[g0 + lane];
+      constexpr uint64_t kmask = (1ull << K) - 1;
+      const uint32_t ne = static_cast<uint32_t>(__popcll(mv & kmask));
+      const bool bad = ne > r - static_cast<uint32_t>(__popcll((mv >> K) & ((1ull << r) - 1)));
+      if (status != nullptr) status[g0 + lane] = bad ? 1 : 0;
+      need = ne > 0 && !bad;
+    }
+    uint64_t work = __ballot(need);
+    while (work) {
+      const uint32_t b = static_cast<uint32_t>(__builtin_ctzll(work));
+      work &= work - 1;
+      const uint64_t m = (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(mv >> 32), b)) << 32) |
+                         __builtin_amdgcn_readlane(static_cast<uint32_t>(mv), b);
+      fused_group<K, MAXE, POL, NM, NT, DIRECT, INLINE>(g0 + b, m, lane, data, parity, rec_off, codebook, P, r, m0,
+                                                        out, rm, nullptr);
+    }
+  }
+
 }
 
 // One wave per group, so the record is wave-uniform (SGPRs).  A packet is covered by
@@ -1214,8 +1261,9 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
   return hipSuccess;
 }
 
-template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false, bool INLINE = DIRECT>
+template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false, bool INLINE = DIRECT, int SCAN = 0>
 hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
+  constexpr uint64_t kGroupsPerBlock = 4u * (SCAN > 0 ? SCAN : 1);
   const uint32_t passes = (a.r + MAXE - 1) / MAXE;
   const uint32_t smem = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_DECODE_WAVES", kDecodeWavesPerCU), 4);
   RankMeta rm{};
@@ -1226,12 +1274,12 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
   }
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t m0 = p * MAXE;
-    const uint64_t blocks = (a.groups + 3) / 4;
+    const uint64_t blocks = (a.groups + kGroupsPerBlock - 1) / kGroupsPerBlock;
     for (uint64_t b0 = 0; b0 < blocks; b0 += kMaxWaveBlocks) {
       const uint64_t bn = (blocks - b0 < kMaxWaveBlocks) ? blocks - b0 : kMaxWaveBlocks;
-      const uint64_t g0 = b0 * 4;
-      const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
-      hipLaunchKernelGGL((decode_fused<K, MAXE, POL, NM, NT, DIRECT, INLINE>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
+      const uint64_t g0 = b0 * kGroupsPerBlock;
+      const uint64_t gn = (a.groups - g0 < bn * kGroupsPerBlock) ? a.groups - g0 : bn * kGroupsPerBlock;
+      hipLaunchKernelGGL((decode_fused<K, MAXE, POL, NM, NT, DIRECT, INLINE, SCAN>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                          a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
                          a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u,
@@ -1262,6 +1310,14 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, b
 #define QFEC_FUSED_D(KK, RR, NMM, NTT)                                                        \
   if (direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                             \
     return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true>(a, s);
+  // k=10 r=3 (the BASELINE shape) also has the scan form, for sparse loss (DecodeLaunch::scan)
+#define QFEC_FUSED_DS(KK, RR, NMM, NTT)                                                       \
+  if (direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT) {                           \
+    if (dry) return hipSuccess;                                                               \
+    if (a.scan == kDecodeScanGroups)                                                          \
+      return run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true, true, kDecodeScanGroups>(a, s); \
+    return run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true>(a, s);                \
+  }
 #define QFEC_FUSED_R(KK, RR, NMM, NTT)                                                        \
   if (!direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                            \
     return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore, NMM, NTT, false>(a, s);
@@ -1271,12 +1327,13 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, b
 #define QFEC_FUSED_P(M, KK, RR)                                                               \
   M(KK, RR, 0, 2) M(KK, RR, 0, 3) M(KK, RR, 0, 4) M(KK, RR, 1, 0) M(KK, RR, 1, 1)            \
   M(KK, RR, 1, 2) M(KK, RR, 1, 3) M(KK, RR, 1, 4)
-  QFEC_FUSED_P(QFEC_FUSED_D, 10, 3)
+  QFEC_FUSED_P(QFEC_FUSED_DS, 10, 3)
   QFEC_FUSED_R(10, 3, 1, 1)
   QFEC_FUSED_P(QFEC_FUSED_L, 20, 5)
   QFEC_FUSED_P(QFEC_FUSED_D, 10, 1)
   QFEC_FUSED_P(QFEC_FUSED_D, 4, 2)
 #undef QFEC_FUSED_P
+#undef QFEC_FUSED_DS
 #undef QFEC_FUSED_L
 #undef QFEC_FUSED_R
 #undef QFEC_FUSED_D

@@ -80,7 +80,17 @@ struct DecodeLaunch {
   int waves_per_cu = 0;      // occupancy cap of the decode kernel (0 = tuned default)
   bool rec_ready = false;    // rec_off already filled by the host (sparse plan): no classify
   int xcd_swizzle = -1;      // XCD-aware group order: -1 tuned default, 0 off, 1 on
+  // Groups per wave of the mask-addressed decode (kDecodeScanGroups or 1).  One wave per
+  // group is best when most groups lost data (C3: 5.35 TB/s vs 4.92 at 8 per wave); when few
+  // did (C5, iid 1% loss: ~10% of groups) 8 per wave saves the dispatch and mask-load latency
+  // of the waves that find nothing to do (0.257 -> 0.243 ms per 1M groups,
+  // profiles/r02_probe_decode_scan.txt).  The host paths that know the masks pick it.
+  uint32_t scan = 1;
 };
+
+constexpr uint32_t kDecodeScanGroups = 8;
+// Share of groups needing a rebuild below which the host paths use the scan form.
+constexpr double kDecodeScanMaxShare = 0.25;
 
 constexpr int kDecodeFusedXcdSwizzle = 1;  // tuned per kernel (fec_kernels.hip decode_swizzle)
 constexpr int kDecodeWaveXcdSwizzle = 1;

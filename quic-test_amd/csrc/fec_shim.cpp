@@ -274,6 +274,9 @@ struct FECEncoderCtx {
   // thread-local fec_hip_last_error.  Own lock: readable while a call holds `mu`.
   std::mutex err_mu;
   std::string last_error;
+  // fec_decode_loss_hint: expected share of groups with lost data in device-resident decode
+  // calls (< 0: unknown, treated as dense).
+  double decode_need_share = -1.0;
 
   ~FECEncoderCtx() {
     DeviceGuard g(device);
@@ -460,7 +463,7 @@ struct StreamScratch {
 int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
                       const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
                       uint8_t* d_status, hipStream_t s, DevBuf* rec = nullptr,
-                      uint8_t* d_out = nullptr) {
+                      uint8_t* d_out = nullptr, double need_share = -1.0) {
   DecodePlan* plan = nullptr;
   int rc = get_decode_plan(ctx, k, r, &plan);
   if (rc != FEC_OK) return rc;
@@ -484,6 +487,12 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   a.r = r;
   a.P = P;
   a.rec_ready = !plan->dense;
+  // Groups per wave of the mask-addressed form: the scan form when the caller knows that
+  // few groups need a rebuild (need_share, from a host scan of the masks); device-resident
+  // callers get one wave per group unless QUICFEC_DECODE_SCAN asks otherwise (tuning).
+  if (need_share < 0.0) need_share = ctx->decode_need_share;
+  if (need_share >= 0.0 && need_share < qfec::kDecodeScanMaxShare) a.scan = qfec::kDecodeScanGroups;
+  if (const char* v = std::getenv("QUICFEC_DECODE_SCAN")) a.scan = static_cast<uint32_t>(std::atoi(v));
   // Workspace: the caller's slot buffer (pipeline slots: private stream, calls serialised
   // by the context lock), else one private to this call.
   StreamScratch scratch;
@@ -711,7 +720,8 @@ int encode_host_zero_copy(FECEncoderCtx* ctx, const uint8_t* data, Mem dmem, voi
 // Small host-resident decode, zero-copy: survivors are read and rebuilt shards written in
 // place through PCIe.  Statuses come from the caller's host scan.  Caller holds ctx->mu.
 int decode_host_zero_copy(FECEncoderCtx* ctx, uint8_t* data, Mem dmem, void* ddev, const uint8_t* parity, Mem pmem,
-                          void* pdev, const uint64_t* masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P) {
+                          void* pdev, const uint64_t* masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
+                          double need_share) {
   const uint64_t in_g = uint64_t(k) * P;
   uint8_t *d = nullptr, *p = nullptr;
   bool d_staged = false, p_staged = false;
@@ -720,7 +730,8 @@ int decode_host_zero_copy(FECEncoderCtx* ctx, uint8_t* data, Mem dmem, void* dde
   if (rc != FEC_OK) return rc;
   QFEC_HIP(ctx->z_aux.ensure(G * 8));
   std::memcpy(ctx->z_aux.ptr, masks, G * 8);
-  rc = decode_dev_locked(ctx, d, p, ctx->z_aux.dev_as<uint64_t>(), G, k, r, P, nullptr, ctx->stream);
+  rc = decode_dev_locked(ctx, d, p, ctx->z_aux.dev_as<uint64_t>(), G, k, r, P, nullptr, ctx->stream, nullptr,
+                         nullptr, need_share);
   if (rc != FEC_OK) return rc;
   QFEC_HIP(wait_stream(ctx->stream));
   if (d_staged) {  // only erased data packets changed (unrecoverable groups: untouched bytes)
@@ -1215,7 +1226,8 @@ static int fec_decode_batch_rs_impl(FECEncoderCtx* ctx, uint8_t* data, const uin
         st[g] = (e > 0 && e > r - static_cast<uint32_t>(__builtin_popcountll((m >> k) & rmask))) ? 1 : 0;
       }
       if (!need.empty())
-        rc = small ? decode_host_zero_copy(ctx, data, dmem, ddev, parity, pmem, pdev, masks, G, k, r, P)
+        rc = small ? decode_host_zero_copy(ctx, data, dmem, ddev, parity, pmem, pdev, masks, G, k, r, P,
+                                           double(need.size()) / double(G))
                    : decode_host_compacted(ctx, data, parity, masks, need, k, r, P);
     } else {
       rc = decode_host_pipelined(ctx, data, parity, masks, G, k, r, P, st);
@@ -1339,6 +1351,13 @@ QFEC_EXPORT int fec_fill_random_dev(FECEncoderCtx* ctx, uint8_t* d_dst, uint64_t
                                     uint64_t byte_offset, void* stream) {
   g_last_error.clear();
   return record_ctx_error(ctx, fec_fill_random_dev_impl(ctx, d_dst, nbytes, seed, byte_offset, stream));
+}
+
+QFEC_EXPORT int fec_decode_loss_hint(FECEncoderCtx* ctx, double share) {
+  if (!ctx) return FEC_ERR_NULL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->decode_need_share = share >= 0.0 && share <= 1.0 ? share : -1.0;
+  return FEC_OK;
 }
 
 QFEC_EXPORT int fec_synchronize(FECEncoderCtx* ctx) {

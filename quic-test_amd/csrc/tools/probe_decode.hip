@@ -210,6 +210,14 @@ int main(int argc, char** argv) {
   } else if (k == 10 && r == 3 && P == 2048) {
     PSET(2, 0)
   }
+  // SCAN groups per wave (mask-addressed inline form): sparse loss without a wave per group
+#define PSCAN(T)                                                                                 \
+  vars.push_back({"scan" #T, kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {               \
+                    return run_decode_fused<10, 3, kNtStore | kNtLoad, 1, 1, true, true, T>(a, nullptr); \
+                  }});
+  if (k == 10 && r == 3 && P == 1200) {
+    PSCAN(2) PSCAN(4) PSCAN(8) PSCAN(16) PSCAN(32) PSCAN(64)
+  }
   // record-addressed fused form with the coefficient tables staged through LDS (kLdsTabs)
 #define PLDS(KK, RR, NMM, NTT)                                                                    \
   if (k == KK && r == RR && P / 1024 == NMM && (P % 1024 + 255) / 256 == NTT) {                   \

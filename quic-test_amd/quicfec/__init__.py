@@ -41,7 +41,7 @@ HIP_SYMBOLS = (
     "fec_hip_device_count", "fec_hip_last_error", "fec_ctx_last_error", "fec_encoder_new_device", "fec_encoder_device",
     "fec_hip_version", "fec_parity_matrix", "fec_encode_batch_rs", "fec_decode_batch_rs",
     "fec_encode_batch_rs_dev", "fec_decode_batch_rs_dev", "fec_decode_prepare",
-    "fec_fill_random_dev", "fec_synchronize",
+    "fec_fill_random_dev", "fec_synchronize", "fec_decode_loss_hint",
     "fec_group_new", "fec_group_free", "fec_group_size", "fec_group_context",
     "fec_group_encode_batch_rs", "fec_group_decode_batch_rs",
 )
@@ -108,6 +108,7 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
         "fec_decode_prepare": (_int, [_vp, _u32, _u32, ctypes.POINTER(_u64)]),
         "fec_fill_random_dev": (_int, [_vp, _vp, _u64, _u64, _u64, _vp]),
         "fec_synchronize": (_int, [_vp]),
+        "fec_decode_loss_hint": (_int, [_vp, _dbl]),
         "fec_group_new": (_vp, [ctypes.POINTER(_int), _int]),
         "fec_group_free": (None, [_vp]),
         "fec_group_size": (_int, [_vp]),
@@ -250,6 +251,10 @@ class Context:
                         stream: Optional[int] = None) -> None:
         _check(self.lib.fec_fill_random_dev(self.handle, _ptr(d_dst), nbytes, seed, byte_offset, stream),
                "fec_fill_random_dev")
+
+    def decode_loss_hint(self, share: float) -> None:
+        """Expected share of groups with lost data in device-resident decodes (< 0: unknown)."""
+        _check(self.lib.fec_decode_loss_hint(self.handle, share), "fec_decode_loss_hint")
 
     def synchronize(self) -> None:
         _check(self.lib.fec_synchronize(self.handle), "fec_synchronize")

@@ -42,8 +42,12 @@ def main():
     out = Path(sys.argv[4]) if len(sys.argv) > 4 else Path(__file__).resolve().parents[1] / "profiles" / f"pmc_{config}.json"
     fetch = collect(fdir, "FETCH_SIZE")
     write = collect(wdir, "WRITE_SIZE")
+    import hashlib
+    lib = Path(__file__).resolve().parents[1] / "quic-test_amd" / "lib" / "libfec_hip.so"
     res = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes)",
-           "correction": "FETCH_SIZE x2 (gfx950 wide-stream read), KiB -> bytes"}
+           "correction": "FETCH_SIZE x2 (gfx950 wide-stream read), KiB -> bytes",
+           # bench.py uses these bytes only while the loaded library is this build
+           "lib_sha256": hashlib.sha256(lib.read_bytes()).hexdigest()}
     for name in set(fetch) | set(write):
         s = short(name)
         f = fetch.get(name, [])

@@ -602,3 +602,29 @@ def test_ctx_last_error_set_on_failure(gpu_ctx, quicfec_mod):
     t.start()
     t.join()
     assert "k=200 r=100" in seen[0]
+
+
+@pytest.mark.parametrize("loss,P", [(0.01, 1200), (0.2, 1200), (0.01, 700), (0.05, 1400)])
+def test_device_decode_scan_form(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, loss, P):
+    """The mask-addressed decode with 8 groups per wave (DecodeLaunch::scan; host paths pick
+    it for sparse loss, QUICFEC_DECODE_SCAN forces it here): statuses of every group and the
+    rebuilt bytes equal the oracle's, with unrecoverable groups and a partial last wave."""
+    monkeypatch.setenv("QUICFEC_DECODE_SCAN", "8")
+    torch = torch_cuda
+    k, r, G = 10, 3, 20_011
+    data = oracle_mod.splitmix_bytes(G * k * P, SEED + 41 + P)
+    par = oracle_mod.rs_encode(data, G, k, r, P, nthreads=8)
+    rng = np.random.default_rng(int(loss * 1000) + P)
+    w = np.left_shift(np.uint64(1), np.arange(k + r, dtype=np.uint64))
+    masks = ((rng.random((G, k + r)) < loss) * w).sum(axis=1, dtype=np.uint64)
+    masks[rng.integers(0, G, size=7)] = np.uint64(0xF)          # 4 data shards lost: unrecoverable
+    broken = _poison(data, masks, G, k, P)
+    ref = broken.copy()
+    bad_exp, st_exp = oracle_mod.rs_decode(ref, par, masks, G, k, r, P, nthreads=8)
+    dd, dp, dm = _dev(torch, broken), _dev(torch, par), _dev(torch, masks.view(np.int64))
+    st = torch.full((G,), 0x55, dtype=torch.uint8, device="cuda")
+    gpu_ctx.decode_dev(dd, dp, dm, G, k, r, P, st)
+    gpu_ctx.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_exp)
+    assert int((st_exp != 0).sum()) == bad_exp
+    assert np.array_equal(dd.cpu().numpy(), ref)
