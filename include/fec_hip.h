@@ -40,6 +40,7 @@ extern "C" {
 #define FEC_ERR_RANGE (-3)     /* k, r, packet size or group count unsupported     */
 #define FEC_ERR_NODEV (-4)     /* no usable GPU                                   */
 #define FEC_ERR_NOMEM (-5)     /* device or pinned allocation failed              */
+#define FEC_ERR_AGAIN (-6)     /* fec_batcher_wait: not ready within the timeout   */
 
 /* Number of visible HIP devices (0 when none or the runtime is unusable). */
 int fec_hip_device_count(void);
@@ -141,6 +142,51 @@ int fec_group_decode_batch_rs(FECDeviceGroup* group, uint8_t* data, const uint8_
                               const uint64_t* erasure_masks, uint64_t num_groups, uint32_t k,
                               uint32_t r, uint32_t packet_size, uint8_t* status_out,
                               uint64_t* unrecoverable_out);
+
+/* ---- batcher: one process-wide batch for the groups of many streams ----
+ * The reference encodes one group per call (encoder_hybrid.go:115, one HybridFECEncoder per
+ * QUIC stream, client.go:783).  A batcher collects finished groups from every stream of the
+ * process and encodes them in one launch when max_groups are pending OR deadline_us have
+ * passed since the oldest pending group arrived (deadline_us = 0: as soon as the flusher is
+ * free; groups arriving meanwhile share the next launch).  A repair therefore waits at most
+ * deadline_us plus one encode.  Groups are k slots of slot_bytes (shorter packets
+ * zero-padded, a group of count < k packets has zero slots count..k-1, as encoder.go:133-143
+ * XORs only the packets present); each group's r repair payloads are as long as its longest
+ * packet (the reference's repair length, encoder_hybrid.go:91-98).  Memory: `slabs` (>= 2)
+ * page-locked slabs of max_groups groups; submitters wait while every slab is in use.
+ * Thread-safe; one flusher thread per batcher.  NULL on failure (fec_batcher_last_error). */
+typedef struct FECBatcher FECBatcher;
+
+typedef struct {
+  uint64_t groups;            /* groups encoded                                    */
+  uint64_t batches;           /* launches                                          */
+  uint64_t full_flushes;      /* batches closed because max_groups were pending    */
+  uint64_t deadline_flushes;  /* batches closed by the deadline (or fec_batcher_flush) */
+  uint64_t max_batch;         /* largest batch                                     */
+} FECBatcherStats;
+
+FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint32_t slot_bytes, uint32_t max_groups,
+                            uint32_t deadline_us, uint32_t slabs);
+/* Encodes what is pending, then frees.  No call may be in flight on the batcher. */
+void fec_batcher_free(FECBatcher* b);
+
+/* One group: `count` (1..k) packets back to back in `packed`, packet j `lens[j]` bytes
+ * (<= slot_bytes; not all empty).  Returns the group's ticket (>= 0) or a negative code. */
+int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, const uint32_t* lens, uint32_t count);
+
+/* Waits for a ticket's batch (timeout_us < 0: no limit; 0: poll) and copies its r repair
+ * payloads to out (row i at out + i*out_stride; NULL: discard).  Returns the payload length,
+ * FEC_ERR_AGAIN on timeout (the ticket stays valid), or another negative code.  Each ticket
+ * can be collected once; uncollected results are kept until fec_batcher_free. */
+int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int64_t timeout_us);
+
+/* Closes the pending batch now (e.g. at the end of a stream) instead of at its deadline. */
+int fec_batcher_flush(FECBatcher* b);
+
+int fec_batcher_stats(FECBatcher* b, FECBatcherStats* out);
+
+/* Message of the calling thread's last failing fec_batcher_* call. */
+const char* fec_batcher_last_error(void);
 
 #ifdef __cplusplus
 }

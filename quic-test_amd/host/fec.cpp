@@ -484,6 +484,168 @@ int64_t RecoverBatchRS(Bytes& data, const Bytes& parity, const std::vector<uint6
   return static_cast<int64_t>(bad);
 }
 
+// ===================================================================== batcher (new)
+std::shared_ptr<SharedFECBatcher> SharedFECBatcher::New(int k, int r, int slotBytes, int maxGroups, int deadlineUs,
+                                                         int device, int slabs) {
+  if (k < 1 || r < 1 || k + r > 256 || k > FECDecoder::kMaxPacketCount || slotBytes < 1 || maxGroups < 1 ||
+      deadlineUs < 0 || slabs < 0)
+    return nullptr;
+  std::shared_ptr<SharedFECBatcher> b(new SharedFECBatcher());
+  b->b_ = fec_batcher_new(device, static_cast<uint32_t>(k), static_cast<uint32_t>(r), static_cast<uint32_t>(slotBytes),
+                          static_cast<uint32_t>(maxGroups), static_cast<uint32_t>(deadlineUs),
+                          static_cast<uint32_t>(slabs));
+  if (!b->b_) return nullptr;
+  b->k_ = k;
+  b->r_ = r;
+  b->slot_ = slotBytes;
+  return b;
+}
+
+SharedFECBatcher::~SharedFECBatcher() {
+  if (b_) fec_batcher_free(b_);
+}
+
+void SharedFECBatcher::Flush() { fec_batcher_flush(b_); }
+
+std::vector<uint64_t> SharedFECBatcher::Stats() {
+  FECBatcherStats st{};
+  fec_batcher_stats(b_, &st);
+  return {st.groups, st.batches, st.full_flushes, st.deadline_flushes, st.max_batch};
+}
+
+BatchedFECEncoder::BatchedFECEncoder(std::shared_ptr<SharedFECBatcher> batcher) : b_(std::move(batcher)) {
+  packets_.reserve(b_ ? b_->k() : 10);
+}
+
+Error BatchedFECEncoder::submitLocked(Ticket* t) {
+  if (!b_) return errorf("GPU FEC engine unavailable");
+  if (packets_.empty()) return errorf("no packets in group");  // encoder_hybrid.go:84-86
+  packed_.clear();
+  lens_.clear();
+  size_t maxSize = 0;
+  for (const auto& p : packets_) {
+    packed_.insert(packed_.end(), p.begin(), p.end());
+    lens_.push_back(static_cast<uint32_t>(p.size()));
+    maxSize = std::max(maxSize, p.size());
+  }
+  // encoder_hybrid.go:95-97.  The reference keeps the packets after this error (every later
+  // AddPacket of the stream then fails the same way); the group is dropped here instead.
+  if (maxSize == 0) {
+    packets_.clear();
+    return errorf("empty packets");
+  }
+  const int64_t tk = fec_batcher_submit(b_->raw(), packed_.data(), lens_.data(), static_cast<uint32_t>(lens_.size()));
+  if (tk < 0) return errorf("fec_batcher_submit failed with code %lld: %s", static_cast<long long>(tk), fec_batcher_last_error());
+  t->ticket = tk;
+  t->groupID = groupID_++;
+  t->count = static_cast<int>(packets_.size());
+  packets_.clear();
+  return {};
+}
+
+Error BatchedFECEncoder::collect(const Ticket& t, int64_t timeoutUs, std::vector<Bytes>* rows, bool* ready) {
+  const int r = b_->r();
+  rowbuf_.resize(size_t(r) * b_->slot());
+  const int rc = fec_batcher_wait(b_->raw(), t.ticket, rowbuf_.data(), static_cast<uint32_t>(b_->slot()), timeoutUs);
+  *ready = rc != FEC_ERR_AGAIN;
+  if (rc == FEC_ERR_AGAIN) return {};
+  if (rc < 0) return errorf("C++ encoding failed: %s", fec_batcher_last_error());
+  const size_t len = static_cast<size_t>(rc);
+  for (int row = 0; row < r; ++row) {
+    RSRepairHeader h;
+    h.groupID = t.groupID;
+    h.count = t.count;
+    h.row = row;
+    h.r = r;
+    h.k = b_->k();
+    // row 0: encoder_hybrid.go:175-192's packet (FE C0 | groupID | count | payload)
+    rows->push_back(MakeRepairPacket(h, rowbuf_.data() + size_t(row) * b_->slot(), len));
+    metrics_.RedundancyPackets++;
+    metrics_.RedundancyBytes += static_cast<int64_t>(rows->back().size());
+  }
+  // encoder_hybrid.go:124-127 (PacketsEncoded counts the group size)
+  metrics_.GroupsProcessed++;
+  metrics_.PacketsEncoded += b_->k();
+  return {};
+}
+
+AddPacketResult BatchedFECEncoder::AddPacket(const uint8_t* packet, size_t len, uint64_t packetID) {
+  (void)packetID;
+  std::lock_guard<std::mutex> lk(mu_);
+  AddPacketResult res;
+  packets_.emplace_back(packet, packet + len);  // copied, as encoder_hybrid.go:64-65
+  if (static_cast<int>(packets_.size()) < (b_ ? b_->k() : 10)) return res;
+  Ticket t;
+  if ((res.err = submitLocked(&t))) return res;
+  std::vector<Bytes> rows;
+  bool ready = false;
+  if ((res.err = collect(t, -1, &rows, &ready))) return res;
+  res.needsRedundancy = true;
+  res.redundancy = std::move(rows[0]);
+  res.extra.assign(std::make_move_iterator(rows.begin() + 1), std::make_move_iterator(rows.end()));
+  return res;
+}
+
+Error BatchedFECEncoder::AddPacketAsync(const uint8_t* packet, size_t len, uint64_t packetID) {
+  (void)packetID;
+  std::lock_guard<std::mutex> lk(mu_);
+  packets_.emplace_back(packet, packet + len);
+  if (static_cast<int>(packets_.size()) < (b_ ? b_->k() : 10)) return {};
+  Ticket t;
+  if (Error e = submitLocked(&t)) return e;
+  outstanding_.push_back(t);
+  return {};
+}
+
+Error BatchedFECEncoder::Poll(std::vector<Bytes>* out, int64_t timeoutUs) {
+  std::lock_guard<std::mutex> lk(mu_);
+  bool first = true;
+  while (!outstanding_.empty()) {
+    bool ready = false;
+    const int64_t wait = timeoutUs < 0 ? -1 : (first ? timeoutUs : 0);
+    if (Error e = collect(outstanding_.front(), wait, out, &ready)) {
+      outstanding_.pop_front();
+      return e;
+    }
+    if (!ready) break;
+    outstanding_.pop_front();
+    first = false;
+  }
+  return {};
+}
+
+AddPacketResult BatchedFECEncoder::Flush() {
+  std::lock_guard<std::mutex> lk(mu_);
+  AddPacketResult res;
+  if (packets_.empty()) return res;
+  Ticket t;
+  if ((res.err = submitLocked(&t))) return res;
+  b_->Flush();
+  std::vector<Bytes> rows;
+  bool ready = false;
+  if ((res.err = collect(t, -1, &rows, &ready))) return res;
+  res.needsRedundancy = true;
+  res.redundancy = std::move(rows[0]);
+  res.extra.assign(std::make_move_iterator(rows.begin() + 1), std::make_move_iterator(rows.end()));
+  return res;
+}
+
+Error BatchedFECEncoder::FlushAsync() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!packets_.empty()) {
+    Ticket t;
+    if (Error e = submitLocked(&t)) return e;
+    outstanding_.push_back(t);
+  }
+  if (b_) b_->Flush();
+  return {};
+}
+
+FECMetrics BatchedFECEncoder::GetMetrics() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return metrics_;
+}
+
 // ===================================================================== r > 1 (new)
 bool ParseRepairHeader(const uint8_t* b, size_t len, RSRepairHeader* h, const uint8_t** payload, size_t* plen) {
   if (len < kRepairHeaderLen || b[0] != 0xFE || (b[1] != 0xC0 && b[1] != 0xC1)) return false;

@@ -20,6 +20,7 @@
 
 #include <chrono>
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -28,6 +29,7 @@
 #include <vector>
 
 struct FECEncoderCtx;
+struct FECBatcher;
 
 namespace quicfec {
 
@@ -90,6 +92,7 @@ struct AddPacketResult {
   bool needsRedundancy = false;
   Bytes redundancy;
   Error err;
+  std::vector<Bytes> extra;  // BatchedFECEncoder with r > 1: rows 1..r-1 (FE C1 packets)
 };
 
 // encoder_hybrid.go:9-237
@@ -279,6 +282,79 @@ class RSBatchEncoder {
   std::vector<uint32_t> count_, maxLen_;  // per group of the open batch
   int open_ = 0;                          // groups started in the open batch
   uint64_t groupID_ = 0;
+  std::mutex mu_;
+  FECMetrics metrics_;
+};
+
+// ===================================================================== batcher (new)
+// SURVEY.md §8(f) item 1.  The reference runs one HybridFECEncoder per QUIC stream and
+// encodes one group per call (encoder_hybrid.go:115).  Here every stream's encoder hands its
+// finished groups to one process-wide SharedFECBatcher (fec_batcher_*, include/fec_hip.h),
+// which encodes them together when maxGroups are pending or deadlineUs after the oldest
+// pending group, whichever comes first: a repair is at most deadlineUs + one encode late.
+class SharedFECBatcher {
+ public:
+  // nullptr when the GPU library cannot be initialised or the shape is invalid.
+  static std::shared_ptr<SharedFECBatcher> New(int k, int r, int slotBytes = 1500, int maxGroups = 4096,
+                                               int deadlineUs = 1000, int device = -1, int slabs = 3);
+  ~SharedFECBatcher();
+  SharedFECBatcher(const SharedFECBatcher&) = delete;
+  SharedFECBatcher& operator=(const SharedFECBatcher&) = delete;
+  FECBatcher* raw() const { return b_; }
+  int k() const { return k_; }
+  int r() const { return r_; }
+  int slot() const { return slot_; }
+  void Flush();
+  // groups, batches, full_flushes, deadline_flushes, max_batch
+  std::vector<uint64_t> Stats();
+
+ private:
+  SharedFECBatcher() = default;
+  FECBatcher* b_ = nullptr;
+  int k_ = 0, r_ = 0, slot_ = 0;
+};
+
+// One stream's encoder on a shared batcher: HybridFECEncoder's API, groups of k packets,
+// and its wire bytes -- the row-0 repair packet (FE C0 | groupID | count | XOR payload) is
+// byte-identical to HybridFECEncoder's for the same packets -- plus rows 1..r-1 as FE C1
+// packets (AddPacketResult::extra) when the batcher's r > 1.
+class BatchedFECEncoder {
+ public:
+  explicit BatchedFECEncoder(std::shared_ptr<SharedFECBatcher> batcher);
+  // Synchronous, like HybridFECEncoder::AddPacket: the k-th packet submits the group and
+  // waits for its batch (at most the deadline plus one encode).
+  AddPacketResult AddPacket(const uint8_t* packet, size_t len, uint64_t packetID);
+  AddPacketResult AddPacket(const Bytes& p, uint64_t id) { return AddPacket(p.data(), p.size(), id); }
+  // Asynchronous: the k-th packet submits without waiting; Poll appends the repair packets
+  // of finished groups (in group order, row order) and waits up to timeoutUs for the oldest
+  // outstanding one (0: no wait, < 0: all of them).
+  Error AddPacketAsync(const uint8_t* packet, size_t len, uint64_t packetID);
+  Error Poll(std::vector<Bytes>* out, int64_t timeoutUs = 0);
+  size_t outstanding() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return outstanding_.size();
+  }
+  // The partial group (count < k) now, synchronously, as HybridFECEncoder::Flush (its rows
+  // 1..r-1 in `extra`).  FlushAsync submits it without waiting and closes the batch now.
+  AddPacketResult Flush();
+  Error FlushAsync();
+  FECMetrics GetMetrics();
+
+ private:
+  struct Ticket {
+    int64_t ticket;
+    uint64_t groupID;
+    int count;
+  };
+  Error submitLocked(Ticket* t);
+  Error collect(const Ticket& t, int64_t timeoutUs, std::vector<Bytes>* rows, bool* ready);
+
+  std::shared_ptr<SharedFECBatcher> b_;
+  std::vector<Bytes> packets_;
+  uint64_t groupID_ = 0;
+  std::deque<Ticket> outstanding_;
+  Bytes packed_, rowbuf_;
+  std::vector<uint32_t> lens_;
   std::mutex mu_;
   FECMetrics metrics_;
 };
