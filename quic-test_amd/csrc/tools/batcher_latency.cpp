@@ -1,0 +1,231 @@
+// batcher_latency.cpp — repair delay and throughput of the shared batcher (fec_batcher_*,
+// host mirror BatchedFECEncoder) under the reference's call pattern, next to the one-group
+// GPU call and the CPU per-group cost.  Not part of the library; results in
+// profiles/r02_batcher_latency.jsonl.
+//
+// The reference: every QUIC stream adds packets at --rate per second (default 100,
+// main.go:32; client.go:1140-1143) and encodes one group per call on its 10th packet
+// (encoder_hybrid.go:71-73, :115).
+//
+//   batcher_latency paced <streams> <rate_pps> <seconds> <r> <deadline_us>
+//   batcher_latency saturate <streams> <seconds> <r> <deadline_us> <max_groups>
+//   batcher_latency cpu                  (per-group CPU cost of the comparators, 1 core)
+//   batcher_latency single <r> <calls>   (one group per synchronous call, no batcher)
+#include <sys/resource.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "fec.hpp"
+#include "fec_hip.h"
+
+extern "C" {
+void oracle_xor_avx2(const uint8_t* const*, size_t, size_t, uint8_t*);
+int oracle_rs_encode_fast(const uint8_t*, uint64_t, uint32_t, uint32_t, uint32_t, uint8_t*, int);
+void oracle_fill_splitmix(uint8_t*, uint64_t, uint64_t, uint64_t);
+}
+
+using namespace quicfec;
+using Clock = std::chrono::steady_clock;
+
+namespace {
+
+constexpr int kK = 10;
+constexpr int kP = 1200;
+
+double cpu_seconds() {
+  rusage u{};
+  getrusage(RUSAGE_SELF, &u);
+  return u.ru_utime.tv_sec + u.ru_stime.tv_sec + (u.ru_utime.tv_usec + u.ru_stime.tv_usec) * 1e-6;
+}
+
+std::vector<Bytes> packets(int n, uint64_t seed) {
+  std::vector<Bytes> v(n, Bytes(kP));
+  for (int i = 0; i < n; ++i) oracle_fill_splitmix(v[i].data(), kP, seed, uint64_t(i) * kP);
+  return v;
+}
+
+void print_lat(const char* mode, const std::string& cfg, std::vector<double>& us, double groups, double seconds,
+               double cpu_s, SharedFECBatcher* sb) {
+  std::sort(us.begin(), us.end());
+  auto pct = [&](double p) { return us.empty() ? 0.0 : us[std::min(us.size() - 1, size_t(p * us.size()))]; };
+  std::printf("{\"mode\": \"%s\", %s, \"groups\": %.0f, \"seconds\": %.3f, \"groups_per_s\": %.1f, "
+              "\"payload_GiBps\": %.4f, \"delay_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"max\": %.1f}, "
+              "\"cpu_us_per_group\": %.3f",
+              mode, cfg.c_str(), groups, seconds, groups / seconds, groups * kK * kP / seconds / (1u << 30), pct(0.5),
+              pct(0.9), pct(0.99), us.empty() ? 0.0 : us.back(), cpu_s / groups * 1e6);
+  if (sb) {
+    auto st = sb->Stats();
+    std::printf(", \"batches\": %llu, \"mean_batch\": %.2f, \"full_flushes\": %llu, \"deadline_flushes\": %llu, "
+                "\"max_batch\": %llu",
+                (unsigned long long)st[1], st[1] ? double(st[0]) / st[1] : 0.0, (unsigned long long)st[2],
+                (unsigned long long)st[3], (unsigned long long)st[4]);
+  }
+  std::printf("}\n");
+  std::fflush(stdout);
+}
+
+// Streams at a fixed packet rate, synchronous AddPacket (HybridFECEncoder's call shape):
+// delay = the 10th packet's AddPacket call, which returns the repair packet(s).
+int paced(int S, double rate, double seconds, int r, int deadline_us) {
+  auto sb = SharedFECBatcher::New(kK, r, kP, 4096, deadline_us);
+  if (!sb) return 2;
+  const auto pk = packets(kK, 0x5EED0A);
+  std::mutex mu;
+  std::vector<double> all;
+  std::atomic<long> groups{0}, errors{0};
+  const auto t0 = Clock::now() + std::chrono::milliseconds(50);
+  const double c0 = cpu_seconds();
+  std::vector<std::thread> th;
+  for (int s = 0; s < S; ++s)
+    th.emplace_back([&, s] {
+      BatchedFECEncoder be(sb);
+      std::vector<double> lat;
+      const double phase = double(s) / S / rate;  // streams spread over one packet interval
+      for (long i = 0;; ++i) {
+        const auto due = t0 + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(phase + i / rate));
+        if (due > t0 + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(seconds))) break;
+        std::this_thread::sleep_until(due);
+        const auto a = Clock::now();
+        AddPacketResult res = be.AddPacket(pk[i % kK], uint64_t(i));
+        if (!res.err.ok()) ++errors;
+        if (res.needsRedundancy) {
+          lat.push_back(std::chrono::duration<double, std::micro>(Clock::now() - a).count());
+          ++groups;
+        }
+      }
+      std::lock_guard<std::mutex> lk(mu);
+      all.insert(all.end(), lat.begin(), lat.end());
+    });
+  for (auto& t : th) t.join();
+  const double cpu = cpu_seconds() - c0;
+  char cfg[256];
+  std::snprintf(cfg, sizeof(cfg), "\"streams\": %d, \"rate_pps\": %.0f, \"r\": %d, \"deadline_us\": %d, \"errors\": %ld", S,
+                rate, r, deadline_us, errors.load());
+  print_lat("paced", cfg, all, double(groups), seconds, cpu, sb.get());
+  return errors ? 1 : 0;
+}
+
+// Every stream submits as fast as it can (async API, up to 256 groups outstanding each).
+int saturate(int S, double seconds, int r, int deadline_us, int max_groups) {
+  auto sb = SharedFECBatcher::New(kK, r, kP, max_groups, deadline_us, -1, 4);
+  if (!sb) return 2;
+  const auto pk = packets(kK, 0x5EED0B);
+  std::mutex mu;
+  std::vector<double> all;
+  std::atomic<long> groups{0}, errors{0};
+  const auto t_end = Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(seconds));
+  const auto t0 = Clock::now();
+  const double c0 = cpu_seconds();
+  std::vector<std::thread> th;
+  for (int s = 0; s < S; ++s)
+    th.emplace_back([&] {
+      BatchedFECEncoder be(sb);
+      std::vector<Clock::time_point> sub;  // submit time of each outstanding group, in order
+      size_t head = 0;
+      std::vector<double> lat;
+      std::vector<Bytes> out;
+      auto drain = [&](int64_t timeout) {
+        out.clear();
+        if (!be.Poll(&out, timeout).ok()) ++errors;
+        const auto now = Clock::now();
+        for (size_t n = out.size() / size_t(r); n > 0; --n, ++head) {
+          lat.push_back(std::chrono::duration<double, std::micro>(now - sub[head]).count());
+          ++groups;
+        }
+      };
+      while (Clock::now() < t_end) {
+        for (int j = 0; j < kK; ++j)
+          if (!be.AddPacketAsync(pk[j].data(), kP, 0).ok()) ++errors;
+        sub.push_back(Clock::now());
+        drain(sub.size() - head >= 256 ? 100000 : 0);
+      }
+      if (!be.FlushAsync().ok()) ++errors;
+      drain(-1);
+      std::lock_guard<std::mutex> lk(mu);
+      all.insert(all.end(), lat.begin(), lat.end());
+    });
+  for (auto& t : th) t.join();
+  const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
+  const double cpu = cpu_seconds() - c0;
+  char cfg[256];
+  std::snprintf(cfg, sizeof(cfg), "\"streams\": %d, \"r\": %d, \"deadline_us\": %d, \"max_groups\": %d, \"errors\": %ld", S,
+                r, deadline_us, max_groups, errors.load());
+  print_lat("saturate", cfg, all, double(groups), wall, cpu, sb.get());
+  return errors ? 1 : 0;
+}
+
+// The one-group call of the reference's pattern without a batcher (HybridFECEncoder ->
+// fec_encode_batch, one launch and synchronize per group), for comparison.
+int single(int calls) {
+  HybridFECEncoder h(0.1);
+  if (!h.UseCXX()) return 2;
+  const auto pk = packets(kK, 0x5EED0C);
+  std::vector<double> us;
+  const double c0 = cpu_seconds();
+  const auto t0 = Clock::now();
+  for (int c = 0; c < calls; ++c) {
+    for (int j = 0; j < kK - 1; ++j) h.AddPacket(pk[j], 0);
+    const auto a = Clock::now();
+    AddPacketResult res = h.AddPacket(pk[kK - 1], 0);
+    if (!res.needsRedundancy) return 1;
+    us.push_back(std::chrono::duration<double, std::micro>(Clock::now() - a).count());
+  }
+  const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
+  print_lat("single_group_call", "\"streams\": 1, \"r\": 1, \"api\": \"HybridFECEncoder -> fec_encode_batch\"", us, calls,
+            wall, cpu_seconds() - c0, nullptr);
+  return 0;
+}
+
+// One core: the reference's computation per group (AVX2 XOR, xor_packets_avx2 restated) and
+// the r = 3 code with GFNI (oracle fast form); 4096 groups of fresh data per pass.
+int cpu() {
+  const uint64_t G = 4096;
+  Bytes data(G * kK * kP), rep(G * 3 * kP);
+  oracle_fill_splitmix(data.data(), data.size(), 0x5EED0D, 0);
+  auto time_it = [&](auto&& fn) {
+    int reps = 0;
+    const auto t0 = Clock::now();
+    double s = 0;
+    do {
+      fn();
+      ++reps;
+      s = std::chrono::duration<double>(Clock::now() - t0).count();
+    } while (s < 1.0);
+    return s / (reps * double(G)) * 1e6;
+  };
+  const double xor_us = time_it([&] {
+    const uint8_t* p[kK];
+    for (uint64_t g = 0; g < G; ++g) {
+      for (int j = 0; j < kK; ++j) p[j] = data.data() + (g * kK + j) * kP;
+      oracle_xor_avx2(p, kK, kP, rep.data() + g * kP);
+    }
+  });
+  const double rs3_us = time_it([&] { oracle_rs_encode_fast(data.data(), G, kK, 3, kP, rep.data(), 1); });
+  std::printf("{\"mode\": \"cpu_one_core\", \"us_per_group_avx2_xor_r1\": %.3f, \"us_per_group_gfni_r3\": %.3f, "
+              "\"groups_per_s_avx2_xor_r1\": %.0f, \"groups_per_s_gfni_r3\": %.0f}\n",
+              xor_us, rs3_us, 1e6 / xor_us, 1e6 / rs3_us);
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const std::string mode = argc > 1 ? argv[1] : "cpu";
+  auto arg = [&](int i, double d) { return argc > i ? std::atof(argv[i]) : d; };
+  if (mode == "paced") return paced(int(arg(2, 10)), arg(3, 100), arg(4, 5), int(arg(5, 1)), int(arg(6, 1000)));
+  if (mode == "saturate")
+    return saturate(int(arg(2, 16)), arg(3, 3), int(arg(4, 1)), int(arg(5, 1000)), int(arg(6, 4096)));
+  if (mode == "single") return single(int(arg(2, 2000)));
+  return cpu();
+}

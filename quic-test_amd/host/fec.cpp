@@ -535,7 +535,10 @@ Error BatchedFECEncoder::submitLocked(Ticket* t) {
     return errorf("empty packets");
   }
   const int64_t tk = fec_batcher_submit(b_->raw(), packed_.data(), lens_.data(), static_cast<uint32_t>(lens_.size()));
-  if (tk < 0) return errorf("fec_batcher_submit failed with code %lld: %s", static_cast<long long>(tk), fec_batcher_last_error());
+  if (tk < 0) {  // refused (e.g. a packet wider than the slot): the group is dropped
+    packets_.clear();
+    return errorf("fec_batcher_submit failed with code %lld: %s", static_cast<long long>(tk), fec_batcher_last_error());
+  }
   t->ticket = tk;
   t->groupID = groupID_++;
   t->count = static_cast<int>(packets_.size());

@@ -4,6 +4,7 @@
 // Run by tests/test_host_mirror.py (GPU).  Prints "PASS <n>" or the failures.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -534,6 +535,123 @@ static void TestContextErrorAcrossThreads() {
   fec_encoder_free(ctx);
 }
 
+
+// ---------------------------------------------------------------- batcher
+// A stream's BatchedFECEncoder on a shared batcher gives HybridFECEncoder's bytes: same
+// row-0 repair packets (variable lengths, partial flush), same metrics.
+static void TestBatchedEncoderMatchesHybrid() {
+  auto sb = SharedFECBatcher::New(10, 1, 1500, 64, 2000);
+  CHECK(sb != nullptr);
+  if (!sb) return;
+  BatchedFECEncoder be(sb);
+  HybridFECEncoder hyb(0.1);
+  std::mt19937_64 rng(21);
+  int groups = 0;
+  bool same = true;
+  for (int i = 0; i < 10 * 17 + 6; ++i) {
+    Bytes pkt = rnd(1 + rng() % 1400, 3000 + i);
+    AddPacketResult a = be.AddPacket(pkt, i), b = hyb.AddPacket(pkt, i);
+    CHECK(a.err.ok() && b.err.ok());
+    same &= a.needsRedundancy == b.needsRedundancy && a.redundancy == b.redundancy && a.extra.empty();
+    groups += a.needsRedundancy;
+  }
+  CHECK(same && groups == 17);
+  AddPacketResult f = be.Flush();
+  auto g = hyb.Flush();
+  CHECK(f.err.ok() && g.second.ok() && f.needsRedundancy && f.redundancy == g.first);
+  FECMetrics m1 = be.GetMetrics(), m2 = hyb.GetMetrics();
+  CHECK(m1.GroupsProcessed == m2.GroupsProcessed && m1.PacketsEncoded == m2.PacketsEncoded &&
+        m1.RedundancyPackets == m2.RedundancyPackets && m1.RedundancyBytes == m2.RedundancyBytes);
+  Bytes big(1501, 1);  // wider than the batcher slot: refused, the stream keeps working
+  for (int i = 0; i < 9; ++i) be.AddPacket(rnd(100, 4000 + i), i);
+  CHECK(!be.AddPacket(big, 9).err.ok());
+}
+
+// r = 3 through the batcher: row 0 = the reference XOR (as HybridFECEncoder), rows 1..2 =
+// the oracle's GF rows, FE C1 headers; async submission collected in group order.
+static void TestBatchedEncoderRSAsync() {
+  const int k = 10, r = 3;
+  auto sb = SharedFECBatcher::New(k, r, 1216, 8, 500);
+  CHECK(sb != nullptr);
+  if (!sb) return;
+  BatchedFECEncoder be(sb);
+  std::vector<Bytes> sent, out;
+  for (int i = 0; i < 10 * 40 + 3; ++i) {
+    sent.push_back(rnd(64 + (i * 37) % 1150, 5000 + i));
+    CHECK(be.AddPacketAsync(sent.back().data(), sent.back().size(), i).ok());
+    if (i % 97 == 0) CHECK(be.Poll(&out, 0).ok());
+  }
+  CHECK(be.FlushAsync().ok());
+  CHECK(be.Poll(&out, -1).ok() && be.outstanding() == 0);
+  CHECK(out.size() == size_t(41) * r);
+  bool ok = out.size() == size_t(41) * r;
+  for (int g = 0; ok && g < 41; ++g) {
+    std::vector<Bytes> pk(sent.begin() + g * k, sent.begin() + std::min<int>(int(sent.size()), g * k + k));
+    auto exp = oracle_rows(pk, k, r);
+    ok &= out[size_t(g) * r] == go_redundancy(pk, uint64_t(g));
+    for (int i = 0; i < r; ++i) {
+      RSRepairHeader h;
+      const uint8_t* pl = nullptr;
+      size_t n = 0;
+      ok &= ParseRepairHeader(out[size_t(g) * r + i].data(), out[size_t(g) * r + i].size(), &h, &pl, &n) &&
+            h.groupID == uint64_t(g) && h.row == i && h.count == int(pk.size()) && Bytes(pl, pl + n) == exp[i];
+    }
+  }
+  CHECK(ok);
+  auto st = sb->Stats();
+  CHECK(st[0] == 41 && st[1] >= 6 && st[2] >= 1 && st[4] <= 8);  // some batches full (8 groups)
+}
+
+// Many streams, one batcher: every repair exact, groups of different streams share launches.
+static void TestBatcherManyStreams() {
+  const int S = 32, G = 30, k = 10;
+  auto sb = SharedFECBatcher::New(k, 1, 1200, 16, 300);
+  CHECK(sb != nullptr);
+  if (!sb) return;
+  std::atomic<int> bad{0}, got{0};
+  std::vector<std::thread> th;
+  for (int s = 0; s < S; ++s)
+    th.emplace_back([&, s] {
+      BatchedFECEncoder be(sb);
+      std::vector<Bytes> grp;
+      for (int i = 0; i < G * k; ++i) {
+        grp.push_back(rnd(1200, uint64_t(s) * 100000 + i));
+        AddPacketResult a = be.AddPacket(grp.back(), i);
+        if (!a.err.ok()) ++bad;
+        if (a.needsRedundancy) {
+          ++got;
+          if (a.redundancy != go_redundancy(grp, uint64_t(i / k))) ++bad;
+          grp.clear();
+        }
+      }
+    });
+  for (auto& t : th) t.join();
+  CHECK(bad == 0 && got == S * G);
+  auto st = sb->Stats();
+  CHECK(st[0] == uint64_t(S * G) && st[1] < st[0]);  // fewer launches than groups
+}
+
+// The deadline bounds a lone stream's wait; deadline 0 encodes at once.
+static void TestBatcherDeadline() {
+  for (int deadline_us : {0, 30000}) {
+    auto sb = SharedFECBatcher::New(10, 1, 1200, 4096, deadline_us);
+    CHECK(sb != nullptr);
+    if (!sb) return;
+    BatchedFECEncoder be(sb);
+    for (int i = 0; i < 9; ++i) be.AddPacket(rnd(1200, 6000 + i), i);
+    const auto t0 = std::chrono::steady_clock::now();
+    AddPacketResult a = be.AddPacket(rnd(1200, 6009), 9);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    CHECK(a.err.ok() && a.needsRedundancy);
+    if (deadline_us == 0) CHECK(ms < 200);
+    else CHECK(ms >= 29.0 && ms < 30.0 + 500);
+    auto st = sb->Stats();
+    CHECK(st[0] == 1 && st[1] == 1 && st[3] == 1);
+  }
+  CHECK(SharedFECBatcher::New(200, 57, 1200, 16, 100) == nullptr);  // k + r > 256
+  CHECK(fec_batcher_wait(nullptr, 0, nullptr, 0, 0) == FEC_ERR_NULL);
+}
+
 int main() {
   TestContextErrorAcrossThreads();
   TestNewFECEncoder();
@@ -555,6 +673,10 @@ int main() {
   TestRSDecoderDeferredBatch();
   TestRSDecoderLimits();
   TestRSDecoderPartialAndShort();
+  TestBatchedEncoderMatchesHybrid();
+  TestBatchedEncoderRSAsync();
+  TestBatcherManyStreams();
+  TestBatcherDeadline();
   if (g_fail) {
     std::printf("FAILED %d of %d checks\n", g_fail, g_checks);
     return 1;
