@@ -163,6 +163,7 @@ typedef struct {
   uint64_t full_flushes;      /* batches closed because max_groups were pending    */
   uint64_t deadline_flushes;  /* batches closed by the deadline (or fec_batcher_flush) */
   uint64_t max_batch;         /* largest batch                                     */
+  uint64_t expired;           /* results dropped uncollected (see fec_batcher_wait) */
 } FECBatcherStats;
 
 FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint32_t slot_bytes, uint32_t max_groups,
@@ -177,7 +178,8 @@ int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, const uint32_t*
 /* Waits for a ticket's batch (timeout_us < 0: no limit; 0: poll) and copies its r repair
  * payloads to out (row i at out + i*out_stride; NULL: discard).  Returns the payload length,
  * FEC_ERR_AGAIN on timeout (the ticket stays valid), or another negative code.  Each ticket
- * can be collected once; uncollected results are kept until fec_batcher_free. */
+ * can be collected once.  Results live in a ring of 2 * slabs * max_groups entries: one not
+ * collected before that many newer groups are encoded is dropped (FEC_ERR_RANGE). */
 int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int64_t timeout_us);
 
 /* Closes the pending batch now (e.g. at the end of a stream) instead of at its deadline. */

@@ -4,36 +4,41 @@
 // The reference encodes one group per cgo call: every QUIC stream owns a HybridFECEncoder
 // and calls EncodeBatch with a single group on its 10th packet (encoder_hybrid.go:71-73,
 // :115), at --rate packets/s per stream (main.go:32, client.go:1140-1143).  A GPU launch per
-// group costs ~15 us against ~0.6 us for the reference's AVX2 loop, so the GPU only pays with
-// many groups per launch.  A batcher is shared by every stream of the process: a stream
-// submits a finished group and gets a ticket; the batch is encoded when `max_groups` groups
-// are pending OR `deadline_us` has passed since the oldest pending group arrived, whichever
-// comes first, so no repair waits longer than the deadline plus one encode.
+// group costs ~15 us against well under a microsecond for the reference's AVX2 loop, so the
+// GPU only pays with many groups per launch.  A batcher is shared by every stream of the
+// process: a stream submits a finished group and gets a ticket; the batch is encoded when
+// `max_groups` groups are pending OR `deadline_us` has passed since the oldest pending group
+// arrived, whichever comes first, so no repair waits longer than the deadline plus one encode.
 //
 // Memory: a ring of `slabs` page-locked slabs (fec_alloc_slab), each max_groups groups of k
 // slots of `slot_bytes`, plus its parity; the kernels read and write them in place over PCIe
 // (the zero-copy path of fec_encode_batch_rs), so a batch costs one launch and one
-// synchronize.  While one slab is being encoded the next one fills.  When every slab is busy,
+// synchronize.  While one slab is being encoded the next ones fill.  When every slab is busy,
 // submitters wait (backpressure).
 //
-// Threads: submitters copy their group into the open slab under the batcher lock; one
-// flusher thread per batcher closes slabs (full or deadline), encodes them on the batcher's
-// own context and publishes every group's r repair payloads (maxLen bytes each, the group's
-// longest packet, as the reference's repair length, encoder_hybrid.go:91-98) under its ticket.
-// fec_batcher_wait hands a ticket's payloads to the caller and forgets them.
+// Threads.  A submitter reserves its group's slot under the batcher lock and copies the
+// packets in after releasing it, so streams copy in parallel; the slab is encoded once every
+// reserved copy has landed.  One flusher thread per batcher closes slabs (full or due),
+// encodes them on the batcher's own context and publishes each group's r repair payloads
+// (maxLen bytes each, the group's longest packet: the reference's repair length,
+// encoder_hybrid.go:91-98) into a ring of result entries indexed by ticket, which waiters read
+// without the lock.  A result not collected before 2 * slabs * max_groups newer groups are
+// published is dropped (the late wait gets FEC_ERR_RANGE; stats.expired counts them).
 #include <hip/hip_runtime.h>
+#include <sys/prctl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
-#include <unordered_map>
 #include <vector>
 
 #include "fec_hip.h"
@@ -54,14 +59,18 @@ struct GroupMeta {
 struct Slab {
   uint8_t* data = nullptr;    // max_groups * k * slot, page-locked
   uint8_t* parity = nullptr;  // max_groups * r * slot, page-locked
-  std::vector<GroupMeta> groups;
+  std::vector<GroupMeta> groups;         // reserved groups (under the batcher lock)
+  std::atomic<uint32_t> committed{0};    // groups whose packets have been copied in
 };
 
-struct Result {
+// One published result.  `ticket` is -1 while the entry is being (re)written, else the
+// ticket whose payloads it holds; a reader copies, then re-checks `ticket` (a rewrite in
+// between makes the copy invalid) and claims it by swapping in -1.
+struct Entry {
+  std::atomic<int64_t> ticket{-1};
   int rc = FEC_OK;
   uint32_t len = 0;
   std::vector<uint8_t> bytes;  // r rows of len bytes
-  std::string err;             // the failed batch's message
 };
 
 }  // namespace
@@ -70,13 +79,15 @@ struct FECBatcher {
   uint32_t k = 0, r = 0, slot = 0, max_groups = 0;
   std::chrono::microseconds deadline{0};
   FECEncoderCtx* ctx = nullptr;
-  std::vector<Slab> slabs;
+  std::vector<std::unique_ptr<Slab>> slabs;
   int open = -1;                 // slab accepting groups, -1 while every slab is busy
   std::deque<int> free_slabs;    // empty slabs
   std::deque<int> closed;        // full or due slabs waiting for the flusher
   int64_t next_ticket = 0;
-  std::unordered_map<int64_t, Result> results;
+  int64_t published_upto = 0;    // every ticket below this has been published (in order)
+  std::vector<Entry> ring;       // results, entry ticket % ring.size()
   FECBatcherStats stats{};
+  std::string last_batch_error;  // message of the last failed batch (under mu)
   bool stop = false;
   std::mutex mu;
   std::condition_variable cv_flusher, cv_done, cv_free;
@@ -90,8 +101,8 @@ struct FECBatcher {
     cv_flusher.notify_all();
     if (flusher.joinable()) flusher.join();
     for (auto& s : slabs) {
-      if (s.data) fec_free_slab(s.data);
-      if (s.parity) fec_free_repair_buffer(s.parity);
+      if (s->data) fec_free_slab(s->data);
+      if (s->parity) fec_free_repair_buffer(s->parity);
     }
     if (ctx) fec_encoder_free(ctx);
   }
@@ -99,7 +110,7 @@ struct FECBatcher {
   // Moves the open slab to the flusher's queue and opens the next free one (or none).
   // Caller holds mu.
   void close_open(bool full) {
-    if (open < 0 || slabs[open].groups.empty()) return;
+    if (open < 0 || slabs[open]->groups.empty()) return;
     closed.push_back(open);
     ++(full ? stats.full_flushes : stats.deadline_flushes);
     if (!free_slabs.empty()) {
@@ -111,8 +122,9 @@ struct FECBatcher {
   }
 
   void encode_slab(int si) {
-    Slab& s = slabs[si];
-    const uint32_t n = static_cast<uint32_t>(s.groups.size());
+    Slab& s = *slabs[si];
+    const uint32_t n = static_cast<uint32_t>(s.groups.size());  // closed: no more reservations
+    while (s.committed.load(std::memory_order_acquire) < n) std::this_thread::yield();  // copies in flight
     const int rc = fec_encode_batch_rs(ctx, s.data, nullptr, n, k, r, slot, s.parity);
     std::string err;
     if (rc != FEC_OK) {
@@ -120,28 +132,29 @@ struct FECBatcher {
       fec_ctx_last_error(ctx, buf, sizeof(buf));
       err = buf;
     }
-    // Repair payloads out of the slab (so it can be refilled at once), outside the lock.
-    std::vector<std::pair<int64_t, Result>> out(n);
+    // Repair payloads out of the slab (so it can be refilled at once), without the lock.
     for (uint32_t g = 0; g < n; ++g) {
       const GroupMeta& m = s.groups[g];
-      Result& res = out[g].second;
-      out[g].first = m.ticket;
-      res.rc = rc;
-      if (rc != FEC_OK) {
-        res.err = err;
-        continue;
-      }
-      res.len = m.max_len;
-      res.bytes.resize(size_t(r) * m.max_len);
-      for (uint32_t i = 0; i < r; ++i)
-        std::memcpy(res.bytes.data() + size_t(i) * m.max_len, s.parity + (size_t(g) * r + i) * slot, m.max_len);
+      Entry& e = ring[static_cast<size_t>(m.ticket) % ring.size()];
+      const int64_t prev = e.ticket.exchange(-1, std::memory_order_acq_rel);
+      if (prev >= 0) ++dropped;  // never collected: dropped
+      e.rc = rc;
+      e.len = rc == FEC_OK ? m.max_len : 0;
+      e.bytes.resize(size_t(r) * e.len);
+      for (uint32_t i = 0; i < r && rc == FEC_OK; ++i)
+        std::memcpy(e.bytes.data() + size_t(i) * e.len, s.parity + (size_t(g) * r + i) * slot, e.len);
+      e.ticket.store(m.ticket, std::memory_order_release);
     }
     std::lock_guard<std::mutex> lk(mu);
-    for (auto& kv : out) results.emplace(kv.first, std::move(kv.second));
     ++stats.batches;
     stats.groups += n;
     if (n > stats.max_batch) stats.max_batch = n;
+    stats.expired += dropped;
+    dropped = 0;
+    if (n > 0) published_upto = s.groups.back().ticket + 1;
+    if (rc != FEC_OK) last_batch_error = err;
     s.groups.clear();
+    s.committed.store(0, std::memory_order_relaxed);
     if (open < 0) {
       open = si;
     } else {
@@ -152,6 +165,8 @@ struct FECBatcher {
   }
 
   void run() {
+    // Wake at the deadline itself, not up to the default 50 us timer slack later.
+    prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
       if (!closed.empty()) {
@@ -162,14 +177,14 @@ struct FECBatcher {
         lk.lock();
         continue;
       }
-      const bool pending = open >= 0 && !slabs[open].groups.empty();
+      const bool pending = open >= 0 && !slabs[open]->groups.empty();
       if (stop) {
         if (!pending) return;
         close_open(false);  // shutdown: encode what is pending, then leave
         continue;
       }
       if (pending) {
-        const Clock::time_point due = slabs[open].groups.front().t_submit + deadline;
+        const Clock::time_point due = slabs[open]->groups.front().t_submit + deadline;
         if (Clock::now() >= due) {
           close_open(false);
           continue;
@@ -180,6 +195,8 @@ struct FECBatcher {
       }
     }
   }
+
+  uint64_t dropped = 0;  // flusher only
 };
 
 namespace {
@@ -216,9 +233,9 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
     return nullptr;
   }
   const uint32_t nslabs = slabs < 2 ? 2 : slabs;
-  b->slabs.resize(nslabs);
   for (uint32_t i = 0; i < nslabs; ++i) {
-    Slab& s = b->slabs[i];
+    b->slabs.push_back(std::make_unique<Slab>());
+    Slab& s = *b->slabs.back();
     s.data = static_cast<uint8_t*>(fec_alloc_slab(size_t(max_groups) * k * slot_bytes));
     s.parity = static_cast<uint8_t*>(fec_alloc_repair_buffer(size_t(max_groups) * r * slot_bytes));
     if (!s.data || !s.parity) {
@@ -228,6 +245,18 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
     }
     s.groups.reserve(max_groups);
     if (i > 0) b->free_slabs.push_back(static_cast<int>(i));
+  }
+  // Results of two full rounds of slabs stay collectable.
+  b->ring = std::vector<Entry>(size_t(2) * nslabs * max_groups);
+  // Warm-up: the first launch loads the code object and the (k, r) tables; do it here, not
+  // in the first stream's repair delay.
+  std::memset(b->slabs[0]->data, 0, size_t(k) * slot_bytes);
+  if (fec_encode_batch_rs(b->ctx, b->slabs[0]->data, nullptr, 1, k, r, slot_bytes, b->slabs[0]->parity) != FEC_OK) {
+    char buf[512];
+    fec_ctx_last_error(b->ctx, buf, sizeof(buf));
+    berr("fec_batcher_new: warm-up encode failed: %s", buf);
+    delete b;
+    return nullptr;
   }
   b->open = 0;
   b->flusher = std::thread([b] { b->run(); });
@@ -254,12 +283,27 @@ QFEC_EXPORT int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, con
     berr("fec_batcher_submit: empty packets");
     return FEC_ERR_RANGE;
   }
-  std::unique_lock<std::mutex> lk(b->mu);
-  b->cv_free.wait(lk, [b] { return b->open >= 0 || b->stop; });
-  if (b->stop) return FEC_ERR_RANGE;
-  Slab& s = b->slabs[b->open];
-  const size_t g = s.groups.size();
-  uint8_t* dst = s.data + g * b->k * size_t(b->slot);
+  // Reserve the slot under the lock ...
+  Slab* s = nullptr;
+  size_t g = 0;
+  int64_t ticket = 0;
+  {
+    std::unique_lock<std::mutex> lk(b->mu);
+    b->cv_free.wait(lk, [b] { return b->open >= 0 || b->stop; });
+    if (b->stop) return FEC_ERR_RANGE;
+    s = b->slabs[b->open].get();
+    g = s->groups.size();
+    ticket = b->next_ticket++;
+    s->groups.push_back(GroupMeta{ticket, count, max_len, Clock::now()});
+    if (s->groups.size() == b->max_groups) {
+      b->close_open(true);
+      b->cv_flusher.notify_one();
+    } else if (g == 0) {
+      b->cv_flusher.notify_one();  // a deadline starts
+    }
+  }
+  // ... and copy without it (the flusher encodes a slab once every reserved copy landed).
+  uint8_t* dst = s->data + g * b->k * size_t(b->slot);
   const uint8_t* src = packed;
   for (uint32_t j = 0; j < b->k; ++j) {  // packets zero-padded to the slot, absent slots zero
     uint8_t* d = dst + size_t(j) * b->slot;
@@ -268,48 +312,80 @@ QFEC_EXPORT int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, con
     std::memset(d + n, 0, b->slot - n);
     src += n;
   }
-  const int64_t ticket = b->next_ticket++;
-  s.groups.push_back(GroupMeta{ticket, count, max_len, Clock::now()});
-  if (s.groups.size() == b->max_groups) {
-    b->close_open(true);
-    b->cv_flusher.notify_one();
-  } else if (g == 0) {
-    b->cv_flusher.notify_one();  // a deadline starts
-  }
+  s->committed.fetch_add(1, std::memory_order_release);
   return ticket;
 }
 
+namespace {
+
+// Copies a published result out of the ring and claims it: 1 done, 0 not published yet,
+// negative code on failure.  *len = payload length.
+int take(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int* len) {
+  Entry& e = b->ring[static_cast<size_t>(ticket) % b->ring.size()];
+  if (e.ticket.load(std::memory_order_acquire) != ticket) return 0;
+  const int rc = e.rc;
+  const uint32_t n = e.len;
+  if (rc == FEC_OK && out) {
+    if (out_stride < n) {
+      berr("fec_batcher_wait: out_stride %u < repair length %u", out_stride, n);
+      return FEC_ERR_RANGE;
+    }
+    for (uint32_t i = 0; i < b->r; ++i) std::memcpy(out + size_t(i) * out_stride, e.bytes.data() + size_t(i) * n, n);
+  }
+  int64_t expect = ticket;
+  if (!e.ticket.compare_exchange_strong(expect, -1, std::memory_order_acq_rel)) {
+    berr("fec_batcher_wait: result of ticket %lld was overwritten while read", static_cast<long long>(ticket));
+    return FEC_ERR_RANGE;
+  }
+  if (rc != FEC_OK) {
+    std::lock_guard<std::mutex> lk(b->mu);
+    berr("fec_batcher_wait: the batch of ticket %lld failed with code %d: %s", static_cast<long long>(ticket), rc,
+         b->last_batch_error.c_str());
+    return rc;
+  }
+  *len = static_cast<int>(n);
+  return 1;
+}
+
+}  // namespace
+
 QFEC_EXPORT int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int64_t timeout_us) {
   if (!b) return FEC_ERR_NULL;
+  int len = 0;
+  int st = ticket >= 0 ? take(b, ticket, out, out_stride, &len) : 0;
+  if (st == 1) return len;
+  if (st < 0) return st;
   std::unique_lock<std::mutex> lk(b->mu);
   if (ticket < 0 || ticket >= b->next_ticket) {
     berr("fec_batcher_wait: unknown ticket %lld", static_cast<long long>(ticket));
     return FEC_ERR_RANGE;
   }
-  auto ready = [&] { return b->results.count(ticket) != 0; };
-  if (timeout_us < 0) {
-    b->cv_done.wait(lk, ready);
-  } else if (!b->cv_done.wait_for(lk, std::chrono::microseconds(timeout_us), ready)) {
-    return FEC_ERR_AGAIN;
-  }
-  auto it = b->results.find(ticket);
-  Result res = std::move(it->second);
-  b->results.erase(it);
-  lk.unlock();
-  if (res.rc != FEC_OK) {
-    berr("fec_batcher_wait: the batch of ticket %lld failed with code %d: %s", static_cast<long long>(ticket), res.rc,
-         res.err.c_str());
-    return res.rc;
-  }
-  if (out) {
-    if (out_stride < res.len) {
-      berr("fec_batcher_wait: out_stride %u < repair length %u", out_stride, res.len);
+  // Results are published between a batch's ring writes and its cv_done signal (under mu),
+  // in ticket order, so checking under mu and waiting on cv_done misses none.
+  const auto until = Clock::now() + std::chrono::microseconds(timeout_us > 0 ? timeout_us : 0);
+  Entry& e = b->ring[static_cast<size_t>(ticket) % b->ring.size()];
+  for (;;) {
+    if (e.ticket.load(std::memory_order_acquire) == ticket) break;
+    if (ticket < b->published_upto) {
+      berr("fec_batcher_wait: ticket %lld was already collected or its result expired (more than %zu newer "
+           "groups encoded)", static_cast<long long>(ticket), b->ring.size());
       return FEC_ERR_RANGE;
     }
-    for (uint32_t i = 0; i < b->r; ++i)
-      std::memcpy(out + size_t(i) * out_stride, res.bytes.data() + size_t(i) * res.len, res.len);
+    if (timeout_us < 0) {
+      b->cv_done.wait(lk);
+    } else if (timeout_us == 0 || b->cv_done.wait_until(lk, until) == std::cv_status::timeout) {
+      if (e.ticket.load(std::memory_order_acquire) == ticket) break;
+      return FEC_ERR_AGAIN;
+    }
   }
-  return static_cast<int>(res.len);
+  lk.unlock();
+  st = take(b, ticket, out, out_stride, &len);
+  if (st == 1) return len;
+  if (st == 0) {
+    berr("fec_batcher_wait: ticket %lld was already collected", static_cast<long long>(ticket));
+    return FEC_ERR_RANGE;
+  }
+  return st;
 }
 
 QFEC_EXPORT int fec_batcher_flush(FECBatcher* b) {
