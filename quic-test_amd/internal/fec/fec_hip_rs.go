@@ -34,15 +34,37 @@ type RSCodec struct {
 	mu  sync.Mutex
 }
 
-func hipError(what string, code C.int) error {
-	return fmt.Errorf("%s failed with code %d: %s", what, int(code), C.GoString(C.fec_hip_last_error()))
+// ctxError reads the failing call's message from the context itself (fec_ctx_last_error):
+// the goroutine may have moved to another OS thread since the call, so the thread-local
+// fec_hip_last_error could be empty or another call's.  The reference wrapper reports the
+// code alone (fec_cgo.go:147-149).
+func ctxError(ctx *C.FECEncoderCtx, what string, code C.int) error {
+	var buf [512]C.char
+	C.fec_ctx_last_error(ctx, &buf[0], C.size_t(len(buf)))
+	return fmt.Errorf("%s failed with code %d: %s", what, int(code), C.GoString(&buf[0]))
 }
+
+// lockedError runs a call whose failure text is thread-local (fec_group_*, fec_batcher_*,
+// context creation) with the goroutine pinned to its OS thread, so the text read after it
+// is this call's.
+func lockedError(call func() C.int, what string, lastError func() *C.char) error {
+	runtime.LockOSThread()
+	defer runtime.UnlockOSThread()
+	if rc := call(); rc != 0 {
+		return fmt.Errorf("%s failed with code %d: %s", what, int(rc), C.GoString(lastError()))
+	}
+	return nil
+}
+
+func hipLastError() *C.char { return C.fec_hip_last_error() }
 
 // NewRSCodec binds a codec to GPU `device` (use -1 for the current HIP device).
 func NewRSCodec(k, r, device int) (*RSCodec, error) {
 	if k <= 0 || r <= 0 || k+r > 256 {
 		return nil, fmt.Errorf("unsupported k=%d r=%d", k, r)
 	}
+	runtime.LockOSThread() // the creation error is thread-local
+	defer runtime.UnlockOSThread()
 	var ctx *C.FECEncoderCtx
 	if device < 0 {
 		ctx = C.fec_encoder_new(C.double(float64(r)/float64(k)), 1024)
@@ -77,7 +99,7 @@ func (c *RSCodec) EncodeBatch(data []byte, packetSize int, parity []byte) error 
 	runtime.KeepAlive(data)
 	runtime.KeepAlive(parity)
 	if rc != 0 {
-		return hipError("fec_encode_batch_rs", rc)
+		return ctxError(c.ctx, "fec_encode_batch_rs", rc)
 	}
 	return nil
 }
@@ -87,6 +109,9 @@ func (c *RSCodec) EncodeBatch(data []byte, packetSize int, parity []byte) error 
 // len >= groups) is 0 when the group is complete afterwards, 1 when it had more losses
 // than surviving parity rows.  Returns the number of unrecoverable groups.
 func (c *RSCodec) DecodeBatch(data, parity []byte, erasures []uint64, packetSize int, status []byte) (int, error) {
+	if c.k+c.r > 64 { // one erasure bit per shard (include/fec_hip.h)
+		return 0, fmt.Errorf("decode needs k+r <= 64 (k=%d r=%d)", c.k, c.r)
+	}
 	groups := len(erasures)
 	if packetSize <= 0 || len(data) < groups*c.k*packetSize || len(parity) < groups*c.r*packetSize {
 		return 0, fmt.Errorf("buffers too small for %d groups", groups)
@@ -112,7 +137,7 @@ func (c *RSCodec) DecodeBatch(data, parity []byte, erasures []uint64, packetSize
 	runtime.KeepAlive(erasures)
 	runtime.KeepAlive(status)
 	if rc != 0 {
-		return 0, hipError("fec_decode_batch_rs", rc)
+		return 0, ctxError(c.ctx, "fec_decode_batch_rs", rc)
 	}
 	return int(bad), nil
 }
@@ -143,6 +168,8 @@ func NewRSDeviceGroup(k, r int, devices []int) (*RSDeviceGroup, error) {
 	if k <= 0 || r <= 0 || k+r > 256 {
 		return nil, fmt.Errorf("unsupported k=%d r=%d", k, r)
 	}
+	runtime.LockOSThread() // the creation error is thread-local
+	defer runtime.UnlockOSThread()
 	var grp *C.FECDeviceGroup
 	if len(devices) == 0 {
 		grp = C.fec_group_new(nil, 0)
@@ -178,18 +205,20 @@ func (g *RSDeviceGroup) EncodeBatch(data []byte, packetSize int, parity []byte) 
 	}
 	g.mu.Lock()
 	defer g.mu.Unlock()
-	rc := C.fec_group_encode_batch_rs(g.grp, (*C.uint8_t)(unsafe.Pointer(&data[0])), C.uint64_t(groups),
-		C.uint32_t(g.k), C.uint32_t(g.r), C.uint32_t(packetSize), (*C.uint8_t)(unsafe.Pointer(&parity[0])))
+	err := lockedError(func() C.int {
+		return C.fec_group_encode_batch_rs(g.grp, (*C.uint8_t)(unsafe.Pointer(&data[0])), C.uint64_t(groups),
+			C.uint32_t(g.k), C.uint32_t(g.r), C.uint32_t(packetSize), (*C.uint8_t)(unsafe.Pointer(&parity[0])))
+	}, "fec_group_encode_batch_rs", hipLastError)
 	runtime.KeepAlive(data)
 	runtime.KeepAlive(parity)
-	if rc != 0 {
-		return hipError("fec_group_encode_batch_rs", rc)
-	}
-	return nil
+	return err
 }
 
 // DecodeBatch: as RSCodec.DecodeBatch, sharded over the group's devices.
 func (g *RSDeviceGroup) DecodeBatch(data, parity []byte, erasures []uint64, packetSize int, status []byte) (int, error) {
+	if g.k+g.r > 64 {
+		return 0, fmt.Errorf("decode needs k+r <= 64 (k=%d r=%d)", g.k, g.r)
+	}
 	groups := len(erasures)
 	if packetSize <= 0 || len(data) < groups*g.k*packetSize || len(parity) < groups*g.r*packetSize {
 		return 0, fmt.Errorf("buffers too small for %d groups", groups)
@@ -207,15 +236,17 @@ func (g *RSDeviceGroup) DecodeBatch(data, parity []byte, erasures []uint64, pack
 		st = (*C.uint8_t)(unsafe.Pointer(&status[0]))
 	}
 	var bad C.uint64_t
-	rc := C.fec_group_decode_batch_rs(g.grp, (*C.uint8_t)(unsafe.Pointer(&data[0])), (*C.uint8_t)(unsafe.Pointer(&parity[0])),
-		(*C.uint64_t)(unsafe.Pointer(&erasures[0])), C.uint64_t(groups), C.uint32_t(g.k), C.uint32_t(g.r),
-		C.uint32_t(packetSize), st, &bad)
+	err := lockedError(func() C.int {
+		return C.fec_group_decode_batch_rs(g.grp, (*C.uint8_t)(unsafe.Pointer(&data[0])), (*C.uint8_t)(unsafe.Pointer(&parity[0])),
+			(*C.uint64_t)(unsafe.Pointer(&erasures[0])), C.uint64_t(groups), C.uint32_t(g.k), C.uint32_t(g.r),
+			C.uint32_t(packetSize), st, &bad)
+	}, "fec_group_decode_batch_rs", hipLastError)
 	runtime.KeepAlive(data)
 	runtime.KeepAlive(parity)
 	runtime.KeepAlive(erasures)
 	runtime.KeepAlive(status)
-	if rc != 0 {
-		return 0, hipError("fec_group_decode_batch_rs", rc)
+	if err != nil {
+		return 0, err
 	}
 	return int(bad), nil
 }

@@ -8,8 +8,11 @@ package fec
 
 import (
 	"bytes"
+	"fmt"
 	"math/rand"
+	"sync"
 	"testing"
+	"time"
 )
 
 // Parity row 0 of RSCodec equals the reference XOR repair (FECEncoderCXX / FECEncoder).
@@ -77,5 +80,49 @@ func TestRSCodecRoundTrip(t *testing.T) {
 	}
 	if !bytes.Equal(broken, data) {
 		t.Fatal("round trip mismatch")
+	}
+}
+
+// BatchedFECEncoder on a SharedBatcher returns HybridFECEncoder's repair packets, from many
+// goroutines at once (one stream each), with groups of different streams sharing launches.
+func TestBatchedEncoderMatchesHybrid(t *testing.T) {
+	sb, err := NewSharedBatcher(10, 1, 1500, 64, time.Millisecond, -1)
+	if err != nil {
+		t.Skipf("no GPU: %v", err)
+	}
+	defer sb.Close()
+	var wg sync.WaitGroup
+	errs := make(chan error, 16)
+	for s := 0; s < 16; s++ {
+		wg.Add(1)
+		go func(seed int64) {
+			defer wg.Done()
+			be := sb.NewEncoder()
+			hy := NewHybridFECEncoder(0.1)
+			rng := rand.New(rand.NewSource(seed))
+			for i := 0; i < 10*20+3; i++ {
+				pkt := make([]byte, 1+rng.Intn(1400))
+				rng.Read(pkt)
+				a1, r1, e1 := be.AddPacket(pkt, uint64(i))
+				a2, r2, e2 := hy.AddPacket(pkt, uint64(i))
+				if e1 != nil || e2 != nil || a1 != a2 || !bytes.Equal(r1, r2) {
+					errs <- fmt.Errorf("stream %d packet %d: batched and hybrid repairs differ", seed, i)
+					return
+				}
+			}
+			f1, e1 := be.Flush()
+			f2, e2 := hy.Flush()
+			if e1 != nil || e2 != nil || !bytes.Equal(f1, f2) {
+				errs <- fmt.Errorf("stream %d: flush differs", seed)
+			}
+		}(int64(s))
+	}
+	wg.Wait()
+	close(errs)
+	for err := range errs {
+		t.Fatal(err)
+	}
+	if st := sb.Stats(); st[0] != 16*21 || st[1] >= st[0] {
+		t.Fatalf("stats %v: expected %d groups in fewer launches", st, 16*21)
 	}
 }

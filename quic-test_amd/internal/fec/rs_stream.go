@@ -130,10 +130,14 @@ func NewRSBatchEncoder(k, r, batch, slot int) (*RSBatchEncoder, error) {
 	if k < 1 || r < 1 || k+r > 64 || batch < 1 || slot < 1 {
 		return nil, fmt.Errorf("unsupported k=%d r=%d batch=%d slot=%d", k, r, batch, slot)
 	}
+	runtime.LockOSThread() // the creation error is thread-local
 	ctx := C.fec_encoder_new(C.double(float64(r)/float64(k)), C.uint32_t(batch))
 	if ctx == nil {
-		return nil, fmt.Errorf("no usable GPU: %s", C.GoString(C.fec_hip_last_error()))
+		err := fmt.Errorf("no usable GPU: %s", C.GoString(C.fec_hip_last_error()))
+		runtime.UnlockOSThread()
+		return nil, err
 	}
+	runtime.UnlockOSThread()
 	e := &RSBatchEncoder{ctx: ctx, k: k, r: r, batch: batch, slot: (slot + 15) &^ 15,
 		count: make([]int, batch), maxLen: make([]int, batch)}
 	e.slab, e.parity = pinned(batch*k*e.slot), pinned(batch*r*e.slot)
@@ -199,7 +203,7 @@ func (e *RSBatchEncoder) encode(groups int) ([][]byte, error) {
 	rc := C.fec_encode_batch_rs(e.ctx, (*C.uint8_t)(unsafe.Pointer(&e.slab[0])), nil, C.uint64_t(groups),
 		C.uint32_t(e.k), C.uint32_t(e.r), C.uint32_t(e.slot), (*C.uint8_t)(unsafe.Pointer(&e.parity[0])))
 	if rc != 0 {
-		return nil, hipError("fec_encode_batch_rs", rc)
+		return nil, ctxError(e.ctx, "fec_encode_batch_rs", rc)
 	}
 	out := make([][]byte, 0, groups*e.r)
 	var firstErr error
@@ -398,6 +402,9 @@ func (d *RSDecoder) try(id uint64, g *rsGroup) []Recovered {
 		d.metrics.FailedRecoveries++
 		return nil
 	}
+	if g.k == 0 { // row 0 only, one loss: the reference's XOR recovery (decoder.go:255-287)
+		return d.recoverSingle(g)
+	}
 	if d.deferred {
 		if !g.queued {
 			g.queued = true
@@ -407,6 +414,55 @@ func (d *RSDecoder) try(id uint64, g *rsGroup) []Recovered {
 	}
 	lists, _ := d.recover([]uint64{id})
 	return lists[0]
+}
+
+// recoverSingle rebuilds a row-0-only group's one lost packet as parity XOR every present
+// packet (decoder.go:255-287), on the GPU through the XOR entry point the reference binds
+// (xor_packets_*, fec_xor_simd.h:107-137), so groups of any count up to 255 work (the batch
+// decode's erasure masks stop at 64 shards).  cgo may not keep Go pointers in C memory, so
+// the symbols are gathered into one C buffer first.
+func (d *RSDecoder) recoverSingle(g *rsGroup) []Recovered {
+	lost := -1
+	for id := 0; id < g.packetCount; id++ {
+		if _, ok := g.packets[id]; !ok {
+			lost = id
+			break
+		}
+	}
+	L := g.symbolLen
+	if lost < 0 || L <= 0 {
+		return nil
+	}
+	n := g.packetCount // parity row 0 + the count-1 present packets
+	buf := (*byte)(C.malloc(C.size_t(n * L)))
+	ptrs := (*unsafe.Pointer)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(unsafe.Pointer(nil)))))
+	defer C.free(unsafe.Pointer(buf))
+	defer C.free(unsafe.Pointer(ptrs))
+	src := unsafe.Slice(buf, n*L)
+	ps := unsafe.Slice(ptrs, n)
+	copy(src[0:L], g.rows[0])
+	ps[0] = unsafe.Pointer(&src[0])
+	i := 1
+	for id := 0; id < g.packetCount; id++ {
+		if p, ok := g.packets[id]; ok {
+			copy(src[i*L:(i+1)*L], p)
+			ps[i] = unsafe.Pointer(&src[i*L])
+			i++
+		}
+	}
+	out := make([]byte, L)
+	runtime.LockOSThread() // xor_packets_* report failure through the thread-local error text
+	C.xor_packets_avx2((**C.uint8_t)(unsafe.Pointer(ptrs)), C.size_t(n), C.size_t(L), (*C.uint8_t)(unsafe.Pointer(&out[0])))
+	failed := C.GoString(C.fec_hip_last_error()) != ""
+	runtime.UnlockOSThread()
+	if failed {
+		d.metrics.FailedRecoveries++
+		return nil
+	}
+	g.packets[lost] = out
+	d.metrics.PacketsRecovered++
+	d.metrics.RecoveryEvents++
+	return []Recovered{{PacketID: uint64(lost), Data: out}}
 }
 
 // RecoverPending rebuilds every queued group, one library call per (k, r).
