@@ -59,6 +59,10 @@ struct GroupMeta {
 struct Slab {
   uint8_t* data = nullptr;    // max_groups * k * slot, page-locked
   uint8_t* parity = nullptr;  // max_groups * r * slot, page-locked
+  uint8_t* d_data = nullptr;  // the same memory as the kernels address it (zero-copy)
+  uint8_t* d_parity = nullptr;
+  hipEvent_t done = nullptr;  // the slab's encode has finished
+  int rc = FEC_OK;            // its launch status
   std::vector<GroupMeta> groups;         // reserved groups (under the batcher lock)
   std::atomic<uint32_t> committed{0};    // groups whose packets have been copied in
 };
@@ -83,8 +87,11 @@ struct FECBatcher {
   int open = -1;                 // slab accepting groups, -1 while every slab is busy
   std::deque<int> free_slabs;    // empty slabs
   std::deque<int> closed;        // full or due slabs waiting for the flusher
-  int64_t next_ticket = 0;
-  int64_t published_upto = 0;    // every ticket below this has been published (in order)
+  std::deque<int> in_flight;     // encodes launched, results not yet published (launch order)
+  int device = 0;
+  hipStream_t stream = nullptr;  // the flusher's launches
+  std::atomic<int64_t> next_ticket{0};
+  std::atomic<int64_t> published_upto{0};  // every ticket below this has been published (in order)
   std::vector<Entry> ring;       // results, entry ticket % ring.size()
   FECBatcherStats stats{};
   std::string last_batch_error;  // message of the last failed batch (under mu)
@@ -103,7 +110,9 @@ struct FECBatcher {
     for (auto& s : slabs) {
       if (s->data) fec_free_slab(s->data);
       if (s->parity) fec_free_repair_buffer(s->parity);
+      if (s->done) (void)hipEventDestroy(s->done);
     }
+    if (stream) (void)hipStreamDestroy(stream);
     if (ctx) fec_encoder_free(ctx);
   }
 
@@ -121,18 +130,32 @@ struct FECBatcher {
     }
   }
 
-  void encode_slab(int si) {
+  // Stage 1 (flusher, no lock): once every reserved copy has landed, launch the slab's
+  // encode asynchronously on the batcher's stream (the kernels read the page-locked slab
+  // and write its parity in place over PCIe) and record its completion event.
+  void launch_slab(int si) {
     Slab& s = *slabs[si];
     const uint32_t n = static_cast<uint32_t>(s.groups.size());  // closed: no more reservations
     while (s.committed.load(std::memory_order_acquire) < n) std::this_thread::yield();  // copies in flight
-    const int rc = fec_encode_batch_rs(ctx, s.data, nullptr, n, k, r, slot, s.parity);
+    s.rc = fec_encode_batch_rs_dev(ctx, s.d_data, n, k, r, slot, s.d_parity, stream);
+    if (s.rc == FEC_OK && hipEventRecord(s.done, stream) != hipSuccess) s.rc = FEC_ERR_HIP;
+  }
+
+  // Stage 2 (flusher, no lock until the end): wait for the slab's encode, copy every group's
+  // payloads into the result ring, then hand the slab back for refilling.  While the flusher
+  // waits here, the next slab's encode is already queued behind this one (stage 1 runs first
+  // whenever a slab is closed), so the GPU never waits for the copies.
+  void publish_slab(int si) {
+    Slab& s = *slabs[si];
+    const uint32_t n = static_cast<uint32_t>(s.groups.size());
+    int rc = s.rc;
+    if (rc == FEC_OK && hipEventSynchronize(s.done) != hipSuccess) rc = FEC_ERR_HIP;
     std::string err;
     if (rc != FEC_OK) {
       char buf[512];
       fec_ctx_last_error(ctx, buf, sizeof(buf));
-      err = buf;
+      err = buf[0] ? buf : "the batch's encode failed on the device";
     }
-    // Repair payloads out of the slab (so it can be refilled at once), without the lock.
     for (uint32_t g = 0; g < n; ++g) {
       const GroupMeta& m = s.groups[g];
       Entry& e = ring[static_cast<size_t>(m.ticket) % ring.size()];
@@ -151,7 +174,7 @@ struct FECBatcher {
     if (n > stats.max_batch) stats.max_batch = n;
     stats.expired += dropped;
     dropped = 0;
-    if (n > 0) published_upto = s.groups.back().ticket + 1;
+    if (n > 0) published_upto.store(s.groups.back().ticket + 1, std::memory_order_release);
     if (rc != FEC_OK) last_batch_error = err;
     s.groups.clear();
     s.committed.store(0, std::memory_order_relaxed);
@@ -167,13 +190,23 @@ struct FECBatcher {
   void run() {
     // Wake at the deadline itself, not up to the default 50 us timer slack later.
     prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);
+    (void)hipSetDevice(device);  // the events and stream live on the batcher's device
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
-      if (!closed.empty()) {
+      if (!closed.empty()) {  // launch first: keep the GPU busy while results are copied
         const int si = closed.front();
         closed.pop_front();
+        in_flight.push_back(si);
         lk.unlock();
-        encode_slab(si);
+        launch_slab(si);
+        lk.lock();
+        continue;
+      }
+      if (!in_flight.empty()) {
+        const int si = in_flight.front();
+        in_flight.pop_front();
+        lk.unlock();
+        publish_slab(si);
         lk.lock();
         continue;
       }
@@ -232,17 +265,36 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
     delete b;
     return nullptr;
   }
+  b->device = fec_encoder_device(b->ctx);
+  int prev_dev = -1;
+  (void)hipGetDevice(&prev_dev);
+  auto restore = [&] {
+    if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
+  };
+  if (hipSetDevice(b->device) != hipSuccess ||
+      hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
+    berr("fec_batcher_new: cannot create a stream on device %d", b->device);
+    restore();
+    delete b;
+    return nullptr;
+  }
   const uint32_t nslabs = slabs < 2 ? 2 : slabs;
   for (uint32_t i = 0; i < nslabs; ++i) {
     b->slabs.push_back(std::make_unique<Slab>());
     Slab& s = *b->slabs.back();
     s.data = static_cast<uint8_t*>(fec_alloc_slab(size_t(max_groups) * k * slot_bytes));
     s.parity = static_cast<uint8_t*>(fec_alloc_repair_buffer(size_t(max_groups) * r * slot_bytes));
-    if (!s.data || !s.parity) {
-      berr("fec_batcher_new: page-locked slab allocation failed (%s)", fec_hip_last_error());
+    void *dd = nullptr, *dp = nullptr;
+    if (!s.data || !s.parity || hipHostGetDevicePointer(&dd, s.data, 0) != hipSuccess ||
+        hipHostGetDevicePointer(&dp, s.parity, 0) != hipSuccess ||
+        hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+      berr("fec_batcher_new: page-locked slab setup failed (%s)", fec_hip_last_error());
+      restore();
       delete b;
       return nullptr;
     }
+    s.d_data = static_cast<uint8_t*>(dd);
+    s.d_parity = static_cast<uint8_t*>(dp);
     s.groups.reserve(max_groups);
     if (i > 0) b->free_slabs.push_back(static_cast<int>(i));
   }
@@ -255,9 +307,11 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
     char buf[512];
     fec_ctx_last_error(b->ctx, buf, sizeof(buf));
     berr("fec_batcher_new: warm-up encode failed: %s", buf);
+    restore();
     delete b;
     return nullptr;
   }
+  restore();
   b->open = 0;
   b->flusher = std::thread([b] { b->run(); });
   return b;
@@ -293,7 +347,7 @@ QFEC_EXPORT int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, con
     if (b->stop) return FEC_ERR_RANGE;
     s = b->slabs[b->open].get();
     g = s->groups.size();
-    ticket = b->next_ticket++;
+    ticket = b->next_ticket.fetch_add(1, std::memory_order_relaxed);
     s->groups.push_back(GroupMeta{ticket, count, max_len, Clock::now()});
     if (s->groups.size() == b->max_groups) {
       b->close_open(true);
@@ -355,8 +409,12 @@ QFEC_EXPORT int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, ui
   int st = ticket >= 0 ? take(b, ticket, out, out_stride, &len) : 0;
   if (st == 1) return len;
   if (st < 0) return st;
+  // A poll of a ticket not published yet needs no lock.
+  if (timeout_us == 0 && ticket >= b->published_upto.load(std::memory_order_acquire) &&
+      ticket < b->next_ticket.load(std::memory_order_relaxed))
+    return FEC_ERR_AGAIN;
   std::unique_lock<std::mutex> lk(b->mu);
-  if (ticket < 0 || ticket >= b->next_ticket) {
+  if (ticket < 0 || ticket >= b->next_ticket.load(std::memory_order_relaxed)) {
     berr("fec_batcher_wait: unknown ticket %lld", static_cast<long long>(ticket));
     return FEC_ERR_RANGE;
   }
@@ -366,7 +424,7 @@ QFEC_EXPORT int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, ui
   Entry& e = b->ring[static_cast<size_t>(ticket) % b->ring.size()];
   for (;;) {
     if (e.ticket.load(std::memory_order_acquire) == ticket) break;
-    if (ticket < b->published_upto) {
+    if (ticket < b->published_upto.load(std::memory_order_acquire)) {
       berr("fec_batcher_wait: ticket %lld was already collected or its result expired (more than %zu newer "
            "groups encoded)", static_cast<long long>(ticket), b->ring.size());
       return FEC_ERR_RANGE;
