@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "coef_tables.hpp"
 #include "fec_kernels.hpp"
 
 namespace qfec {
@@ -59,6 +60,15 @@ constexpr int kLdsTabs = 64;
 constexpr int kProbeWin10 = 128;  // probes only: kLdsTabs survivor window of 10 (default 6)
 constexpr int kProbeWin14 = 256;  // probes only: window of 14
 constexpr int kProbeWindowed = 512;  // probes only: windowed body, tables from the record
+// decode_fused: rebuilt shard m of group g goes to out + (g * MAXE + m) * P (one contiguous
+// run of rebuilt packets per group, groups back to back, like encode's parity rows) instead
+// of its place among the group's data shards.
+constexpr int kCompactOut = 1024;
+// decode_fused with kLdsTabs: the record holds bare coefficient bytes (compact codebook,
+// gf256.hpp) and the wave computes each coefficient's tables into its LDS slice
+// (coef_tables.hpp) instead of copying 32-byte table entries in: k=20 r=5 records shrink
+// from up to 3.3 KB to 256 B, the whole codebook from 143 MB to 12 MB.
+constexpr int kCoefBytes = 2048;
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
@@ -583,6 +593,14 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
       sid[s] = rec_byte(rw, s);
     }
   }
+  // destination of rebuilt row m (erased data shard `erased(m)`)
+  auto dest = [&](uint32_t m, uint32_t eid) -> uint8_t* {
+    if constexpr ((POL & kCompactOut) != 0) {
+      return out + (gw * MAXE + m) * static_cast<uint64_t>(P);
+    } else {
+      return og + eid * static_cast<uint64_t>(P);
+    }
+  };
   auto erased = [&](uint32_t m) -> uint32_t {
     if constexpr (DIRECT) {
       uint64_t x = lost;
@@ -604,7 +622,7 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
     if constexpr ((POL & kProbeNoStore) != 0) {
       if (acc[0] != 0x9E3779B9u || acc[NW - 1] != 0x7F4A7C15u) return;
     }
-    store(og + erased(0) * static_cast<uint64_t>(P), acc);
+    store(dest(0, erased(0)), acc);
     return;
   }
   // kLdsTabs: the wave's coefficient rows [m0, m0 + MAXE) come in with vector loads issued
@@ -616,7 +634,20 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
   const uint32_t tab_pieces = (e - m0 < MAXE ? e - m0 : MAXE) * K * 2u;
   // the slice holds kTabIter whole wave-loads (16 B per lane), so no load writes past it
   constexpr int kSliceTabs = kTabIter * 64 / 2;
-  if constexpr (kLds) {
+  // kCoefBytes: coefficient (m, s) of this pass is byte m * K + s after the compact record's
+  // header; lane i loads coefficient i (+ 64 j) now, ahead of the survivor loads, and builds
+  // its tables into the LDS slice once the survivor loads are in flight (below).
+  constexpr int kCoefIter = (MAXE * K + 63) / 64;
+  uint32_t coef[kCoefIter];
+  if constexpr (kLds && (POL & kCoefBytes) != 0) {
+    const uint8_t* cb = recp + 128 + m0 * K;
+    const uint32_t ncoef = tab_pieces / 2u;
+#pragma unroll
+    for (int j = 0; j < kCoefIter; ++j) {
+      const uint32_t i = lane + 64u * j;
+      coef[j] = i < ncoef ? cb[i] : 0u;
+    }
+  } else if constexpr (kLds) {
     // direct-to-LDS loads (global_load_lds_dwordx4: LDS address = wave base + lane * 16, no
     // VGPR destination); pieces past the rows re-read the last piece into unused slots
     const uint8_t* src = reinterpret_cast<const uint8_t*>(tabs + m0 * K);
@@ -642,6 +673,18 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
   uint32_t x[K][NW];
 #pragma unroll
   for (int s = 0; s < kWin; ++s) load(shard(sid[s]), x[s]);
+  if constexpr (kLds && (POL & kCoefBytes) != 0) {
+    Tab* lt = wave_tabs_lds<kSliceTabs>();
+    const uint32_t ncoef = tab_pieces / 2u;
+#pragma unroll
+    for (int j = 0; j < kCoefIter; ++j) {
+      const uint32_t i = lane + 64u * j;
+      if (i < ncoef) {
+        const TabWords w = tab_words(coef[j]);
+        lt[i] = Tab{w.t0lo, w.t0hi, w.t1lo, w.t1hi, w.t2, coef[j], 0u, 0u};
+      }
+    }
+  }
   const Tab* rt = tabs + m0 * K;  // rows of this pass: entry (m, s) at rt[m * K + s]
   if constexpr (kWinPath) {
     const Tab* lt = rt;
@@ -691,7 +734,7 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
         }
       }
 #pragma unroll
-      for (int m = 0; m < NR; ++m) store(og + erased(m0 + m) * static_cast<uint64_t>(P), acc[m]);
+      for (int m = 0; m < NR; ++m) store(dest(m0 + m, erased(m0 + m)), acc[m]);
     };
     for_row_count<MAXE>(e - m0 < MAXE ? e - m0 : MAXE, rebuild);
     return;
@@ -732,7 +775,7 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
   }
 #pragma unroll
   for (int m = 0; m < MAXE; ++m)
-    if (m0 + m < e) store(og + erased(m0 + m) * static_cast<uint64_t>(P), acc[m]);
+    if (m0 + m < e) store(dest(m0 + m, erased(m0 + m)), acc[m]);
 }
 
 template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false, bool INLINE = DIRECT, int SCAN = 0>
@@ -1323,7 +1366,7 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, b
     return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore, NMM, NTT, false>(a, s);
 #define QFEC_FUSED_L(KK, RR, NMM, NTT)                                                        \
   if (!direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                            \
-    return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore | kLdsTabs, NMM, NTT, false>(a, s);
+    return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore | kLdsTabs | kCoefBytes, NMM, NTT, false>(a, s);
 #define QFEC_FUSED_P(M, KK, RR)                                                               \
   M(KK, RR, 0, 2) M(KK, RR, 0, 3) M(KK, RR, 0, 4) M(KK, RR, 1, 0) M(KK, RR, 1, 1)            \
   M(KK, RR, 1, 2) M(KK, RR, 1, 3) M(KK, RR, 1, 4)
@@ -1382,8 +1425,19 @@ bool decode_direct_form(const DecodeLaunch& a) {
 
 bool decode_needs_rec_off(const DecodeLaunch& a) { return a.groups > 0 && !decode_direct_form(a); }
 
+// The record-addressed LDS-table forms (QFEC_FUSED_L: k=20 r=5, 256 < P < 2048) read compact
+// codebooks; every other form reads CoefEntry records.
+bool decode_compact_tables(const DecodeLaunch& a) {
+  if (a.groups == 0 || a.P < kVecMinP || a.rec_ready || decode_tiled_form(a) || decode_direct_form(a)) return false;
+  if (a.variant != kDecodeFused && a.variant != kDecodeAuto && a.variant != kDecodeFusedDirect) return false;
+  const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
+  return a.k == 20 && a.r == 5 && ((nm == 0 && nt >= 2) || nm == 1);
+}
+
 hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
   if (a.groups == 0) return hipSuccess;
+  // the codebook's format must be the one the chosen form reads
+  if (a.compact_tables != decode_compact_tables(a)) return hipErrorInvalidValue;
   const uint32_t tile = a.P >= kVecMinP ? pick_tile((a.P + 15u) / 16u, a.k, a.P) : 0u;
   const bool tiled = decode_tiled_form(a);
   if (decode_direct_form(a)) return try_decode_fused(a, s, true);

@@ -86,6 +86,9 @@ struct DecodeLaunch {
   // of the waves that find nothing to do (0.257 -> 0.243 ms per 1M groups,
   // profiles/r02_probe_decode_scan.txt).  The host paths that know the masks pick it.
   uint32_t scan = 1;
+  // `codebook` holds coefficient bytes (compact layout, gf256.hpp) rather than CoefEntry
+  // tables: set exactly when decode_compact_tables(*this) (launch_decode checks).
+  bool compact_tables = false;
 };
 
 constexpr uint32_t kDecodeScanGroups = 8;
@@ -100,6 +103,8 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s);
 // Whether launch_decode(a) uses the rec_off workspace (every form but the mask-addressed
 // one, which classifies inline).  The caller then provides a workspace private to the call.
 bool decode_needs_rec_off(const DecodeLaunch& a);
+// Whether launch_decode(a) runs a form that reads a compact codebook (coefficient bytes).
+bool decode_compact_tables(const DecodeLaunch& a);
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);
 

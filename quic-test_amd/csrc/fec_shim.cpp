@@ -112,6 +112,8 @@ struct DecodePlan {
   bool dense = false;          // dense codebook of every pattern (else: sparse per call)
   qfec::CodebookLayout layout;
   DevBuf codebook;
+  qfec::CodebookLayout clayout;  // compact (coefficient-byte) book, built on first use
+  DevBuf cbook;
   std::vector<uint8_t> M;      // parity matrix, for sparse per-call records
   DevBuf sparse_book;          // the last sparse call's records
 };
@@ -487,6 +489,25 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   a.r = r;
   a.P = P;
   a.rec_ready = !plan->dense;
+  if (plan->dense && qfec::decode_compact_tables(a)) {
+    // the form reads bare coefficient bytes: the compact book of the same patterns
+    if (!plan->cbook.ptr) {
+      std::vector<uint8_t> book;
+      if (!qfec::codebook_layout(k, r, kCodebookCap, plan->clayout, /*compact=*/true) ||
+          !qfec::build_codebook(plan->clayout, plan->M, book)) {
+        set_error("decode: compact codebook failed for k=%u r=%u", k, r);
+        return FEC_ERR_RANGE;
+      }
+      QFEC_HIP(plan->cbook.ensure(book.size()));
+      QFEC_HIP(hipMemcpy(plan->cbook.ptr, book.data(), book.size(), hipMemcpyHostToDevice));
+    }
+    a.compact_tables = true;
+    a.codebook = plan->cbook.as<uint8_t>();
+    for (uint32_t e = 1; e <= 32; ++e) {
+      a.meta.base[e] = plan->clayout.level_base[e];
+      a.meta.stride[e] = plan->clayout.level_stride[e];
+    }
+  }
   // Groups per wave of the mask-addressed form: the scan form when the caller knows that
   // few groups need a rebuild (need_share, from a host scan of the masks); device-resident
   // callers get one wave per group unless QUICFEC_DECODE_SCAN asks otherwise (tuning).

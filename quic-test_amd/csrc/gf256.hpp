@@ -164,6 +164,8 @@ inline uint64_t colex_rank(const uint32_t* c, uint32_t n) {
 //   [96]       e
 //   [97]       1 if every coefficient is 1 (single loss rebuilt from parity row 0: XOR)
 //   [128, ...) e x k CoefEntry, row m (output E_m) major, survivor slot s minor
+//              (compact books: e x k coefficient bytes instead, same order, padded to 32;
+//              the kernels that read them compute the tables, coef_tables.hpp)
 //
 // Rebuild (syndrome form): with Inv = (M[R][E])^-1,
 //   d_{E_m} = sum_t Inv[m][t] * p_{R_t}  ^  sum_{j in S} (sum_t Inv[m][t] * M[R_t][j]) * d_j
@@ -175,23 +177,29 @@ constexpr uint32_t kMaxDecodeShards = 64;  // k + r <= 64 (u64 erasure masks)
 
 struct CodebookLayout {
   uint32_t k = 0, r = 0;
+  bool compact = false;                                  // coefficient bytes, not CoefEntry
   uint64_t level_base[kMaxDecodeShards + 1] = {};   // byte offset of level e
   uint64_t level_stride[kMaxDecodeShards + 1] = {}; // record bytes at level e
   uint64_t level_count[kMaxDecodeShards + 1] = {};  // records at level e
   uint64_t total_bytes = 0;
 };
 
-inline bool codebook_layout(uint32_t k, uint32_t r, uint64_t cap_bytes, CodebookLayout& L) {
+inline uint64_t record_bytes(uint32_t k, uint32_t e, bool compact = false) {
+  return kRecordHeader + (compact ? (uint64_t(e) * k + 31) / 32 * 32 : uint64_t(e) * k * sizeof(CoefEntry));
+}
+
+inline bool codebook_layout(uint32_t k, uint32_t r, uint64_t cap_bytes, CodebookLayout& L, bool compact = false) {
   if (k == 0 || r == 0 || k + r > kMaxDecodeShards) return false;
   L = CodebookLayout();
   L.k = k;
   L.r = r;
+  L.compact = compact;
   uint64_t off = 0;
   for (uint32_t e = 1; e <= r && e <= k; ++e) {
     const uint64_t ce = binom().c[k][e], cr = binom().c[r][e];
     if (ce == UINT64_MAX || cr == UINT64_MAX) return false;
     const long double cnt = (long double)ce * (long double)cr;
-    const uint64_t stride = kRecordHeader + uint64_t(e) * k * sizeof(CoefEntry);
+    const uint64_t stride = record_bytes(k, e, compact);
     if (cnt * stride + off > (long double)cap_bytes) return false;
     L.level_base[e] = off;
     L.level_stride[e] = stride;
@@ -218,15 +226,11 @@ inline void for_each_subset(uint32_t n, uint32_t e, F&& f) {
   }
 }
 
-inline uint64_t record_bytes(uint32_t k, uint32_t e) {
-  return kRecordHeader + uint64_t(e) * k * sizeof(CoefEntry);
-}
-
 // Write the record of pattern (E, R) (sorted, |E| = |R| = e) at `rec` (record_bytes(k, e)
 // bytes, zeroed by the caller).  false on a singular submatrix (cannot happen for this
 // Cauchy construction; kept as a guard).
 inline bool build_record(uint32_t k, const std::vector<uint8_t>& M, const uint32_t* E, const uint32_t* R,
-                         uint32_t e, uint8_t* rec) {
+                         uint32_t e, uint8_t* rec, bool compact = false) {
   const GF256& g = gf();
   // survivors: data not in E ascending, then parity rows R
   uint32_t ns = 0;
@@ -257,7 +261,11 @@ inline bool build_record(uint32_t k, const std::vector<uint8_t>& M, const uint32
         c = inv[m * e + (s - (k - e))];
       }
       all_one &= (c == 1);
-      ent[m * k + s] = make_entry(c);
+      if (compact) {
+        rec[kRecordHeader + m * k + s] = c;
+      } else {
+        ent[m * k + s] = make_entry(c);
+      }
     }
   }
   rec[97] = all_one ? 1 : 0;
@@ -276,7 +284,7 @@ inline bool build_codebook(const CodebookLayout& L, const std::vector<uint8_t>& 
       const uint64_t rankE = colex_rank(E, e);
       for_each_subset(r, e, [&](const uint32_t* R) {
         const uint64_t idx = rankE * cr + colex_rank(R, e);
-        ok &= build_record(k, M, E, R, e, out.data() + L.level_base[e] + idx * L.level_stride[e]);
+        ok &= build_record(k, M, E, R, e, out.data() + L.level_base[e] + idx * L.level_stride[e], L.compact);
       });
     });
   }

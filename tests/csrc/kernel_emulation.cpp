@@ -11,6 +11,7 @@
 #include <random>
 #include <vector>
 
+#include "coef_tables.hpp"
 #include "gf256.hpp"
 
 extern "C" {
@@ -58,6 +59,38 @@ static int fail(const char* what, int a, int b, int c) {
 int main() {
   std::mt19937_64 rng(12345);
   int cases = 0;
+  // The tables kernels build from a bare coefficient (kCoefBytes, coef_tables.hpp) are the
+  // host's make_entry tables, for every coefficient.
+  for (uint32_t c = 0; c < 256; ++c) {
+    const CoefEntry e = qfec::make_entry(static_cast<uint8_t>(c));
+    const qfec::TabWords w = qfec::tab_words(c);
+    if (w.t0lo != e.t0lo || w.t0hi != e.t0hi || w.t1lo != e.t1lo || w.t1hi != e.t1hi || w.t2 != e.t2)
+      return fail("tab_words", int(c), 0, 0);
+    ++cases;
+  }
+  // A compact codebook holds exactly the coefficients of the full one, record for record.
+  for (auto kr : {std::pair<uint32_t, uint32_t>{20, 5}, {10, 3}, {7, 4}}) {
+    const uint32_t k = kr.first, r = kr.second;
+    std::vector<uint8_t> M, full, comp;
+    qfec::parity_matrix(k, r, M);
+    qfec::CodebookLayout Lf, Lc;
+    qfec::codebook_layout(k, r, 2ull << 30, Lf);
+    qfec::codebook_layout(k, r, 2ull << 30, Lc, true);
+    qfec::build_codebook(Lf, M, full);
+    qfec::build_codebook(Lc, M, comp);
+    for (uint32_t e = 1; e <= r; ++e) {
+      if (Lc.level_count[e] != Lf.level_count[e] || Lc.level_stride[e] % 32 != 0) return fail("compact layout", int(k), int(r), int(e));
+      for (uint64_t i = 0; i < Lf.level_count[e]; ++i) {
+        const uint8_t* a = full.data() + Lf.level_base[e] + i * Lf.level_stride[e];
+        const uint8_t* b = comp.data() + Lc.level_base[e] + i * Lc.level_stride[e];
+        if (std::memcmp(a, b, qfec::kRecordHeader) != 0) return fail("compact header", int(k), int(e), int(i));
+        const CoefEntry* ent = reinterpret_cast<const CoefEntry*>(a + qfec::kRecordHeader);
+        for (uint32_t t = 0; t < e * k; ++t)
+          if (b[qfec::kRecordHeader + t] != ent[t].coef) return fail("compact coef", int(k), int(e), int(t));
+      }
+    }
+    ++cases;
+  }
   // every product of the multiply tables against the field definition
   for (int c = 0; c < 256; ++c) {
     const CoefEntry e = qfec::make_entry(uint8_t(c));
