@@ -94,6 +94,18 @@ int fec_decode_batch_rs_dev(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* 
                             const uint64_t* d_erasure_masks, uint64_t num_groups, uint32_t k,
                             uint32_t r, uint32_t packet_size, uint8_t* d_status, void* stream);
 
+/* Recover: decode without touching d_data.  The rebuilt data shards of group g go to
+ * d_rebuilt + (g*r + m)*P, m = 0..e-1 over the group's lost data shards in ascending shard
+ * order -- the reference decoder hands recovered packets back as separate buffers
+ * (decoder.go:29-34 Recovered{PacketID, Data}, :170-178), and a device-resident receiver
+ * consumes them the same way.  d_rebuilt holds num_groups*r*P bytes; slots m >= e of a
+ * group, and all slots of an unrecoverable group, are left unwritten.  Writing the rebuilt
+ * packets back to back (the write pattern of encode's parity rows) instead of scattered
+ * among the data shards measured 2.32 vs 2.47 ms at k=10 r=3, 2 erasures, 1M groups. */
+int fec_recover_batch_rs_dev(FECEncoderCtx* ctx, const uint8_t* d_data, const uint8_t* d_parity,
+                             const uint64_t* d_erasure_masks, uint64_t num_groups, uint32_t k, uint32_t r,
+                             uint32_t packet_size, uint8_t* d_rebuilt, uint8_t* d_status, void* stream);
+
 /* Build (and upload) the decode codebook for (k, r) ahead of the first decode.  The
  * codebook holds the recovery tables of every recoverable erasure pattern; its size is
  * returned in *bytes_out (nullable).  When it would exceed the 2 GiB cap (e.g. k=16 r=16)

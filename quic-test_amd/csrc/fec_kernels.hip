@@ -60,9 +60,11 @@ constexpr int kLdsTabs = 64;
 constexpr int kProbeWin10 = 128;  // probes only: kLdsTabs survivor window of 10 (default 6)
 constexpr int kProbeWin14 = 256;  // probes only: window of 14
 constexpr int kProbeWindowed = 512;  // probes only: windowed body, tables from the record
-// decode_fused: rebuilt shard m of group g goes to out + (g * MAXE + m) * P (one contiguous
-// run of rebuilt packets per group, groups back to back, like encode's parity rows) instead
-// of its place among the group's data shards.
+// decode_fused / decode_wave: the m-th rebuilt shard of group g (erased data shards in
+// ascending order) goes to out + (g * r + m) * P -- one contiguous run of rebuilt packets
+// per group, groups back to back, like encode's parity rows -- instead of its place among
+// the group's data shards (fec_recover_batch_rs_dev).  Measured at k=10 r=3, 2 erasures:
+// 2.32 vs 2.47 ms in place (profiles/r02_probe_decode_compact_out.txt).
 constexpr int kCompactOut = 1024;
 // decode_fused with kLdsTabs: the record holds bare coefficient bytes (compact codebook,
 // gf256.hpp) and the wave computes each coefficient's tables into its LDS slice
@@ -398,7 +400,7 @@ __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, co
 #pragma unroll
           for (int q = 0; q < NW; ++q) acc[q] ^= v[b][q];
     }
-    stw<NW, POL>(og + rec_byte(rw, 64) * static_cast<uint64_t>(P) + off, acc);
+    stw<NW, POL>(og + ((POL & kCompactOut) != 0 ? 0u : rec_byte(rw, 64)) * static_cast<uint64_t>(P) + off, acc);
     return;
   }
   uint32_t acc[MAXE][NW];
@@ -455,7 +457,8 @@ __device__ __forceinline__ void decode_piece(const uint32_t* __restrict__ rw, co
 #pragma unroll
   for (int m = 0; m < MAXE; ++m) {
     if (m0 + m < e) {
-      const uint32_t eid = rec_byte(rw, 64 + m0 + m);
+      // in place: at the erased shard; compact (kCompactOut): row m0 + m of the group's run
+      const uint32_t eid = (POL & kCompactOut) != 0 ? m0 + m : rec_byte(rw, 64 + m0 + m);
       stw<NW, POL>(og + eid * static_cast<uint64_t>(P) + off, acc[m]);
     }
   }
@@ -596,7 +599,7 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
   // destination of rebuilt row m (erased data shard `erased(m)`)
   auto dest = [&](uint32_t m, uint32_t eid) -> uint8_t* {
     if constexpr ((POL & kCompactOut) != 0) {
-      return out + (gw * MAXE + m) * static_cast<uint64_t>(P);
+      return out + (gw * r + m) * static_cast<uint64_t>(P);
     } else {
       return og + eid * static_cast<uint64_t>(P);
     }
@@ -883,7 +886,7 @@ __global__ __launch_bounds__(256) void decode_wave(uint8_t* __restrict__ data,
   }
   const uint8_t* dg = data + gw * k * static_cast<uint64_t>(P);
   const uint8_t* pg = parity + gw * r * static_cast<uint64_t>(P);
-  uint8_t* og = out + gw * k * static_cast<uint64_t>(P);
+  uint8_t* og = out + gw * ((POL & kCompactOut) != 0 ? r : k) * static_cast<uint64_t>(P);
   const uint32_t main_end = P & ~1023u;
   for (uint32_t base = 0; base < main_end; base += 1024u)
     decode_piece<K, MAXE, POL, 4>(rw, tabs, dg, pg, og, k, P, base + lane * 16u, e, m0, xor_only);
@@ -1052,7 +1055,8 @@ __global__ __launch_bounds__(256) void decode_bytes(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ rec_off,
                                                     const uint8_t* __restrict__ codebook,
                                                     uint64_t g_first, uint32_t nthreads, uint32_t P,
-                                                    uint32_t k, uint32_t r, uint8_t* __restrict__ out) {
+                                                    uint32_t k, uint32_t r, uint8_t* __restrict__ out,
+                                                    uint32_t compact) {
   const uint32_t t = blockIdx.x * 256u + threadIdx.x;
   if (t >= nthreads) return;
   const uint32_t gl = t / P;
@@ -1073,7 +1077,8 @@ __global__ __launch_bounds__(256) void decode_bytes(const uint8_t* __restrict__ 
       acc ^= gmul_byte(x, tabs[m * k + s]);
     }
     // Erased shards are never survivors, so writing here cannot feed a later read.
-    out[(g * k + recp[64 + m]) * static_cast<uint64_t>(P) + b] = static_cast<uint8_t>(acc);
+    const uint64_t slot = compact ? g * r + m : g * k + recp[64 + m];
+    out[slot * static_cast<uint64_t>(P) + b] = static_cast<uint8_t>(acc);
   }
 }
 
@@ -1295,7 +1300,7 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
       hipLaunchKernelGGL((decode_wave<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                          a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
-                         a.k, a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u,
+                         a.k, a.r, m0, (a.out ? a.out : a.data) + g0 * ((POL & kCompactOut) != 0 ? a.r : a.k) * static_cast<uint64_t>(a.P), 0u,
                          decode_swizzle(a, kDecodeWaveXcdSwizzle), slice);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
@@ -1325,7 +1330,7 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
       hipLaunchKernelGGL((decode_fused<K, MAXE, POL, NM, NT, DIRECT, INLINE, SCAN>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                          a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
-                         a.r, m0, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P), 0u,
+                         a.r, m0, (a.out ? a.out : a.data) + g0 * ((POL & kCompactOut) != 0 ? a.r : a.k) * static_cast<uint64_t>(a.P), 0u,
                          decode_swizzle(a, kDecodeFusedXcdSwizzle), DIRECT ? a.masks + g0 : nullptr, rm,
                          INLINE && a.status ? a.status + g0 : nullptr);
       const hipError_t e = hipGetLastError();
@@ -1351,22 +1356,27 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
 hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, bool dry = false) {
   const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
 #define QFEC_FUSED_D(KK, RR, NMM, NTT)                                                        \
-  if (direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                             \
+  if (direct && !a.compact_out && a.k == KK && a.r == RR && nm == NMM && nt == NTT)           \
     return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true>(a, s);
-  // k=10 r=3 (the BASELINE shape) also has the scan form, for sparse loss (DecodeLaunch::scan)
+  // k=10 r=3 (the BASELINE shape) also has the scan form, for sparse loss (DecodeLaunch::scan),
+  // and the compact-output form (DecodeLaunch::compact_out)
 #define QFEC_FUSED_DS(KK, RR, NMM, NTT)                                                       \
   if (direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT) {                           \
     if (dry) return hipSuccess;                                                               \
+    if (a.compact_out)                                                                        \
+      return run_decode_fused<KK, RR, kNtStore | kNtLoad | kCompactOut, NMM, NTT, true>(a, s); \
     if (a.scan == kDecodeScanGroups)                                                          \
       return run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true, true, kDecodeScanGroups>(a, s); \
     return run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true>(a, s);                \
   }
 #define QFEC_FUSED_R(KK, RR, NMM, NTT)                                                        \
-  if (!direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                            \
+  if (!direct && !a.compact_out && a.k == KK && a.r == RR && nm == NMM && nt == NTT)          \
     return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore, NMM, NTT, false>(a, s);
 #define QFEC_FUSED_L(KK, RR, NMM, NTT)                                                        \
   if (!direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                            \
-    return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore | kLdsTabs | kCoefBytes, NMM, NTT, false>(a, s);
+    return dry ? hipSuccess                                                                   \
+           : a.compact_out ? run_decode_fused<KK, RR, kNtStore | kLdsTabs | kCoefBytes | kCompactOut, NMM, NTT, false>(a, s) \
+                           : run_decode_fused<KK, RR, kNtStore | kLdsTabs | kCoefBytes, NMM, NTT, false>(a, s);
 #define QFEC_FUSED_P(M, KK, RR)                                                               \
   M(KK, RR, 0, 2) M(KK, RR, 0, 3) M(KK, RR, 0, 4) M(KK, RR, 1, 0) M(KK, RR, 1, 1)            \
   M(KK, RR, 1, 2) M(KK, RR, 1, 3) M(KK, RR, 1, 4)
@@ -1407,6 +1417,7 @@ hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s)
 }
 
 bool decode_tiled_form(const DecodeLaunch& a) {
+  if (a.compact_out) return false;  // in-place only; compact output runs the wave forms
   const uint32_t tile = a.P >= kVecMinP ? pick_tile((a.P + 15u) / 16u, a.k, a.P) : 0u;
   return tile > 0 && ((a.variant == kDecodeAuto && a.P <= kTiledMaxP) || a.variant == kDecodeTiledPlain ||
                       a.variant == kDecodeTiledNt);
@@ -1455,11 +1466,20 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
       const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
       const uint32_t n = static_cast<uint32_t>(gn * a.P);
       hipLaunchKernelGGL(decode_bytes, dim3(blocks_for(n)), dim3(256), 0, s, a.data, a.parity,
-                         a.rec_off, a.codebook, g0, n, a.P, a.k, a.r, a.out ? a.out : a.data);
+                         a.rec_off, a.codebook, g0, n, a.P, a.k, a.r, a.out ? a.out : a.data,
+                         a.compact_out ? 1u : 0u);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
+  }
+  if (a.compact_out) {
+    // fused forms were tried above; everything else: the runtime-k wave kernel, compact
+    if (a.variant == kDecodeFused || a.variant == kDecodeAuto || a.variant == kDecodeFusedDirect) {
+      const hipError_t e = try_decode_fused(a, s, false);
+      if (e != hipErrorNotSupported) return e;
+    }
+    return run_decode_wave<0, 8, kNtStore | kNoCoefBranch | kCompactOut>(a, s);
   }
   const bool separate_out = a.out != nullptr && a.out != a.data;  // decode_v16 lacks it
   if (tiled) {

@@ -89,6 +89,9 @@ struct DecodeLaunch {
   // `codebook` holds coefficient bytes (compact layout, gf256.hpp) rather than CoefEntry
   // tables: set exactly when decode_compact_tables(*this) (launch_decode checks).
   bool compact_tables = false;
+  // Rebuilt shards go to out + (g * r + m) * P (m-th lost data shard of group g, ascending),
+  // `data` is only read (fec_recover_batch_rs_dev); else in place / at `out` like `data`.
+  bool compact_out = false;
 };
 
 constexpr uint32_t kDecodeScanGroups = 8;

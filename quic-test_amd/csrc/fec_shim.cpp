@@ -465,7 +465,7 @@ struct StreamScratch {
 int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
                       const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
                       uint8_t* d_status, hipStream_t s, DevBuf* rec = nullptr,
-                      uint8_t* d_out = nullptr, double need_share = -1.0) {
+                      uint8_t* d_out = nullptr, double need_share = -1.0, bool compact_out = false) {
   DecodePlan* plan = nullptr;
   int rc = get_decode_plan(ctx, k, r, &plan);
   if (rc != FEC_OK) return rc;
@@ -475,6 +475,7 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   a.masks = d_masks;
   a.rec_off = nullptr;
   a.out = d_out;
+  a.compact_out = compact_out;
   a.status = d_status;
   a.codebook = plan->codebook.as<uint8_t>();
   a.binom = ctx->d_binom.as<uint64_t>();
@@ -1337,6 +1338,29 @@ QFEC_EXPORT int fec_decode_batch_rs_dev(FECEncoderCtx* ctx, uint8_t* d_data, con
                                         uint32_t P, uint8_t* d_status, void* stream) {
   g_last_error.clear();
   return record_ctx_error(ctx, fec_decode_batch_rs_dev_impl(ctx, d_data, d_parity, d_masks, G, k, r, P, d_status, stream));
+}
+
+static int fec_recover_batch_rs_dev_impl(FECEncoderCtx* ctx, const uint8_t* d_data, const uint8_t* d_parity,
+                                         const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
+                                         uint8_t* d_rebuilt, uint8_t* d_status, void* stream) {
+  if (!ctx || !d_data || !d_parity || !d_masks || !d_rebuilt) return FEC_ERR_NULL;
+  int rc = check_shape(G, k, r, P, true);
+  if (rc != FEC_OK) return rc;
+  if (G == 0) return FEC_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return FEC_ERR_NODEV;
+  // the kernels only read `data` when the output is compact
+  return decode_dev_locked(ctx, const_cast<uint8_t*>(d_data), d_parity, d_masks, G, k, r, P, d_status,
+                           pick_stream(ctx, stream), nullptr, d_rebuilt, -1.0, /*compact_out=*/true);
+}
+
+QFEC_EXPORT int fec_recover_batch_rs_dev(FECEncoderCtx* ctx, const uint8_t* d_data, const uint8_t* d_parity,
+                                         const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
+                                         uint8_t* d_rebuilt, uint8_t* d_status, void* stream) {
+  g_last_error.clear();
+  return record_ctx_error(ctx, fec_recover_batch_rs_dev_impl(ctx, d_data, d_parity, d_masks, G, k, r, P, d_rebuilt,
+                                                             d_status, stream));
 }
 
 static int fec_decode_prepare_impl(FECEncoderCtx* ctx, uint32_t k, uint32_t r, uint64_t* bytes_out) {

@@ -40,7 +40,7 @@ REFERENCE_SYMBOLS = (
 HIP_SYMBOLS = (
     "fec_hip_device_count", "fec_hip_last_error", "fec_ctx_last_error", "fec_encoder_new_device", "fec_encoder_device",
     "fec_hip_version", "fec_parity_matrix", "fec_encode_batch_rs", "fec_decode_batch_rs",
-    "fec_encode_batch_rs_dev", "fec_decode_batch_rs_dev", "fec_decode_prepare",
+    "fec_encode_batch_rs_dev", "fec_decode_batch_rs_dev", "fec_recover_batch_rs_dev", "fec_decode_prepare",
     "fec_fill_random_dev", "fec_synchronize", "fec_decode_loss_hint",
     "fec_group_new", "fec_group_free", "fec_group_size", "fec_group_context",
     "fec_group_encode_batch_rs", "fec_group_decode_batch_rs",
@@ -105,6 +105,7 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
         "fec_decode_batch_rs": (_int, [_vp, _vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp]),
         "fec_encode_batch_rs_dev": (_int, [_vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp]),
         "fec_decode_batch_rs_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp]),
+        "fec_recover_batch_rs_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp, _vp]),
         "fec_decode_prepare": (_int, [_vp, _u32, _u32, ctypes.POINTER(_u64)]),
         "fec_fill_random_dev": (_int, [_vp, _vp, _u64, _u64, _u64, _vp]),
         "fec_synchronize": (_int, [_vp]),
@@ -241,6 +242,15 @@ class Context:
                                               num_groups, k, r, packet_size,
                                               _ptr(d_status) if d_status is not None else None, stream)
         _check(rc, "fec_decode_batch_rs_dev")
+
+    def recover_dev(self, d_data, d_parity, d_masks, num_groups: int, k: int, r: int, packet_size: int,
+                    d_rebuilt, d_status=None, stream: Optional[int] = None) -> None:
+        """Rebuilt shards of group g at d_rebuilt[(g*r + m)*P:...], m over the lost data shards
+        in ascending order; d_data is not modified."""
+        rc = self.lib.fec_recover_batch_rs_dev(self.handle, _ptr(d_data), _ptr(d_parity), _ptr(d_masks),
+                                               num_groups, k, r, packet_size, _ptr(d_rebuilt),
+                                               _ptr(d_status) if d_status is not None else None, stream)
+        _check(rc, "fec_recover_batch_rs_dev")
 
     def decode_prepare(self, k: int, r: int) -> int:
         n = ctypes.c_uint64(0)

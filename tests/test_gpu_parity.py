@@ -628,3 +628,41 @@ def test_device_decode_scan_form(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, l
     assert np.array_equal(st.cpu().numpy(), st_exp)
     assert int((st_exp != 0).sum()) == bad_exp
     assert np.array_equal(dd.cpu().numpy(), ref)
+
+
+RECOVER_SHAPES = [(10, 3, 1200), (10, 3, 700), (10, 3, 1400), (20, 5, 1200), (20, 5, 96), (4, 2, 256), (7, 4, 48),
+                  (12, 9, 64), (10, 1, 1200), (5, 3, 33), (3, 2, 7), (30, 20, 32), (10, 3, 2500)]
+
+
+@pytest.mark.parametrize("k,r,P", RECOVER_SHAPES)
+def test_recover_compact_output(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
+    """fec_recover_batch_rs_dev: the m-th lost data shard of group g lands at
+    rebuilt[(g*r + m)*P], bit-exact vs the oracle; data is not modified; slots past e and
+    unrecoverable groups stay unwritten; statuses match."""
+    torch = torch_cuda
+    G = 1031
+    rng = np.random.default_rng(k * 100 + r * 10 + P)
+    data = oracle_mod.splitmix_bytes(G * k * P, SEED + 51 + k + P)
+    par = oracle_mod.rs_encode(data, G, k, r, P, nthreads=8)
+    masks = np.zeros(G, dtype=np.uint64)
+    for g in range(G):
+        for s in rng.permutation(k + r)[: rng.integers(0, r + 2)]:
+            masks[g] |= np.uint64(1) << np.uint64(int(s))
+    lost = ((masks[:, None] >> np.arange(k, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+    broken = data.copy().reshape(G, k, P)
+    broken[lost] = 0xEE
+    ref = broken.copy().reshape(-1)
+    bad_exp, st_exp = oracle_mod.rs_decode(ref, par, masks, G, k, r, P, nthreads=8)
+    exp = np.full((G, r, P), 0x5A, dtype=np.uint8)
+    ref3 = ref.reshape(G, k, P)
+    for g in np.nonzero(st_exp == 0)[0]:
+        for m, j in enumerate(np.nonzero(lost[g])[0]):
+            exp[g, m] = ref3[g, j]
+    dd, dp, dm = _dev(torch, broken.reshape(-1)), _dev(torch, par), _dev(torch, masks.view(np.int64))
+    out = torch.full((G * r * P,), 0x5A, dtype=torch.uint8, device="cuda")
+    st = torch.full((G,), 7, dtype=torch.uint8, device="cuda")
+    gpu_ctx.recover_dev(dd, dp, dm, G, k, r, P, out, st)
+    gpu_ctx.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_exp)
+    assert np.array_equal(out.cpu().numpy().reshape(G, r, P), exp)
+    assert np.array_equal(dd.cpu().numpy(), broken.reshape(-1))     # data untouched
