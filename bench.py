@@ -8,8 +8,11 @@
 Workload (one "step" = one pass of the hot path over one batch):
   c2c3 (default; BASELINE.json configs[1] + configs[2]): per GPU 1,000,000 groups of
        k=10 data packets x 1200 B (12.0 GB resident in HBM).  A step encodes every group
-       (r=3 parity rows) and then rebuilds, in place, every group with 2 erased shards
-       (positions uniform over the 13 shards, seeded).  value = payload GiB (k*P*G, all
+       (r=3 parity rows) and then rebuilds every group with 2 erased shards (positions
+       uniform over the 13 shards, seeded): fec_recover_batch_rs_dev returns the rebuilt
+       packets back to back, as the reference decoder returns Recovered buffers
+       (decoder.go:29-34); --decode-api in-place rebuilds them inside the data instead (both
+       timed, the other one as kernels.decode.other_api).  value = payload GiB (k*P*G, all
        ranks) / step time: the rate at which data goes through encode AND decode.
   c4   (configs[3]): per GPU 1,000,000 groups of k=20 x 1200 B, r=5 encode only.
 
@@ -478,6 +481,9 @@ def main() -> int:
                     help="k,r,P override of the config's code shape (tuning sweeps; not the headline)")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-resident path (pinned buffers, H2D -> kernel -> D2H)")
+    ap.add_argument("--decode-api", default="recover", choices=("recover", "in-place"),
+                    help="recover: fec_recover_batch_rs_dev (rebuilt packets returned back to back, as the "
+                         "reference decoder returns Recovered buffers); in-place: fec_decode_batch_rs_dev")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -522,6 +528,15 @@ def main() -> int:
     # this rank's slice of one global synthetic stream
     ctx.fill_random_dev(data, data.numel(), SEED + 2, byte_offset=g0 * k * P, stream=sp)
     dec_bytes = 0
+    recover = cfg["decode"] and args.decode_api == "recover"
+    rebuilt = torch.empty(G * r * P, dtype=torch.uint8, device="cuda") if recover else None
+
+    def decode_call(api: str, status=None):
+        if api == "recover":
+            ctx.recover_dev(data, parity, masks, G, k, r, P, rebuilt, status, stream=sp)
+        else:
+            ctx.decode_dev(data, parity, masks, G, k, r, P, status, stream=sp)
+
     if cfg["decode"]:
         masks_h = make_masks(cfg, G, SEED + 3 + rank)
         dec_bytes = decode_algorithmic_bytes(masks_h, k, r, P)
@@ -544,14 +559,23 @@ def main() -> int:
             lost = ((masks.view(G, 1) >> bits.view(1, k)) & 1).bool()
             data.view(G, k, P)[lost] = 0xEE
             st = torch.zeros(G, dtype=torch.uint8, device="cuda")
-            ctx.decode_dev(data, parity, masks, G, k, r, P, st, stream=sp)
+            decode_call(args.decode_api, st)
             torch.cuda.synchronize()
             bad_exp = unrecoverable_count(masks_h, k, r)
             n_bad = int(st.sum().item())
-            if n_bad == 0:
+            ok_rows = st == 0
+            if recover:
+                # slot m of group g = its m-th lost data shard: the same (g, j ascending) order
+                # as boolean indexing of the lost shards
+                e_g = lost.sum(dim=1, keepdim=True)
+                slots = torch.arange(r, device="cuda").view(1, r) < e_g
+                got = rebuilt.view(G, r, P)[slots & ok_rows.view(G, 1)]
+                want = orig.view(G, k, P)[lost & ok_rows.view(G, 1)]
+                verified = bool(torch.equal(got, want)) and n_bad == bad_exp
+                data.copy_(orig)
+            elif n_bad == 0:
                 verified = bool(torch.equal(data, orig)) and bad_exp == 0
             else:
-                ok_rows = st == 0
                 verified = bool(torch.equal(data.view(G, -1)[ok_rows], orig.view(G, -1)[ok_rows])) and n_bad == bad_exp
         else:
             torch.cuda.synchronize()
@@ -566,7 +590,7 @@ def main() -> int:
         if ev is not None:
             ev[1].record(stream)
         if cfg["decode"]:
-            ctx.decode_dev(data, parity, masks, G, k, r, P, None, stream=sp)
+            decode_call(args.decode_api)
             if ev is not None:
                 ev[2].record(stream)
 
@@ -607,22 +631,26 @@ def main() -> int:
     # without the write-back of the other kernel's output still draining from the caches
     # when it starts (which the in-step times above include).
     reps = max(5, args.steps // 4)
-    iso = {}
-    for name in kernels:
+
+    def isolated(fn, nbytes):
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
         evs[0].record(stream)
         for i in range(reps):
-            if name == "encode":
-                ctx.encode_dev(data, G, k, r, P, parity, stream=sp)
-            else:
-                ctx.decode_dev(data, parity, masks, G, k, r, P, None, stream=sp)
+            fn()
             evs[i + 1].record(stream)
         torch.cuda.synchronize()
         ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(reps))[reps // 2]
-        iso[name] = {"ms_median": round(ms, 4),
-                     "achieved_GBps": round(kernels[name]["algorithmic_bytes"] / (ms * 1e-3) / 1e9, 1)}
-    for name in kernels:
-        kernels[name]["isolated"] = iso[name]
+        return {"ms_median": round(ms, 4), "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1)}
+
+    kernels["encode"]["isolated"] = isolated(lambda: ctx.encode_dev(data, G, k, r, P, parity, stream=sp), enc_bytes)
+    if cfg["decode"]:
+        kernels["decode"]["api"] = args.decode_api
+        kernels["decode"]["isolated"] = isolated(lambda: decode_call(args.decode_api), dec_bytes)
+        # the other decode API on the same buffers, for comparison (not in `value`)
+        other = "in-place" if recover else "recover"
+        if other == "recover" and rebuilt is None:
+            rebuilt = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
+        kernels["decode"]["other_api"] = {"api": other, **isolated(lambda: decode_call(other), dec_bytes)}
     dom = max(kernels, key=lambda n: kernels[n]["ms"])
     pmc, pmc_note = load_pmc_traffic(args.config)
     pmc = pmc or {}
@@ -652,6 +680,9 @@ def main() -> int:
             "config": {"workload": cfg["workload"], "k": k, "r": r, "packet_bytes": P,
                        "groups_per_gpu": G, "erasures_per_group": cfg["erasures"] or None,
                        "iid_loss": cfg.get("loss"),
+                       "decode_api": (("fec_recover_batch_rs_dev (rebuilt packets back to back, decoder.go Recovered)"
+                                       if args.decode_api == "recover" else "fec_decode_batch_rs_dev (in place)")
+                                      if cfg["decode"] else None),
                        "parallelism": f"group-sharded x{world} (no collective)"},
             "verified": verified,
             "kernels": kernels,
