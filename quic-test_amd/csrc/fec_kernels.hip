@@ -1364,7 +1364,9 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, b
   if (direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT) {                           \
     if (dry) return hipSuccess;                                                               \
     if (a.compact_out)                                                                        \
-      return run_decode_fused<KK, RR, kNtStore | kNtLoad | kCompactOut, NMM, NTT, true>(a, s); \
+      return a.scan == kDecodeScanGroups                                                      \
+                 ? run_decode_fused<KK, RR, kNtStore | kNtLoad | kCompactOut, NMM, NTT, true, true, kDecodeScanGroups>(a, s) \
+                 : run_decode_fused<KK, RR, kNtStore | kNtLoad | kCompactOut, NMM, NTT, true>(a, s); \
     if (a.scan == kDecodeScanGroups)                                                          \
       return run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true, true, kDecodeScanGroups>(a, s); \
     return run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true>(a, s);                \
