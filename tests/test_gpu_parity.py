@@ -666,3 +666,31 @@ def test_recover_compact_output(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
     assert np.array_equal(st.cpu().numpy(), st_exp)
     assert np.array_equal(out.cpu().numpy().reshape(G, r, P), exp)
     assert np.array_equal(dd.cpu().numpy(), broken.reshape(-1))     # data untouched
+
+
+@pytest.mark.parametrize("loss,P", [(0.01, 1200), (0.3, 1400)])
+def test_recover_scan_form(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, loss, P):
+    """fec_recover_batch_rs_dev in the 8-groups-per-wave form (sparse loss): compact rows
+    and statuses equal the oracle's."""
+    monkeypatch.setenv("QUICFEC_DECODE_SCAN", "8")
+    torch = torch_cuda
+    k, r, G = 10, 3, 10_007
+    data = oracle_mod.splitmix_bytes(G * k * P, SEED + 61 + P)
+    par = oracle_mod.rs_encode(data, G, k, r, P, nthreads=8)
+    rng = np.random.default_rng(int(loss * 100) + P)
+    w = np.left_shift(np.uint64(1), np.arange(k + r, dtype=np.uint64))
+    masks = ((rng.random((G, k + r)) < loss) * w).sum(axis=1, dtype=np.uint64)
+    lost = ((masks[:, None] >> np.arange(k, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+    _, st_exp = oracle_mod.rs_decode(_poison(data, masks, G, k, P), par, masks, G, k, r, P, nthreads=8)
+    exp = np.full((G, r, P), 0x5A, dtype=np.uint8)
+    d3 = data.reshape(G, k, P)
+    for g in np.nonzero(st_exp == 0)[0]:
+        for m, j in enumerate(np.nonzero(lost[g])[0]):
+            exp[g, m] = d3[g, j]
+    dd, dp, dm = _dev(torch, data), _dev(torch, par), _dev(torch, masks.view(np.int64))
+    out = torch.full((G * r * P,), 0x5A, dtype=torch.uint8, device="cuda")
+    st = torch.full((G,), 7, dtype=torch.uint8, device="cuda")
+    gpu_ctx.recover_dev(dd, dp, dm, G, k, r, P, out, st)
+    gpu_ctx.synchronize()
+    assert np.array_equal(st.cpu().numpy(), st_exp)
+    assert np.array_equal(out.cpu().numpy().reshape(G, r, P), exp)
