@@ -1377,8 +1377,8 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, b
 #define QFEC_FUSED_L(KK, RR, NMM, NTT)                                                        \
   if (!direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                            \
     return dry ? hipSuccess                                                                   \
-           : a.compact_out ? run_decode_fused<KK, RR, kNtStore | kLdsTabs | kCoefBytes | kCompactOut, NMM, NTT, false>(a, s) \
-                           : run_decode_fused<KK, RR, kNtStore | kLdsTabs | kCoefBytes, NMM, NTT, false>(a, s);
+           : a.compact_out ? run_decode_fused<KK, RR, kNtStore | kNtLoad | kLdsTabs | kCoefBytes | kCompactOut, NMM, NTT, false>(a, s) \
+                           : run_decode_fused<KK, RR, kNtStore | kNtLoad | kLdsTabs | kCoefBytes, NMM, NTT, false>(a, s);
 #define QFEC_FUSED_P(M, KK, RR)                                                               \
   M(KK, RR, 0, 2) M(KK, RR, 0, 3) M(KK, RR, 0, 4) M(KK, RR, 1, 0) M(KK, RR, 1, 1)            \
   M(KK, RR, 1, 2) M(KK, RR, 1, 3) M(KK, RR, 1, 4)

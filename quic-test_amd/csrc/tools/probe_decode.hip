@@ -283,6 +283,11 @@ int main(int argc, char** argv) {
                       probe(b);
                       return run_decode_fused<20, 5, kNtStore | kLdsTabs | kCoefBytes, 1, 1, false>(b, nullptr);
                     }});
+    vars.push_back({"coef-bytes nt-load", kDecodeFused, -1, 1, {}, [probe, with_book](const DecodeLaunch& a) {
+                      const DecodeLaunch b = with_book(a, true);
+                      probe(b);
+                      return run_decode_fused<20, 5, kNtStore | kNtLoad | kLdsTabs | kCoefBytes, 1, 1, false>(b, nullptr);
+                    }});
   }
   // windowed straight-line body (6-deep survivor window) with tables from the record
   if (k == 10 && r == 3 && P == 1200) {
