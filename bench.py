@@ -657,7 +657,7 @@ def main() -> int:
     roofline = {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["achieved_GBps"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(kernels[dom]["achieved_GBps"] / HBM_PEAK_GBS, 4),
-                "traffic": pmc.get(dom, {}).get("hbm_bytes_per_launch"),
+                "traffic": pmc.get("recover" if dom == "decode" and recover else dom, {}).get("hbm_bytes_per_launch"),
                 "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes"],
                 "traffic_source": pmc_note,
                 "timing": "torch.cuda.Event on the launch stream, averaged over the timed steps"}

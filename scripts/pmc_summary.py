@@ -30,8 +30,20 @@ def collect(d: Path, counter: str):
     return vals
 
 
+K_COMPACT_OUT = 1024  # fec_kernels.hip kCompactOut: the recover (rebuilt packets back to back) forms
+
+
 def short(name: str) -> str:
-    for key in ("encode_v16", "decode_fused", "decode_wave", "decode_v16", "decode_tiled", "classify", "fill_words", "encode_bytes", "decode_bytes"):
+    """Summary key of a kernel: encode, recover (decode forms with kCompactOut in their
+    policy template argument), decode (in place), or the kernel's own name."""
+    if "encode_v16" in name:
+        return "encode"
+    for key in ("decode_fused", "decode_wave", "decode_v16", "decode_tiled"):
+        if key in name:
+            args = name.split(key + "<", 1)[1].split(">", 1)[0].split(",")
+            pol = int(args[2]) if len(args) > 2 and args[2].strip().isdigit() else 0
+            return "recover" if pol & K_COMPACT_OUT else "decode"
+    for key in ("classify", "fill_words", "encode_bytes", "decode_bytes"):
         if key in name:
             return key
     return name[:40]
@@ -60,8 +72,7 @@ def main():
             entry["hbm_read_bytes_per_launch"] = int(fk * 1024 * 2)
             entry["hbm_write_bytes_per_launch"] = int(wk * 1024)
             entry["hbm_bytes_per_launch"] = entry["hbm_read_bytes_per_launch"] + entry["hbm_write_bytes_per_launch"]
-        key = {"encode_v16": "encode", "decode_fused": "decode", "decode_tiled": "decode", "decode_wave": "decode", "decode_v16": "decode"}.get(s, s)
-        res[key] = entry
+        res[s] = entry
     out.write_text(json.dumps(res, indent=1))
     print(json.dumps(res, indent=1))
 
