@@ -71,6 +71,11 @@ constexpr int kCompactOut = 1024;
 // (coef_tables.hpp) instead of copying 32-byte table entries in: k=20 r=5 records shrink
 // from up to 3.3 KB to 256 B, the whole codebook from 143 MB to 12 MB.
 constexpr int kCoefBytes = 2048;
+// encode_v16: coefficients taken two at a time, so every 3-input XOR (v_bitop3) folds two
+// new table products into the accumulator: 6 v_perm + 3 v_bitop3 per pair of coefficients
+// and dword instead of 6 v_perm + 2 v_bitop3 + 2 v_xor, and one v_bitop3 per pair on the
+// XOR row instead of two v_xor.
+constexpr int kPairMac = 4096;
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
@@ -117,6 +122,32 @@ __device__ __forceinline__ void mac(u32x4& acc, const Sel& s, const Tab& t) {
 }
 
 __device__ __forceinline__ void xor_into(u32x4& acc, const u32x4& x) { acc ^= x; }
+
+// acc ^= a*ta ^ b*tb (two coefficients, see kPairMac)
+__device__ __forceinline__ uint32_t mac2_dword(uint32_t acc, uint32_t sa0, uint32_t sa1, uint32_t sa2, const Tab& ta,
+                                               uint32_t sb0, uint32_t sb1, uint32_t sb2, const Tab& tb) {
+  const uint32_t a0 = __builtin_amdgcn_perm(ta.t0hi, ta.t0lo, sa0);
+  const uint32_t a1 = __builtin_amdgcn_perm(ta.t1hi, ta.t1lo, sa1);
+  const uint32_t a2 = __builtin_amdgcn_perm(ta.t2, ta.t2, sa2);
+  const uint32_t b0 = __builtin_amdgcn_perm(tb.t0hi, tb.t0lo, sb0);
+  const uint32_t b1 = __builtin_amdgcn_perm(tb.t1hi, tb.t1lo, sb1);
+  const uint32_t b2 = __builtin_amdgcn_perm(tb.t2, tb.t2, sb2);
+  return xor3(xor3(xor3(acc, a0, a1), a2, b0), b1, b2);
+}
+
+__device__ __forceinline__ void mac2(u32x4& acc, const Sel& a, const Tab& ta, const Sel& b, const Tab& tb) {
+  acc.x = mac2_dword(acc.x, a.s0[0], a.s1[0], a.s2[0], ta, b.s0[0], b.s1[0], b.s2[0], tb);
+  acc.y = mac2_dword(acc.y, a.s0[1], a.s1[1], a.s2[1], ta, b.s0[1], b.s1[1], b.s2[1], tb);
+  acc.z = mac2_dword(acc.z, a.s0[2], a.s1[2], a.s2[2], ta, b.s0[2], b.s1[2], b.s2[2], tb);
+  acc.w = mac2_dword(acc.w, a.s0[3], a.s1[3], a.s2[3], ta, b.s0[3], b.s1[3], b.s2[3], tb);
+}
+
+__device__ __forceinline__ void xor2_into(u32x4& acc, const u32x4& x, const u32x4& y) {
+  acc.x = xor3(acc.x, x.x, y.x);
+  acc.y = xor3(acc.y, x.y, y.y);
+  acc.z = xor3(acc.z, x.z, y.z);
+  acc.w = xor3(acc.w, x.w, y.w);
+}
 
 __device__ __forceinline__ uint8_t gmul_byte(uint32_t x, const Tab& t) {
   return static_cast<uint8_t>(gmul(x & 7u, (x >> 3) & 7u, (x >> 6) & 3u, t));
@@ -203,8 +234,29 @@ __global__ __launch_bounds__(512) void encode_v16(const uint8_t* __restrict__ da
     for (int j = 0; j < K; ++j) d[j] = ld16<POL>(packet_ptr<OFF>(data, offsets, g, K, j, P) + coff);
 #pragma unroll
     for (int i = 0; i < R; ++i) acc[i] = d[0];
+    // kPairMac: coefficients j = 1..K-1 two at a time; an odd one left over takes the
+    // single-coefficient loop below (jstart)
+    constexpr bool kPair = (POL & kPairMac) != 0 && !(FIRST && R == 1);
+    constexpr int kPairs = kPair ? (K - 1) / 2 : 0;
 #pragma unroll
-    for (int j = 1; j < K; ++j) {
+    for (int pj = 0; pj < kPairs; ++pj) {
+      const int j = 1 + 2 * pj;
+      Sel sa, sb;
+      prep(d[j], sa);
+      prep(d[j + 1], sb);
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        if (FIRST && i == 0) {
+          xor2_into(acc[0], d[j], d[j + 1]);
+        } else {
+          const uint32_t row = row0 + static_cast<uint32_t>(i);
+          mac2(acc[i], sa, tabs[(row - 1) * K + j], sb, tabs[(row - 1) * K + j + 1]);
+        }
+      }
+    }
+    constexpr int jstart = 1 + 2 * kPairs;
+#pragma unroll
+    for (int j = jstart; j < K; ++j) {
       if constexpr (FIRST && R == 1) {
         xor_into(acc[0], d[j]);
       } else {
@@ -1240,9 +1292,13 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
   if (a.groups == 0) return hipSuccess;
   if (a.P >= kVecMinP) {
     if (a.off_kind == OffsetKind::kNone) {
-      if (a.k == 10 && a.r == 3) return run_encode_v16<10, 3, 0, true>(a, 0, s);
+      // QUICFEC_ENCODE_PAIR=1: the paired-coefficient arithmetic (kPairMac; tuning A/B)
+      static const bool pair = env_waves("QUICFEC_ENCODE_PAIR", 0) == 1;
+      if (a.k == 10 && a.r == 3)
+        return pair ? run_encode_v16<10, 3, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<10, 3, 0, true>(a, 0, s);
       if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 0, true>(a, 0, s);
-      if (a.k == 20 && a.r == 5) return run_encode_v16<20, 5, 0, true>(a, 0, s);
+      if (a.k == 20 && a.r == 5)
+        return pair ? run_encode_v16<20, 5, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<20, 5, 0, true>(a, 0, s);
       if (a.k == 4 && a.r == 2) return run_encode_v16<4, 2, 0, true>(a, 0, s);
     } else if (a.off_kind == OffsetKind::kU32) {
       if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 1, true>(a, 0, s);
