@@ -1292,8 +1292,10 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
   if (a.groups == 0) return hipSuccess;
   if (a.P >= kVecMinP) {
     if (a.off_kind == OffsetKind::kNone) {
-      // QUICFEC_ENCODE_PAIR=1: the paired-coefficient arithmetic (kPairMac; tuning A/B)
-      static const bool pair = env_waves("QUICFEC_ENCODE_PAIR", 0) == 1;
+      // The paired-coefficient arithmetic (kPairMac): +0.9% at k=20 r=5 (5.53 vs 5.58 ms),
+      // +1.0% at k=10 r=3 (2.65 vs 2.68 ms), same box, alternating runs
+      // (profiles/r02_ab_encode_pair.txt).  QUICFEC_ENCODE_PAIR=0 restores the single form.
+      static const bool pair = env_waves("QUICFEC_ENCODE_PAIR", 1) == 1;
       if (a.k == 10 && a.r == 3)
         return pair ? run_encode_v16<10, 3, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<10, 3, 0, true>(a, 0, s);
       if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 0, true>(a, 0, s);
