@@ -10,7 +10,8 @@ for rd in $(seq 1 "${ROUNDS:-2}"); do
 import json, sys
 d = json.load(open("/tmp/ab.json"))
 print(sys.argv[1], d["config"]["workload"][:40], "value", d["value"],
-      {k: (v["ms"], v["achieved_GBps"], v.get("isolated", {}).get("ms_median")) for k, v in d["kernels"].items()})
+      {k: (v["ms"], v["achieved_GBps"], v.get("isolated", {}).get("ms_median"), v.get("api"),
+           (v.get("other_api") or {}).get("ms_median")) for k, v in d["kernels"].items()})
 PY
   done
 done
