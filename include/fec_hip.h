@@ -187,6 +187,11 @@ void fec_batcher_free(FECBatcher* b);
  * (<= slot_bytes; not all empty).  Returns the group's ticket (>= 0) or a negative code. */
 int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, const uint32_t* lens, uint32_t count);
 
+/* The same with the packets where they are (packet j at packets[j]): one copy fewer for
+ * C / C++ callers (cgo may not pass Go memory that holds Go pointers, so Go packs). */
+int64_t fec_batcher_submit_packets(FECBatcher* b, const uint8_t* const* packets, const uint32_t* lens,
+                                   uint32_t count);
+
 /* Waits for a ticket's batch (timeout_us < 0: no limit; 0: poll) and copies its r repair
  * payloads to out (row i at out + i*out_stride; NULL: discard).  Returns the payload length,
  * FEC_ERR_AGAIN on timeout (the ticket stays valid), or another negative code.  Each ticket

@@ -319,8 +319,11 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
 
 QFEC_EXPORT void fec_batcher_free(FECBatcher* b) { delete b; }
 
-QFEC_EXPORT int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, const uint32_t* lens, uint32_t count) {
-  if (!b || !lens || (!packed && count > 0)) return FEC_ERR_NULL;
+namespace {
+
+// Shared by both submit forms: packet j is at src(j).
+template <class Src>
+int64_t submit_group(FECBatcher* b, Src&& src, const uint32_t* lens, uint32_t count) {
   if (count == 0 || count > b->k) {
     berr("fec_batcher_submit: %u packets (group size k=%u)", count, b->k);
     return FEC_ERR_RANGE;
@@ -331,6 +334,7 @@ QFEC_EXPORT int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, con
       berr("fec_batcher_submit: packet of %u bytes exceeds the %u-byte slot", lens[j], b->slot);
       return FEC_ERR_RANGE;
     }
+    if (lens[j] > 0 && src(j) == nullptr) return FEC_ERR_NULL;
     max_len = std::max(max_len, lens[j]);
   }
   if (max_len == 0) {  // encoder_hybrid.go:95-97
@@ -358,16 +362,34 @@ QFEC_EXPORT int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, con
   }
   // ... and copy without it (the flusher encodes a slab once every reserved copy landed).
   uint8_t* dst = s->data + g * b->k * size_t(b->slot);
-  const uint8_t* src = packed;
   for (uint32_t j = 0; j < b->k; ++j) {  // packets zero-padded to the slot, absent slots zero
     uint8_t* d = dst + size_t(j) * b->slot;
     const uint32_t n = j < count ? lens[j] : 0;
-    if (n) std::memcpy(d, src, n);
+    if (n) std::memcpy(d, src(j), n);
     std::memset(d + n, 0, b->slot - n);
-    src += n;
   }
   s->committed.fetch_add(1, std::memory_order_release);
   return ticket;
+}
+
+}  // namespace
+
+QFEC_EXPORT int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, const uint32_t* lens, uint32_t count) {
+  if (!b || !lens || (!packed && count > 0)) return FEC_ERR_NULL;
+  // packed back to back: prefix sums of the lengths
+  uint64_t offs[256];
+  uint64_t o = 0;
+  for (uint32_t j = 0; j < count && j < 256; ++j) {
+    offs[j] = o;
+    o += lens[j];
+  }
+  return submit_group(b, [&](uint32_t j) { return packed + offs[j]; }, lens, count);
+}
+
+QFEC_EXPORT int64_t fec_batcher_submit_packets(FECBatcher* b, const uint8_t* const* packets, const uint32_t* lens,
+                                               uint32_t count) {
+  if (!b || !lens || (!packets && count > 0)) return FEC_ERR_NULL;
+  return submit_group(b, [&](uint32_t j) { return packets[j]; }, lens, count);
 }
 
 namespace {

@@ -520,11 +520,11 @@ BatchedFECEncoder::BatchedFECEncoder(std::shared_ptr<SharedFECBatcher> batcher) 
 Error BatchedFECEncoder::submitLocked(Ticket* t) {
   if (!b_) return errorf("GPU FEC engine unavailable");
   if (packets_.empty()) return errorf("no packets in group");  // encoder_hybrid.go:84-86
-  packed_.clear();
   lens_.clear();
+  ptrs_.clear();
   size_t maxSize = 0;
   for (const auto& p : packets_) {
-    packed_.insert(packed_.end(), p.begin(), p.end());
+    ptrs_.push_back(p.data());
     lens_.push_back(static_cast<uint32_t>(p.size()));
     maxSize = std::max(maxSize, p.size());
   }
@@ -534,7 +534,8 @@ Error BatchedFECEncoder::submitLocked(Ticket* t) {
     packets_.clear();
     return errorf("empty packets");
   }
-  const int64_t tk = fec_batcher_submit(b_->raw(), packed_.data(), lens_.data(), static_cast<uint32_t>(lens_.size()));
+  const int64_t tk =
+      fec_batcher_submit_packets(b_->raw(), ptrs_.data(), lens_.data(), static_cast<uint32_t>(lens_.size()));
   if (tk < 0) {  // refused (e.g. a packet wider than the slot): the group is dropped
     packets_.clear();
     return errorf("fec_batcher_submit failed with code %lld: %s", static_cast<long long>(tk), fec_batcher_last_error());

@@ -353,7 +353,8 @@ class BatchedFECEncoder {
   std::vector<Bytes> packets_;
   uint64_t groupID_ = 0;
   std::deque<Ticket> outstanding_;
-  Bytes packed_, rowbuf_;
+  Bytes rowbuf_;
+  std::vector<const uint8_t*> ptrs_;
   std::vector<uint32_t> lens_;
   std::mutex mu_;
   FECMetrics metrics_;

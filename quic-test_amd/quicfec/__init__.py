@@ -29,6 +29,7 @@ FEC_ERR_HIP = -2
 FEC_ERR_RANGE = -3
 FEC_ERR_NODEV = -4
 FEC_ERR_NOMEM = -5
+FEC_ERR_AGAIN = -6
 
 # Every function the headers declare (tests check the library exports all of them).
 REFERENCE_SYMBOLS = (
@@ -44,6 +45,8 @@ HIP_SYMBOLS = (
     "fec_fill_random_dev", "fec_synchronize", "fec_decode_loss_hint",
     "fec_group_new", "fec_group_free", "fec_group_size", "fec_group_context",
     "fec_group_encode_batch_rs", "fec_group_decode_batch_rs",
+    "fec_batcher_new", "fec_batcher_free", "fec_batcher_submit", "fec_batcher_submit_packets",
+    "fec_batcher_wait", "fec_batcher_flush", "fec_batcher_stats", "fec_batcher_last_error",
 )
 
 
@@ -116,6 +119,14 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
         "fec_group_context": (_vp, [_vp, _int]),
         "fec_group_encode_batch_rs": (_int, [_vp, _vp, _u64, _u32, _u32, _u32, _vp]),
         "fec_group_decode_batch_rs": (_int, [_vp, _vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp]),
+        "fec_batcher_new": (_vp, [_int, _u32, _u32, _u32, _u32, _u32, _u32]),
+        "fec_batcher_free": (None, [_vp]),
+        "fec_batcher_submit": (ctypes.c_int64, [_vp, _vp, _vp, _u32]),
+        "fec_batcher_submit_packets": (ctypes.c_int64, [_vp, ctypes.POINTER(_vp), _vp, _u32]),
+        "fec_batcher_wait": (_int, [_vp, ctypes.c_int64, _vp, _u32, ctypes.c_int64]),
+        "fec_batcher_flush": (_int, [_vp]),
+        "fec_batcher_stats": (_int, [_vp, _vp]),
+        "fec_batcher_last_error": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -319,6 +330,77 @@ class DeviceGroup:
                                                 ctypes.byref(bad))
         _check(rc, "fec_group_decode_batch_rs")
         return int(bad.value)
+
+
+class Batcher:
+    """An FECBatcher: one batch for the groups of many streams, encoded when max_groups are
+    pending or deadline_us after the oldest pending group (include/fec_hip.h)."""
+
+    STATS = ("groups", "batches", "full_flushes", "deadline_flushes", "max_batch", "expired")
+
+    def __init__(self, k: int, r: int, slot_bytes: int = 1500, max_groups: int = 4096, deadline_us: int = 1000,
+                 device: int = -1, slabs: int = 3):
+        self.lib = load_library()
+        self.k, self.r, self.slot = k, r, slot_bytes
+        h = self.lib.fec_batcher_new(device, k, r, slot_bytes, max_groups, deadline_us, slabs)
+        if not h:
+            raise FecError("fec_batcher_new", FEC_ERR_NODEV, self.last_error())
+        self.handle = h
+
+    def last_error(self) -> str:
+        return (self.lib.fec_batcher_last_error() or b"").decode(errors="replace")
+
+    def submit(self, packets) -> int:
+        """One group (1..k packets, any lengths <= slot); returns its ticket."""
+        n = len(packets)
+        lens = np.array([len(p) for p in packets], dtype=np.uint32)
+        ptrs = (_vp * max(1, n))(*[_ptr(p) for p in packets])
+        t = int(self.lib.fec_batcher_submit_packets(self.handle, ptrs, lens.ctypes.data, n))
+        if t < 0:
+            raise FecError("fec_batcher_submit_packets", t, self.last_error())
+        return t
+
+    def submit_packed(self, packed: np.ndarray, lens) -> int:
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        t = int(self.lib.fec_batcher_submit(self.handle, _ptr(packed), lens.ctypes.data, len(lens)))
+        if t < 0:
+            raise FecError("fec_batcher_submit", t, self.last_error())
+        return t
+
+    def wait(self, ticket: int, timeout_us: int = -1):
+        """The group's r repair payloads (a list of arrays), or None when not ready in time."""
+        out = np.zeros(self.r * self.slot, dtype=np.uint8)
+        n = int(self.lib.fec_batcher_wait(self.handle, ticket, out.ctypes.data, self.slot, timeout_us))
+        if n == FEC_ERR_AGAIN:
+            return None
+        if n < 0:
+            raise FecError("fec_batcher_wait", n, self.last_error())
+        return [out[i * self.slot:i * self.slot + n].copy() for i in range(self.r)]
+
+    def flush(self) -> None:
+        _check(self.lib.fec_batcher_flush(self.handle), "fec_batcher_flush")
+
+    def stats(self) -> dict:
+        st = np.zeros(len(self.STATS), dtype=np.uint64)
+        _check(self.lib.fec_batcher_stats(self.handle, st.ctypes.data), "fec_batcher_stats")
+        return dict(zip(self.STATS, (int(x) for x in st)))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self.lib.fec_batcher_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def _nbytes(a) -> int:

@@ -1,0 +1,110 @@
+"""The shared batcher's C-ABI (fec_batcher_*, include/fec_hip.h) on the GPU: repair payloads
+equal the oracle's code rows for every group (row 0 = the reference XOR), both submit forms,
+timeouts, the result ring's expiry, errors, concurrent submitters."""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _expected_rows(oracle_mod, packets, k, r):
+    """Rows 0..r-1 of one group over its packets zero-padded to the longest, truncated to it."""
+    L = max(len(p) for p in packets)
+    P = (L + 15) // 16 * 16
+    data = np.zeros(k * P, dtype=np.uint8)
+    for j, p in enumerate(packets):
+        data[j * P:j * P + len(p)] = p
+    par = oracle_mod.rs_encode(data, 1, k, r, P)
+    return [par[i * P:i * P + L] for i in range(r)]
+
+
+@pytest.mark.parametrize("k,r", [(10, 1), (10, 3), (20, 5), (4, 2)])
+def test_batcher_rows_match_oracle(quicfec_mod, oracle_mod, k, r):
+    rng = np.random.default_rng(k * 10 + r)
+    with quicfec_mod.Batcher(k, r, slot_bytes=1500, max_groups=16, deadline_us=500) as b:
+        groups, tickets = [], []
+        for g in range(70):
+            n = k if g % 7 else int(rng.integers(1, k + 1))          # some partial groups
+            pk = [oracle_mod.splitmix_bytes(int(rng.integers(1, 1501)), 1000 * g + j) for j in range(n)]
+            groups.append(pk)
+            if g % 2:
+                tickets.append(b.submit(pk))
+            else:
+                packed = np.concatenate(pk)
+                tickets.append(b.submit_packed(packed, [len(p) for p in pk]))
+        b.flush()
+        for pk, t in zip(groups, tickets):
+            rows = b.wait(t)
+            exp = _expected_rows(oracle_mod, pk, k, r)
+            assert len(rows) == r and all(np.array_equal(a, e) for a, e in zip(rows, exp)), t
+        st = b.stats()
+        assert st["groups"] == 70 and st["batches"] >= 5 and st["full_flushes"] >= 1 and st["max_batch"] <= 16
+        # row 0 is the reference XOR of the packets (fec_xor_simd.cpp:411-427, zero-padded)
+        pk = groups[1]
+        L = max(len(p) for p in pk)
+        x = np.zeros(L, dtype=np.uint8)
+        for p in pk:
+            x[:len(p)] ^= p
+        assert np.array_equal(_expected_rows(oracle_mod, pk, k, r)[0], x)
+
+
+def test_batcher_wait_semantics(quicfec_mod, oracle_mod):
+    k, r = 10, 3
+    pk = [oracle_mod.splitmix_bytes(1200, j) for j in range(k)]
+    with quicfec_mod.Batcher(k, r, slot_bytes=1200, max_groups=64, deadline_us=2_000_000) as b:
+        t = b.submit(pk)
+        assert b.wait(t, timeout_us=0) is None                   # 2 s deadline: still pending
+        assert b.wait(t, timeout_us=20_000) is None
+        b.flush()
+        rows = b.wait(t, timeout_us=5_000_000)
+        assert rows is not None and np.array_equal(rows[0], _expected_rows(oracle_mod, pk, k, r)[0])
+        with pytest.raises(quicfec_mod.FecError):                 # collected once only
+            b.wait(t, timeout_us=0)
+        with pytest.raises(quicfec_mod.FecError):                 # never issued
+            b.wait(t + 100, timeout_us=0)
+        with pytest.raises(quicfec_mod.FecError, match="exceeds"):
+            b.submit([np.zeros(1201, dtype=np.uint8)])
+        with pytest.raises(quicfec_mod.FecError):
+            b.submit([np.zeros(10, dtype=np.uint8)] * (k + 1))
+        with pytest.raises(quicfec_mod.FecError, match="empty"):
+            b.submit([np.zeros(0, dtype=np.uint8)] * 3)
+
+
+def test_batcher_result_ring_expiry(quicfec_mod, oracle_mod):
+    """Results live in a ring of 2 * slabs * max_groups entries; older uncollected ones are
+    dropped and counted."""
+    k, r = 4, 2
+    with quicfec_mod.Batcher(k, r, slot_bytes=64, max_groups=2, deadline_us=100, slabs=2) as b:
+        tickets = [b.submit([oracle_mod.splitmix_bytes(64, 7 * g + j) for j in range(k)]) for g in range(20)]
+        b.flush()
+        last = b.wait(tickets[-1], timeout_us=5_000_000)
+        assert last is not None
+        with pytest.raises(quicfec_mod.FecError, match="expired|collected"):
+            b.wait(tickets[0], timeout_us=0)
+        assert b.stats()["expired"] >= 20 - 8
+
+
+def test_batcher_concurrent_streams(quicfec_mod, oracle_mod):
+    k, r, S, G = 10, 3, 8, 40
+    errors = []
+    with quicfec_mod.Batcher(k, r, slot_bytes=1200, max_groups=32, deadline_us=300) as b:
+        def stream(s):
+            try:
+                for g in range(G):
+                    pk = [oracle_mod.splitmix_bytes(200 + (s * 37 + g * 13 + j) % 1000, s * 10_000 + g * 16 + j)
+                          for j in range(k)]
+                    rows = b.wait(b.submit(pk))
+                    if not all(np.array_equal(a, e) for a, e in zip(rows, _expected_rows(oracle_mod, pk, k, r))):
+                        errors.append((s, g))
+            except Exception as e:   # noqa: BLE001 - reported below
+                errors.append(repr(e))
+        th = [threading.Thread(target=stream, args=(s,)) for s in range(S)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        st = b.stats()
+    assert not errors, errors[:5]
+    assert st["groups"] == S * G and st["batches"] < S * G
