@@ -23,12 +23,14 @@ def _expected_rows(oracle_mod, packets, k, r):
 @pytest.mark.parametrize("k,r", [(10, 1), (10, 3), (20, 5), (4, 2)])
 def test_batcher_rows_match_oracle(quicfec_mod, oracle_mod, k, r):
     rng = np.random.default_rng(k * 10 + r)
-    with quicfec_mod.Batcher(k, r, slot_bytes=1500, max_groups=16, deadline_us=500) as b:
-        groups, tickets = [], []
-        for g in range(70):
-            n = k if g % 7 else int(rng.integers(1, k + 1))          # some partial groups
-            pk = [oracle_mod.splitmix_bytes(int(rng.integers(1, 1501)), 1000 * g + j) for j in range(n)]
-            groups.append(pk)
+    groups = []
+    for g in range(70):
+        n = k if g % 7 else int(rng.integers(1, k + 1))              # some partial groups
+        groups.append([oracle_mod.splitmix_bytes(int(rng.integers(1, 1501)), 1000 * g + j) for j in range(n)])
+    # a long deadline: batches close when 16 groups are pending, the last one at flush()
+    with quicfec_mod.Batcher(k, r, slot_bytes=1500, max_groups=16, deadline_us=2_000_000) as b:
+        tickets = []
+        for g, pk in enumerate(groups):
             if g % 2:
                 tickets.append(b.submit(pk))
             else:
@@ -40,7 +42,7 @@ def test_batcher_rows_match_oracle(quicfec_mod, oracle_mod, k, r):
             exp = _expected_rows(oracle_mod, pk, k, r)
             assert len(rows) == r and all(np.array_equal(a, e) for a, e in zip(rows, exp)), t
         st = b.stats()
-        assert st["groups"] == 70 and st["batches"] >= 5 and st["full_flushes"] >= 1 and st["max_batch"] <= 16
+        assert st == dict(st, groups=70, batches=5, full_flushes=4, deadline_flushes=1, max_batch=16), st
         # row 0 is the reference XOR of the packets (fec_xor_simd.cpp:411-427, zero-padded)
         pk = groups[1]
         L = max(len(p) for p in pk)
