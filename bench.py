@@ -248,8 +248,9 @@ def _popcount(x):
     return c
 
 
-def decode_algorithmic_bytes(masks, k: int, r: int, P: int) -> int:
-    """Sum over groups with lost data shards of (k + e) * P (read k survivors, write e)."""
+def decode_algorithmic_bytes(masks, k: int, r: int, P: int, reads_only: bool = False) -> int:
+    """Sum over groups with lost data shards of (k + e) * P (read k survivors, write e);
+    reads_only: the k * P read part alone."""
     import numpy as np
     m = masks & np.uint64((1 << k) - 1)
     e = np.zeros(len(m), dtype=np.int64)
@@ -264,6 +265,8 @@ def decode_algorithmic_bytes(masks, k: int, r: int, P: int) -> int:
         alive -= (pp & np.uint64(1)).astype(np.int64)
         pp >>= np.uint64(1)
     ok = (e > 0) & (e <= alive)
+    if reads_only:
+        return int(ok.sum()) * k * P
     return int(((k + e[ok]) * P).sum())
 
 
@@ -527,7 +530,7 @@ def main() -> int:
     parity = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
     # this rank's slice of one global synthetic stream
     ctx.fill_random_dev(data, data.numel(), SEED + 2, byte_offset=g0 * k * P, stream=sp)
-    dec_bytes = 0
+    dec_bytes = dec_read = 0
     recover = cfg["decode"] and args.decode_api == "recover"
     rebuilt = torch.empty(G * r * P, dtype=torch.uint8, device="cuda") if recover else None
 
@@ -540,6 +543,7 @@ def main() -> int:
     if cfg["decode"]:
         masks_h = make_masks(cfg, G, SEED + 3 + rank)
         dec_bytes = decode_algorithmic_bytes(masks_h, k, r, P)
+        dec_read = decode_algorithmic_bytes(masks_h, k, r, P, reads_only=True)
         masks = torch.from_numpy(masks_h.view(np.int64)).to("cuda")
         ctx.decode_prepare(k, r)
         if cfg.get("loss"):
@@ -651,7 +655,16 @@ def main() -> int:
         if other == "recover" and rebuilt is None:
             rebuilt = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
         kernels["decode"]["other_api"] = {"api": other, **isolated(lambda: decode_call(other), dec_bytes)}
+    # The box's own HBM copy rate (fec_copy_dev: the encode's 16-B-per-lane pattern, no
+    # arithmetic), measured the same way: box-to-box spread is a few percent, so the kernels
+    # are also quoted against it.
+    half = (data.numel() // 2) // 16 * 16
+    scratch = torch.empty(half, dtype=torch.uint8, device="cuda")
+    copy = isolated(lambda: ctx.copy_dev(data, scratch, half, stream=sp), 2 * half)
+    del scratch
+    torch.cuda.empty_cache()
     dom = max(kernels, key=lambda n: kernels[n]["ms"])
+    dom_read = k * P * G if dom == "encode" else dec_read
     pmc, pmc_note = load_pmc_traffic(args.config)
     pmc = pmc or {}
     roofline = {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["achieved_GBps"],
@@ -660,6 +673,9 @@ def main() -> int:
                 "traffic": pmc.get("recover" if dom == "decode" and recover else dom, {}).get("hbm_bytes_per_launch"),
                 "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes"],
                 "traffic_source": pmc_note,
+                "read_frac": round(dom_read / (kernels[dom]["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "box_copy_GBps": copy["achieved_GBps"],
+                "frac_of_box_copy": round(kernels[dom]["achieved_GBps"] / copy["achieved_GBps"], 4),
                 "timing": "torch.cuda.Event on the launch stream, averaged over the timed steps"}
 
     e2e = None

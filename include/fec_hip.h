@@ -128,6 +128,11 @@ int fec_decode_loss_hint(FECEncoderCtx* ctx, double share);
 int fec_fill_random_dev(FECEncoderCtx* ctx, uint8_t* d_dst, uint64_t nbytes, uint64_t seed,
                         uint64_t byte_offset, void* stream);
 
+/* d_dst <- d_src with the engine's own 16-B-per-lane access pattern, asynchronously on
+ * stream: the HBM copy rate a box achieves, which the benchmark reports the FEC kernels
+ * against.  nbytes and both addresses must be multiples of 16 (else FEC_ERR_RANGE). */
+int fec_copy_dev(FECEncoderCtx* ctx, const uint8_t* d_src, uint8_t* d_dst, uint64_t nbytes, void* stream);
+
 /* Wait for the context's own stream. */
 int fec_synchronize(FECEncoderCtx* ctx);
 

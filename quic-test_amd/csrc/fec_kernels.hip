@@ -1164,6 +1164,14 @@ __global__ __launch_bounds__(256) void fill_bytes(uint8_t* __restrict__ dst, uin
   dst[t] = static_cast<uint8_t>(w >> (8 * (pos % 8)));
 }
 
+// Box calibration: a plain 16-B-per-lane copy, the same access pattern as the encode's loads
+// and stores without the arithmetic; bench.py reports the kernels against its rate.
+__global__ __launch_bounds__(256) void copy_words(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                  uint32_t n16) {
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  if (t < n16) dst[t] = src[t];
+}
+
 constexpr uint32_t kMaxThreadsPerLaunch = 1u << 30;
 // Wave-per-group decode launches: 256-thread workgroups, so at most 2^22 of them keep the
 // grid's work-item count (blocks * 256) inside 32 bits with room to spare.
@@ -1612,6 +1620,19 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
     const uint64_t cn = (nbytes - c0 < kMaxThreadsPerLaunch) ? nbytes - c0 : kMaxThreadsPerLaunch;
     hipLaunchKernelGGL(fill_bytes, dim3(blocks_for(cn)), dim3(256), 0, s, dst + c0,
                        static_cast<uint32_t>(cn), seed, byte_offset + c0);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_copy_words(const uint8_t* src, uint8_t* dst, uint64_t nbytes, hipStream_t s) {
+  const uint64_t n16 = nbytes / 16;
+  for (uint64_t c0 = 0; c0 < n16; c0 += kMaxThreadsPerLaunch) {
+    const uint64_t cn = (n16 - c0 < kMaxThreadsPerLaunch) ? n16 - c0 : kMaxThreadsPerLaunch;
+    hipLaunchKernelGGL(copy_words, dim3(blocks_for(cn)), dim3(256), 0, s,
+                       reinterpret_cast<const uint4*>(src + c0 * 16), reinterpret_cast<uint4*>(dst + c0 * 16),
+                       static_cast<uint32_t>(cn));
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

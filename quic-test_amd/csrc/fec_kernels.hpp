@@ -110,6 +110,8 @@ bool decode_needs_rec_off(const DecodeLaunch& a);
 bool decode_compact_tables(const DecodeLaunch& a);
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);
+// dst <- src, nbytes a multiple of 16, both 16-B aligned (box calibration).
+hipError_t launch_copy_words(const uint8_t* src, uint8_t* dst, uint64_t nbytes, hipStream_t s);
 
 // Records marking "nothing to do" / "unrecoverable" in rec_off.
 constexpr uint32_t kRecNone = 0xFFFFFFFFu;

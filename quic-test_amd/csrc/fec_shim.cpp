@@ -1398,6 +1398,27 @@ QFEC_EXPORT int fec_fill_random_dev(FECEncoderCtx* ctx, uint8_t* d_dst, uint64_t
   return record_ctx_error(ctx, fec_fill_random_dev_impl(ctx, d_dst, nbytes, seed, byte_offset, stream));
 }
 
+static int fec_copy_dev_impl(FECEncoderCtx* ctx, const uint8_t* d_src, uint8_t* d_dst, uint64_t nbytes,
+                             void* stream) {
+  if (!ctx || !d_src || !d_dst) return FEC_ERR_NULL;
+  if (nbytes % 16 || reinterpret_cast<uintptr_t>(d_src) % 16 || reinterpret_cast<uintptr_t>(d_dst) % 16)
+  {
+    set_error("fec_copy_dev: size and addresses must be multiples of 16");
+    return FEC_ERR_RANGE;
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return FEC_ERR_NODEV;
+  QFEC_HIP(qfec::launch_copy_words(d_src, d_dst, nbytes, pick_stream(ctx, stream)));
+  return FEC_OK;
+}
+
+QFEC_EXPORT int fec_copy_dev(FECEncoderCtx* ctx, const uint8_t* d_src, uint8_t* d_dst, uint64_t nbytes,
+                             void* stream) {
+  g_last_error.clear();
+  return record_ctx_error(ctx, fec_copy_dev_impl(ctx, d_src, d_dst, nbytes, stream));
+}
+
 QFEC_EXPORT int fec_decode_loss_hint(FECEncoderCtx* ctx, double share) {
   if (!ctx) return FEC_ERR_NULL;
   std::lock_guard<std::mutex> lk(ctx->mu);

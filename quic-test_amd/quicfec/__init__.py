@@ -42,7 +42,7 @@ HIP_SYMBOLS = (
     "fec_hip_device_count", "fec_hip_last_error", "fec_ctx_last_error", "fec_encoder_new_device", "fec_encoder_device",
     "fec_hip_version", "fec_parity_matrix", "fec_encode_batch_rs", "fec_decode_batch_rs",
     "fec_encode_batch_rs_dev", "fec_decode_batch_rs_dev", "fec_recover_batch_rs_dev", "fec_decode_prepare",
-    "fec_fill_random_dev", "fec_synchronize", "fec_decode_loss_hint",
+    "fec_fill_random_dev", "fec_copy_dev", "fec_synchronize", "fec_decode_loss_hint",
     "fec_group_new", "fec_group_free", "fec_group_size", "fec_group_context",
     "fec_group_encode_batch_rs", "fec_group_decode_batch_rs",
     "fec_batcher_new", "fec_batcher_free", "fec_batcher_submit", "fec_batcher_submit_packets",
@@ -111,6 +111,7 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
         "fec_recover_batch_rs_dev": (_int, [_vp, _vp, _vp, _vp, _u64, _u32, _u32, _u32, _vp, _vp, _vp]),
         "fec_decode_prepare": (_int, [_vp, _u32, _u32, ctypes.POINTER(_u64)]),
         "fec_fill_random_dev": (_int, [_vp, _vp, _u64, _u64, _u64, _vp]),
+        "fec_copy_dev": (_int, [_vp, _vp, _vp, _u64, _vp]),
         "fec_synchronize": (_int, [_vp]),
         "fec_decode_loss_hint": (_int, [_vp, _dbl]),
         "fec_group_new": (_vp, [ctypes.POINTER(_int), _int]),
@@ -267,6 +268,11 @@ class Context:
         n = ctypes.c_uint64(0)
         _check(self.lib.fec_decode_prepare(self.handle, k, r, ctypes.byref(n)), "fec_decode_prepare")
         return int(n.value)
+
+    def copy_dev(self, d_src, d_dst, nbytes: int, stream=None) -> None:
+        """d_dst <- d_src (box HBM copy calibration; nbytes a multiple of 16)."""
+        _check(self.lib.fec_copy_dev(self.handle, _ptr(d_src), _ptr(d_dst), nbytes, stream),
+               "fec_copy_dev")
 
     def fill_random_dev(self, d_dst, nbytes: int, seed: int, byte_offset: int = 0,
                         stream: Optional[int] = None) -> None:

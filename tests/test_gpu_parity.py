@@ -335,6 +335,17 @@ def test_fill_random_matches_oracle(gpu_ctx, oracle_mod, torch_cuda):
         assert np.array_equal(d.cpu().numpy()[:n], oracle_mod.splitmix_bytes(n, 0x1234, off))
 
 
+def test_copy_dev(gpu_ctx, quicfec_mod, torch_cuda):
+    src = torch_cuda.randint(0, 256, (1 << 20,), dtype=torch_cuda.uint8, device="cuda")
+    dst = torch_cuda.zeros(src.numel() + 32, dtype=torch_cuda.uint8, device="cuda")
+    gpu_ctx.copy_dev(src, dst, src.numel())
+    gpu_ctx.synchronize()
+    assert torch_cuda.equal(dst[:src.numel()], src) and int(dst[src.numel():].sum()) == 0
+    with pytest.raises(quicfec_mod.FecError) as ei:
+        gpu_ctx.copy_dev(src, dst, 100)
+    assert ei.value.code == quicfec_mod.FEC_ERR_RANGE
+
+
 def test_decode_prepare_sizes(gpu_ctx):
     assert gpu_ctx.decode_prepare(10, 3) > 0
     assert gpu_ctx.decode_prepare(20, 5) > 0
