@@ -43,7 +43,7 @@ def short(name: str) -> str:
             args = name.split(key + "<", 1)[1].split(">", 1)[0].split(",")
             pol = int(args[2]) if len(args) > 2 and args[2].strip().isdigit() else 0
             return "recover" if pol & K_COMPACT_OUT else "decode"
-    for key in ("classify", "fill_words", "encode_bytes", "decode_bytes"):
+    for key in ("classify", "fill_words", "copy_words", "encode_bytes", "decode_bytes"):
         if key in name:
             return key
     return name[:40]
