@@ -843,13 +843,69 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
                                                     const uint64_t* __restrict__ masks, RankMeta rm,
                                                     uint8_t* __restrict__ status) {
   static_assert(!INLINE || (DIRECT && MAXE <= 3), "inline classify: mask-addressed forms with r <= 3");
-  static_assert(SCAN == 0 || (DIRECT && INLINE && SCAN <= 64), "scan: mask-addressed inline forms, <= 64 groups");
+  static_assert(SCAN == 0 || (DIRECT && INLINE && (SCAN <= 64 || SCAN % 256 == 0)),
+                "scan: mask-addressed inline forms, <= 64 groups per wave or whole 256-group rows per block");
   extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];  // see encode_v16
   if (never) occupancy_lds[threadIdx.x] = 0;
   const uint64_t wv = static_cast<uint64_t>(swz ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * 4u +
                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   const uint32_t lane = threadIdx.x & 63u;
-  if constexpr (SCAN == 0) {
+  if constexpr (SCAN > 64) {
+    // Segment form: the block's 4 waves check SCAN groups (one mask per thread and row of
+    // 256), write every status byte, compact the groups to rebuild into LDS in group order
+    // and share them out round robin, so every wave of the block gets the same number of
+    // groups (+-1) whatever the loss pattern; a block's groups sit within SCAN * (k + r)
+    // packets of each other.
+    constexpr int J = SCAN / 256;
+    __shared__ uint64_t seg_mask[SCAN];
+    __shared__ uint16_t seg_idx[SCAN];
+    __shared__ uint32_t seg_cnt[J * 4];
+    const uint64_t g0 = static_cast<uint64_t>(swz ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * SCAN;
+    if (g0 >= groups) return;
+    const uint32_t wave = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+    constexpr uint64_t kmask = (1ull << K) - 1;
+    uint64_t mv[J], bal[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const uint64_t g = g0 + j * 256u + threadIdx.x;
+      bool need = false;
+      mv[j] = 0;
+      if (g < groups) {
+        mv[j] = masks[g];
+        const uint32_t ne = static_cast<uint32_t>(__popcll(mv[j] & kmask));
+        const bool bad = ne > r - static_cast<uint32_t>(__popcll((mv[j] >> K) & ((1ull << r) - 1)));
+        if (status != nullptr) status[g] = bad ? 1 : 0;
+        need = ne > 0 && !bad;
+      }
+      bal[j] = __ballot(need);
+      if (lane == 0) seg_cnt[j * 4 + wave] = static_cast<uint32_t>(__popcll(bal[j]));
+    }
+    __syncthreads();
+    uint32_t total = 0, off[J];
+#pragma unroll
+    for (int c = 0; c < J * 4; ++c) {
+      if (static_cast<uint32_t>(c % 4) == wave) off[c / 4] = total;
+      total += seg_cnt[c];
+    }
+    const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      if ((bal[j] >> lane) & 1u) {
+        const uint32_t pos = off[j] + static_cast<uint32_t>(__popcll(bal[j] & below));
+        seg_mask[pos] = mv[j];
+        seg_idx[pos] = static_cast<uint16_t>(j * 256u + threadIdx.x);
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = wave; i < total; i += 4u) {
+      const uint64_t mi = seg_mask[i];
+      const uint64_t m = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(mi >> 32))) << 32) |
+                         __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(mi));
+      const uint32_t gl = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(seg_idx[i]));
+      fused_group<K, MAXE, POL, NM, NT, DIRECT, INLINE>(g0 + gl, m, lane, data, parity, rec_off, codebook, P, r, m0,
+                                                        out, rm, nullptr);
+    }
+  } else if constexpr (SCAN == 0) {
     if (wv >= groups) return;
     const uint64_t m = DIRECT ? masks[wv] : 0;
     fused_group<K, MAXE, POL, NM, NT, DIRECT, INLINE>(wv, m, lane, data, parity, rec_off, codebook, P, r, m0, out, rm,
@@ -1377,7 +1433,7 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
 
 template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false, bool INLINE = DIRECT, int SCAN = 0>
 hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
-  constexpr uint64_t kGroupsPerBlock = 4u * (SCAN > 0 ? SCAN : 1);
+  constexpr uint64_t kGroupsPerBlock = SCAN > 64 ? SCAN : 4u * (SCAN > 0 ? SCAN : 1);
   const uint32_t passes = (a.r + MAXE - 1) / MAXE;
   const uint32_t smem = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_DECODE_WAVES", kDecodeWavesPerCU), 4);
   RankMeta rm{};

@@ -250,6 +250,7 @@ int main(int argc, char** argv) {
                   }});
   if (k == 10 && r == 3 && P == 1200) {
     PSCAN(2) PSCAN(4) PSCAN(8) PSCAN(16) PSCAN(32) PSCAN(64)
+    PSCAN(256) PSCAN(512) PSCAN(1024)
   }
   // record-addressed fused form with the coefficient tables staged through LDS (kLdsTabs)
 #define PLDS(KK, RR, NMM, NTT)                                                                    \
