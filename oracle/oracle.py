@@ -158,7 +158,9 @@ def go_recover_single(pkts: Sequence[Optional[np.ndarray]], parity_payload: np.n
     return int(mid), out
 
 
-# ---- the reference itself (this container only) ----
+# ---- the reference itself: oracle/_ref/libfec_ref.so, compiled from /root/reference in the
+# build container and carried to the GPU box with the tree (git-ignored, not gpurun-ignored);
+# loaded only by the oracle tests and bench.py's cpu_baseline leg ----
 def ref_lib() -> Optional[ctypes.CDLL]:
     if not REF_LIB.exists():
         return None
