@@ -200,8 +200,10 @@ int64_t fec_batcher_submit_packets(FECBatcher* b, const uint8_t* const* packets,
 /* Waits for a ticket's batch (timeout_us < 0: no limit; 0: poll) and copies its r repair
  * payloads to out (row i at out + i*out_stride; NULL: discard).  Returns the payload length,
  * FEC_ERR_AGAIN on timeout (the ticket stays valid), or another negative code.  Each ticket
- * can be collected once.  Results live in a ring of 2 * slabs * max_groups entries: one not
- * collected before that many newer groups are encoded is dropped (FEC_ERR_RANGE). */
+ * can be collected once; the payloads are copied straight from the batcher's page-locked
+ * parity ring.  A result not collected before 2 * slabs * max_groups newer groups are encoded
+ * may be dropped (FEC_ERR_RANGE).  Polling (timeout 0) a ticket never issued returns
+ * FEC_ERR_AGAIN; a blocking wait on it returns FEC_ERR_RANGE. */
 int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int64_t timeout_us);
 
 /* Closes the pending batch now (e.g. at the end of a stream) instead of at its deadline. */

@@ -11,19 +11,26 @@
 // arrived, whichever comes first, so no repair waits longer than the deadline plus one encode.
 //
 // Memory: a ring of `slabs` page-locked slabs (fec_alloc_slab), each max_groups groups of k
-// slots of `slot_bytes`, plus its parity; the kernels read and write them in place over PCIe
-// (the zero-copy path of fec_encode_batch_rs), so a batch costs one launch and one
-// synchronize.  While one slab is being encoded the next ones fill.  When every slab is busy,
-// submitters wait (backpressure).
+// slots of `slot_bytes`, and one page-locked parity ring of C = 3 * slabs * max_groups group
+// slots (r * slot_bytes each; ticket t's parity sits in slot t % C); the kernels read a slab
+// and write its groups' parity slots in place over PCIe (the zero-copy path of
+// fec_encode_batch_rs), so a batch costs one launch (two where it wraps the ring) and one
+// synchronize.  While one slab is being encoded the next ones fill.  When every slab is
+// busy, submitters wait (backpressure).
 //
-// Threads.  A submitter reserves its group's slot under the batcher lock and copies the
-// packets in after releasing it, so streams copy in parallel; the slab is encoded once every
-// reserved copy has landed.  One flusher thread per batcher closes slabs (full or due),
-// encodes them on the batcher's own context and publishes each group's r repair payloads
-// (maxLen bytes each, the group's longest packet: the reference's repair length,
-// encoder_hybrid.go:91-98) into a ring of result entries indexed by ticket, which waiters read
-// without the lock.  A result not collected before 2 * slabs * max_groups newer groups are
-// published is dropped (the late wait gets FEC_ERR_RANGE; stats.expired counts them).
+// Threads.  A submitter reserves its group's slot with one atomic add on the open slab's
+// reservation word (no lock: the global lock serialised 16 saturating streams), copies the
+// packets in, and counts itself committed; the slab is encoded once every reserved copy has
+// landed.  The lock is taken only by a slab's first group (its deadline starts), by the group
+// that fills it, and while every slab is busy.  One flusher thread per batcher closes slabs (full or due),
+// encodes them on the batcher's own context and publishes each group's result (where its r
+// repair payloads of maxLen bytes sit -- the group's longest packet: the reference's repair
+// length, encoder_hybrid.go:91-98) into a ring of C entries indexed by ticket.  Waiters copy
+// the payloads straight out of the parity ring without the lock and then check that no encode
+// covering ticket + C has been launched meanwhile (a seqlock on `launched_upto`), so the
+// flusher copies nothing per group.  A result not collected before C newer groups are
+// launched (at least 2 * slabs * max_groups newer groups encoded) is dropped: the late wait
+// gets FEC_ERR_RANGE and stats.expired counts it.
 #include <hip/hip_runtime.h>
 #include <sys/prctl.h>
 
@@ -33,6 +40,7 @@
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -50,31 +58,36 @@ namespace {
 using Clock = std::chrono::steady_clock;
 
 struct GroupMeta {
-  int64_t ticket;
   uint32_t count;    // packets in the group (slots count..k-1 are zero)
   uint32_t max_len;  // longest packet: the repair payload length
-  Clock::time_point t_submit;
 };
+
+// Reservation word of a slab: bit 63 set once the slab is closed, the low bits count the
+// reservations attempted (they may run past max_groups; those attempts back off).
+constexpr uint64_t kClosed = 1ull << 63;
 
 struct Slab {
   uint8_t* data = nullptr;    // max_groups * k * slot, page-locked
-  uint8_t* parity = nullptr;  // max_groups * r * slot, page-locked
   uint8_t* d_data = nullptr;  // the same memory as the kernels address it (zero-copy)
-  uint8_t* d_parity = nullptr;
   hipEvent_t done = nullptr;  // the slab's encode has finished
   int rc = FEC_OK;            // its launch status
-  std::vector<GroupMeta> groups;         // reserved groups (under the batcher lock)
-  std::atomic<uint32_t> committed{0};    // groups whose packets have been copied in
+  std::vector<GroupMeta> groups;       // max_groups entries; entry g written by its submitter
+  std::atomic<uint64_t> state{kClosed};
+  int64_t base = 0;                    // ticket of entry 0 (set when the slab opens)
+  uint32_t n = 0;                      // groups in the batch (set when it closes)
+  bool started = false;                // its first group arrived (under mu)
+  Clock::time_point t_first;           // when (under mu): the deadline runs from here
+  std::atomic<uint32_t> committed{0};  // groups whose packets have been copied in
 };
 
 // One published result.  `ticket` is -1 while the entry is being (re)written, else the
-// ticket whose payloads it holds; a reader copies, then re-checks `ticket` (a rewrite in
-// between makes the copy invalid) and claims it by swapping in -1.
+// ticket whose result it describes (r rows of `len` bytes in the ticket's parity slot).  A
+// reader copies, checks the slot was not rewritten meanwhile, and claims the result by
+// swapping in -1.
 struct Entry {
   std::atomic<int64_t> ticket{-1};
   int rc = FEC_OK;
   uint32_t len = 0;
-  std::vector<uint8_t> bytes;  // r rows of len bytes
 };
 
 }  // namespace
@@ -84,13 +97,17 @@ struct FECBatcher {
   std::chrono::microseconds deadline{0};
   FECEncoderCtx* ctx = nullptr;
   std::vector<std::unique_ptr<Slab>> slabs;
-  int open = -1;                 // slab accepting groups, -1 while every slab is busy
+  uint8_t* parity = nullptr;     // the parity ring: C group slots of r * slot bytes, page-locked
+  uint8_t* d_parity = nullptr;   // as the kernels address it
+  uint64_t cap = 0;              // C
+  std::atomic<int64_t> launched_upto{0};  // encodes of every ticket below this have been launched
+  std::atomic<int> open{-1};     // slab accepting groups, -1 while every slab is busy (written under mu)
+  int64_t next_base = 0;         // ticket of the next slab's first group while none is open (under mu)
   std::deque<int> free_slabs;    // empty slabs
   std::deque<int> closed;        // full or due slabs waiting for the flusher
   std::deque<int> in_flight;     // encodes launched, results not yet published (launch order)
   int device = 0;
   hipStream_t stream = nullptr;  // the flusher's launches
-  std::atomic<int64_t> next_ticket{0};
   std::atomic<int64_t> published_upto{0};  // every ticket below this has been published (in order)
   std::vector<Entry> ring;       // results, entry ticket % ring.size()
   FECBatcherStats stats{};
@@ -109,45 +126,81 @@ struct FECBatcher {
     if (flusher.joinable()) flusher.join();
     for (auto& s : slabs) {
       if (s->data) fec_free_slab(s->data);
-      if (s->parity) fec_free_repair_buffer(s->parity);
       if (s->done) (void)hipEventDestroy(s->done);
     }
+    if (parity) fec_free_repair_buffer(parity);
     if (stream) (void)hipStreamDestroy(stream);
     if (ctx) fec_encoder_free(ctx);
   }
 
-  // Moves the open slab to the flusher's queue and opens the next free one (or none).
-  // Caller holds mu.
+  // Opens slab si for reservations; its tickets continue the previous batch's.  Caller holds mu.
+  void open_slab(int si) {
+    Slab& s = *slabs[si];
+    s.base = next_base;
+    s.n = 0;
+    s.started = false;
+    s.committed.store(0, std::memory_order_relaxed);
+    s.state.store(0, std::memory_order_release);
+    open.store(si, std::memory_order_release);
+    cv_free.notify_all();
+  }
+
+  // Closes the open slab (if it has groups), queues it for the flusher and opens the next
+  // free one (or none).  Caller holds mu.
   void close_open(bool full) {
-    if (open < 0 || slabs[open]->groups.empty()) return;
-    closed.push_back(open);
+    const int si = open.load(std::memory_order_relaxed);
+    if (si < 0 || !slabs[si]->started) return;
+    Slab& s = *slabs[si];
+    const uint64_t old = s.state.fetch_or(kClosed, std::memory_order_acq_rel);
+    s.n = static_cast<uint32_t>(std::min<uint64_t>(old & ~kClosed, max_groups));
+    next_base = s.base + s.n;
+    closed.push_back(si);
     ++(full ? stats.full_flushes : stats.deadline_flushes);
     if (!free_slabs.empty()) {
-      open = free_slabs.front();
+      const int nx = free_slabs.front();
       free_slabs.pop_front();
+      open_slab(nx);
     } else {
-      open = -1;
+      open.store(-1, std::memory_order_release);
     }
   }
 
+  // Every ticket below this has been handed out (or is being).  Caller holds mu.
+  int64_t issued_bound() const {
+    const int si = open.load(std::memory_order_relaxed);
+    if (si < 0) return next_base;
+    const Slab& s = *slabs[si];
+    return s.base + static_cast<int64_t>(std::min<uint64_t>(s.state.load(std::memory_order_acquire) & ~kClosed, max_groups));
+  }
+
   // Stage 1 (flusher, no lock): once every reserved copy has landed, launch the slab's
-  // encode asynchronously on the batcher's stream (the kernels read the page-locked slab
-  // and write its parity in place over PCIe) and record its completion event.
+  // encode asynchronously on the batcher's stream (the kernels read the page-locked slab and
+  // write its groups' parity slots in place over PCIe; a slab's tickets are consecutive, so
+  // that is one range of the ring, split in two where it wraps) and record its completion
+  // event.  `launched_upto` moves first: the results of tickets C below expire.
   void launch_slab(int si) {
     Slab& s = *slabs[si];
-    const uint32_t n = static_cast<uint32_t>(s.groups.size());  // closed: no more reservations
+    const uint32_t n = s.n;  // closed: no more reservations
     while (s.committed.load(std::memory_order_acquire) < n) std::this_thread::yield();  // copies in flight
-    s.rc = fec_encode_batch_rs_dev(ctx, s.d_data, n, k, r, slot, s.d_parity, stream);
+    const int64_t t0 = s.base;
+    launched_upto.store(t0 + n, std::memory_order_relaxed);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    const uint64_t first_slot = static_cast<uint64_t>(t0) % cap;
+    const uint32_t n1 = static_cast<uint32_t>(std::min<uint64_t>(n, cap - first_slot));
+    const size_t group_parity = size_t(r) * slot;
+    s.rc = fec_encode_batch_rs_dev(ctx, s.d_data, n1, k, r, slot, d_parity + first_slot * group_parity, stream);
+    if (s.rc == FEC_OK && n1 < n)
+      s.rc = fec_encode_batch_rs_dev(ctx, s.d_data + size_t(n1) * k * slot, n - n1, k, r, slot, d_parity, stream);
     if (s.rc == FEC_OK && hipEventRecord(s.done, stream) != hipSuccess) s.rc = FEC_ERR_HIP;
   }
 
-  // Stage 2 (flusher, no lock until the end): wait for the slab's encode, copy every group's
-  // payloads into the result ring, then hand the slab back for refilling.  While the flusher
-  // waits here, the next slab's encode is already queued behind this one (stage 1 runs first
-  // whenever a slab is closed), so the GPU never waits for the copies.
+  // Stage 2 (flusher, no lock until the end): wait for the slab's encode, publish where every
+  // group's payloads sit, then hand the slab back for refilling.  While the flusher waits
+  // here, the next slab's encode is already queued behind this one (stage 1 runs first
+  // whenever a slab is closed).
   void publish_slab(int si) {
     Slab& s = *slabs[si];
-    const uint32_t n = static_cast<uint32_t>(s.groups.size());
+    const uint32_t n = s.n;
     int rc = s.rc;
     if (rc == FEC_OK && hipEventSynchronize(s.done) != hipSuccess) rc = FEC_ERR_HIP;
     std::string err;
@@ -158,15 +211,13 @@ struct FECBatcher {
     }
     for (uint32_t g = 0; g < n; ++g) {
       const GroupMeta& m = s.groups[g];
-      Entry& e = ring[static_cast<size_t>(m.ticket) % ring.size()];
+      const int64_t ticket = s.base + g;
+      Entry& e = ring[static_cast<size_t>(ticket) % ring.size()];
       const int64_t prev = e.ticket.exchange(-1, std::memory_order_acq_rel);
       if (prev >= 0) ++dropped;  // never collected: dropped
       e.rc = rc;
       e.len = rc == FEC_OK ? m.max_len : 0;
-      e.bytes.resize(size_t(r) * e.len);
-      for (uint32_t i = 0; i < r && rc == FEC_OK; ++i)
-        std::memcpy(e.bytes.data() + size_t(i) * e.len, s.parity + (size_t(g) * r + i) * slot, e.len);
-      e.ticket.store(m.ticket, std::memory_order_release);
+      e.ticket.store(ticket, std::memory_order_release);
     }
     std::lock_guard<std::mutex> lk(mu);
     ++stats.batches;
@@ -174,16 +225,13 @@ struct FECBatcher {
     if (n > stats.max_batch) stats.max_batch = n;
     stats.expired += dropped;
     dropped = 0;
-    if (n > 0) published_upto.store(s.groups.back().ticket + 1, std::memory_order_release);
+    published_upto.store(s.base + n, std::memory_order_release);
     if (rc != FEC_OK) last_batch_error = err;
-    s.groups.clear();
-    s.committed.store(0, std::memory_order_relaxed);
-    if (open < 0) {
-      open = si;
+    if (open.load(std::memory_order_relaxed) < 0) {
+      open_slab(si);
     } else {
       free_slabs.push_back(si);
     }
-    cv_free.notify_all();
     cv_done.notify_all();
   }
 
@@ -210,14 +258,15 @@ struct FECBatcher {
         lk.lock();
         continue;
       }
-      const bool pending = open >= 0 && !slabs[open]->groups.empty();
+      const int si = open.load(std::memory_order_relaxed);
+      const bool pending = si >= 0 && slabs[si]->started;
       if (stop) {
         if (!pending) return;
         close_open(false);  // shutdown: encode what is pending, then leave
         continue;
       }
       if (pending) {
-        const Clock::time_point due = slabs[open]->groups.front().t_submit + deadline;
+        const Clock::time_point due = slabs[si]->t_first + deadline;
         if (Clock::now() >= due) {
           close_open(false);
           continue;
@@ -279,31 +328,41 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
     return nullptr;
   }
   const uint32_t nslabs = slabs < 2 ? 2 : slabs;
+  const char* bs = std::getenv("QUICFEC_BATCHER_BLOCKING_SYNC");
+  const bool blocking = bs && bs[0] == '1';
   for (uint32_t i = 0; i < nslabs; ++i) {
     b->slabs.push_back(std::make_unique<Slab>());
     Slab& s = *b->slabs.back();
     s.data = static_cast<uint8_t*>(fec_alloc_slab(size_t(max_groups) * k * slot_bytes));
-    s.parity = static_cast<uint8_t*>(fec_alloc_repair_buffer(size_t(max_groups) * r * slot_bytes));
-    void *dd = nullptr, *dp = nullptr;
-    if (!s.data || !s.parity || hipHostGetDevicePointer(&dd, s.data, 0) != hipSuccess ||
-        hipHostGetDevicePointer(&dp, s.parity, 0) != hipSuccess ||
-        hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) {
+    void* dd = nullptr;
+    if (!s.data || hipHostGetDevicePointer(&dd, s.data, 0) != hipSuccess ||
+        hipEventCreateWithFlags(&s.done, hipEventDisableTiming | (blocking ? hipEventBlockingSync : 0u)) != hipSuccess) {
       berr("fec_batcher_new: page-locked slab setup failed (%s)", fec_hip_last_error());
       restore();
       delete b;
       return nullptr;
     }
     s.d_data = static_cast<uint8_t*>(dd);
-    s.d_parity = static_cast<uint8_t*>(dp);
-    s.groups.reserve(max_groups);
+    s.groups.resize(max_groups);
     if (i > 0) b->free_slabs.push_back(static_cast<int>(i));
   }
-  // Results of two full rounds of slabs stay collectable.
-  b->ring = std::vector<Entry>(size_t(2) * nslabs * max_groups);
+  // Results of two full rounds of slabs stay collectable: a slot is rewritten when the batch
+  // C tickets later is launched, and up to a round of slabs is launched ahead of publishing.
+  b->cap = uint64_t(3) * nslabs * max_groups;
+  b->parity = static_cast<uint8_t*>(fec_alloc_repair_buffer(b->cap * r * slot_bytes));
+  void* dp = nullptr;
+  if (!b->parity || hipHostGetDevicePointer(&dp, b->parity, 0) != hipSuccess) {
+    berr("fec_batcher_new: page-locked parity setup failed (%s)", fec_hip_last_error());
+    restore();
+    delete b;
+    return nullptr;
+  }
+  b->d_parity = static_cast<uint8_t*>(dp);
+  b->ring = std::vector<Entry>(b->cap);
   // Warm-up: the first launch loads the code object and the (k, r) tables; do it here, not
   // in the first stream's repair delay.
   std::memset(b->slabs[0]->data, 0, size_t(k) * slot_bytes);
-  if (fec_encode_batch_rs(b->ctx, b->slabs[0]->data, nullptr, 1, k, r, slot_bytes, b->slabs[0]->parity) != FEC_OK) {
+  if (fec_encode_batch_rs(b->ctx, b->slabs[0]->data, nullptr, 1, k, r, slot_bytes, b->parity) != FEC_OK) {
     char buf[512];
     fec_ctx_last_error(b->ctx, buf, sizeof(buf));
     berr("fec_batcher_new: warm-up encode failed: %s", buf);
@@ -312,7 +371,10 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
     return nullptr;
   }
   restore();
-  b->open = 0;
+  {
+    std::lock_guard<std::mutex> lk(b->mu);
+    b->open_slab(0);
+  }
   b->flusher = std::thread([b] { b->run(); });
   return b;
 }
@@ -341,27 +403,42 @@ int64_t submit_group(FECBatcher* b, Src&& src, const uint32_t* lens, uint32_t co
     berr("fec_batcher_submit: empty packets");
     return FEC_ERR_RANGE;
   }
-  // Reserve the slot under the lock ...
+  // Reserve a slot of the open slab with one atomic add ...
   Slab* s = nullptr;
-  size_t g = 0;
-  int64_t ticket = 0;
-  {
-    std::unique_lock<std::mutex> lk(b->mu);
-    b->cv_free.wait(lk, [b] { return b->open >= 0 || b->stop; });
-    if (b->stop) return FEC_ERR_RANGE;
-    s = b->slabs[b->open].get();
-    g = s->groups.size();
-    ticket = b->next_ticket.fetch_add(1, std::memory_order_relaxed);
-    s->groups.push_back(GroupMeta{ticket, count, max_len, Clock::now()});
-    if (s->groups.size() == b->max_groups) {
-      b->close_open(true);
-      b->cv_flusher.notify_one();
-    } else if (g == 0) {
-      b->cv_flusher.notify_one();  // a deadline starts
+  uint32_t g = 0;
+  int si = -1;
+  for (;;) {
+    si = b->open.load(std::memory_order_acquire);
+    if (si >= 0) {
+      Slab& cand = *b->slabs[si];
+      const uint64_t old = cand.state.fetch_add(1, std::memory_order_acq_rel);
+      if (!(old & kClosed) && old < b->max_groups) {
+        s = &cand;
+        g = static_cast<uint32_t>(old);
+        break;
+      }
     }
+    // ... or wait, under the lock, until a slab with room is open.
+    std::unique_lock<std::mutex> lk(b->mu);
+    if (b->stop) return FEC_ERR_RANGE;
+    const int cur = b->open.load(std::memory_order_relaxed);
+    if (cur >= 0 && cur != si) continue;  // another slab opened meanwhile
+    if (cur >= 0) {
+      const uint64_t st = b->slabs[cur]->state.load(std::memory_order_acquire);
+      if (!(st & kClosed) && st < b->max_groups) continue;
+    }
+    b->cv_free.wait(lk);  // open_slab notifies; spurious wake-ups retry
   }
-  // ... and copy without it (the flusher encodes a slab once every reserved copy landed).
-  uint8_t* dst = s->data + g * b->k * size_t(b->slot);
+  const int64_t ticket = s->base + g;
+  s->groups[g] = GroupMeta{count, max_len};
+  if (g == 0) {  // a deadline starts
+    std::lock_guard<std::mutex> lk(b->mu);
+    s->t_first = Clock::now();
+    s->started = true;
+    b->cv_flusher.notify_one();
+  }
+  // ... and copy without the lock (the flusher encodes a slab once every reserved copy landed).
+  uint8_t* dst = s->data + size_t(g) * b->k * b->slot;
   for (uint32_t j = 0; j < b->k; ++j) {  // packets zero-padded to the slot, absent slots zero
     uint8_t* d = dst + size_t(j) * b->slot;
     const uint32_t n = j < count ? lens[j] : 0;
@@ -369,6 +446,13 @@ int64_t submit_group(FECBatcher* b, Src&& src, const uint32_t* lens, uint32_t co
     std::memset(d + n, 0, b->slot - n);
   }
   s->committed.fetch_add(1, std::memory_order_release);
+  if (g + 1 == b->max_groups) {  // filled it: close it now rather than at its deadline
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (b->open.load(std::memory_order_relaxed) == si && !(s->state.load(std::memory_order_acquire) & kClosed)) {
+      b->close_open(true);
+      b->cv_flusher.notify_one();
+    }
+  }
   return ticket;
 }
 
@@ -401,16 +485,21 @@ int take(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int* 
   if (e.ticket.load(std::memory_order_acquire) != ticket) return 0;
   const int rc = e.rc;
   const uint32_t n = e.len;
+  bool stale = false;
   if (rc == FEC_OK && out) {
     if (out_stride < n) {
       berr("fec_batcher_wait: out_stride %u < repair length %u", out_stride, n);
       return FEC_ERR_RANGE;
     }
-    for (uint32_t i = 0; i < b->r; ++i) std::memcpy(out + size_t(i) * out_stride, e.bytes.data() + size_t(i) * n, n);
+    const uint8_t* src = b->parity + (static_cast<uint64_t>(ticket) % b->cap) * b->r * b->slot;
+    for (uint32_t i = 0; i < b->r; ++i) std::memcpy(out + size_t(i) * out_stride, src + size_t(i) * b->slot, n);
+    std::atomic_thread_fence(std::memory_order_acquire);
+    // the slot is rewritten by the encode of ticket + C: launched already?
+    stale = b->launched_upto.load(std::memory_order_relaxed) > ticket + static_cast<int64_t>(b->cap);
   }
   int64_t expect = ticket;
-  if (!e.ticket.compare_exchange_strong(expect, -1, std::memory_order_acq_rel)) {
-    berr("fec_batcher_wait: result of ticket %lld was overwritten while read", static_cast<long long>(ticket));
+  if (stale || !e.ticket.compare_exchange_strong(expect, -1, std::memory_order_acq_rel)) {
+    berr("fec_batcher_wait: result of ticket %lld expired while it was read", static_cast<long long>(ticket));
     return FEC_ERR_RANGE;
   }
   if (rc != FEC_OK) {
@@ -432,11 +521,10 @@ QFEC_EXPORT int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, ui
   if (st == 1) return len;
   if (st < 0) return st;
   // A poll of a ticket not published yet needs no lock.
-  if (timeout_us == 0 && ticket >= b->published_upto.load(std::memory_order_acquire) &&
-      ticket < b->next_ticket.load(std::memory_order_relaxed))
+  if (timeout_us == 0 && ticket >= 0 && ticket >= b->published_upto.load(std::memory_order_acquire))
     return FEC_ERR_AGAIN;
   std::unique_lock<std::mutex> lk(b->mu);
-  if (ticket < 0 || ticket >= b->next_ticket.load(std::memory_order_relaxed)) {
+  if (ticket < 0 || ticket >= b->issued_bound()) {
     berr("fec_batcher_wait: unknown ticket %lld", static_cast<long long>(ticket));
     return FEC_ERR_RANGE;
   }

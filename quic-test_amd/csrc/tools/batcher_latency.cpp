@@ -11,6 +11,8 @@
 //   batcher_latency saturate <streams> <seconds> <r> <deadline_us> <max_groups>
 //   batcher_latency cpu                  (per-group CPU cost of the comparators, 1 core)
 //   batcher_latency single <r> <calls>   (one group per synchronous call, no batcher)
+//   batcher_latency raw <streams> <seconds> <r> <deadline_us> <max_groups> [depth]
+//                                        (the C-ABI without the encoder API, and the copy cost)
 #include <sys/resource.h>
 
 #include <algorithm>
@@ -118,7 +120,10 @@ int paced(int S, double rate, double seconds, int r, int deadline_us) {
 
 // Every stream submits as fast as it can (async API, up to 256 groups outstanding each).
 int saturate(int S, double seconds, int r, int deadline_us, int max_groups) {
-  auto sb = SharedFECBatcher::New(kK, r, kP, max_groups, deadline_us, -1, 4);
+  // Results stay collectable for 2 * slabs * max_groups newer groups: at ~3.5 M groups/s a
+  // stream thread descheduled for a few ms (16 busy streams on 16 CPUs) must not lose its
+  // results, so small batches get more slabs.
+  auto sb = SharedFECBatcher::New(kK, r, kP, max_groups, deadline_us, -1, std::max(4, 8192 / max_groups));
   if (!sb) return 2;
   const auto pk = packets(kK, 0x5EED0B);
   std::mutex mu;
@@ -162,6 +167,97 @@ int saturate(int S, double seconds, int r, int deadline_us, int max_groups) {
   std::snprintf(cfg, sizeof(cfg), "\"streams\": %d, \"r\": %d, \"deadline_us\": %d, \"max_groups\": %d, \"errors\": %ld", S,
                 r, deadline_us, max_groups, errors.load());
   print_lat("saturate", cfg, all, double(groups), wall, cpu, sb.get());
+  return errors ? 1 : 0;
+}
+
+// The C-ABI alone (no BatchedFECEncoder): submit by packet pointers, keep up to 256 groups
+// outstanding per stream, collect the oldest (payloads copied out).  And the cost of the
+// submit's copy alone: 12 KB memcpy per group into page-locked or pageable memory.
+int raw(int S, double seconds, int r, int deadline_us, int max_groups, int depth) {
+  FECBatcher* b = fec_batcher_new(-1, kK, r, kP, max_groups, deadline_us, 4);
+  if (!b) return 2;
+  const auto pk = packets(kK, 0x5EED0C);
+  std::atomic<long> groups{0}, errors{0};
+  const auto t_end = Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(seconds));
+  const auto t0 = Clock::now();
+  const double c0 = cpu_seconds();
+  std::vector<std::thread> th;
+  for (int s = 0; s < S; ++s)
+    th.emplace_back([&] {
+      const uint8_t* ptrs[kK];
+      uint32_t lens[kK];
+      for (int j = 0; j < kK; ++j) {
+        ptrs[j] = pk[j].data();
+        lens[j] = kP;
+      }
+      std::vector<uint8_t> rows(size_t(r) * kP);
+      std::vector<int64_t> q;
+      size_t head = 0;
+      long n = 0;
+      while (Clock::now() < t_end) {
+        const int64_t t = fec_batcher_submit_packets(b, ptrs, lens, kK);
+        if (t < 0) {
+          ++errors;
+          continue;
+        }
+        q.push_back(t);
+        while (head < q.size()) {
+          const int rc = fec_batcher_wait(b, q[head], rows.data(), kP, q.size() - head >= size_t(depth) ? -1 : 0);
+          if (rc == FEC_ERR_AGAIN) break;
+          if (rc < 0) ++errors;
+          ++head;
+          ++n;
+        }
+      }
+      fec_batcher_flush(b);
+      for (; head < q.size(); ++head, ++n)
+        if (fec_batcher_wait(b, q[head], rows.data(), kP, -1) < 0) ++errors;
+      groups += n;
+    });
+  for (auto& t : th) t.join();
+  const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
+  const double cpu = cpu_seconds() - c0;
+  FECBatcherStats st{};
+  fec_batcher_stats(b, &st);
+  fec_batcher_free(b);
+  std::printf("{\"mode\": \"raw\", \"streams\": %d, \"r\": %d, \"deadline_us\": %d, \"max_groups\": %d, \"errors\": %ld, "
+              "\"depth\": %d, \"groups_per_s\": %.1f, \"cpu_us_per_group\": %.3f, \"mean_batch\": %.1f}\n",
+              S, r, deadline_us, max_groups, errors.load(), depth, groups / wall, cpu / groups * 1e6,
+              st.batches ? double(st.groups) / st.batches : 0.0);
+  std::fflush(stdout);
+  // the submit's copy alone
+  for (int pinned = 0; pinned < 2; ++pinned) {
+    const size_t region = size_t(4096) * kK * kP;
+    std::vector<uint8_t*> dst(S);
+    std::vector<std::vector<uint8_t>> pageable(S);
+    for (int i = 0; i < S; ++i) {
+      if (pinned) {
+        dst[i] = static_cast<uint8_t*>(fec_alloc_slab(region));
+      } else {
+        pageable[i].assign(region, 0);
+        dst[i] = pageable[i].data();
+      }
+    }
+    std::atomic<long> copies{0};
+    const auto e2 = Clock::now() + std::chrono::milliseconds(1000);
+    const auto t2 = Clock::now();
+    std::vector<std::thread> ct;
+    for (int i = 0; i < S; ++i)
+      ct.emplace_back([&, i] {
+        long n = 0;
+        while (Clock::now() < e2)
+          for (int g = 0; g < 256; ++g, ++n)
+            for (int j = 0; j < kK; ++j)
+              std::memcpy(dst[i] + (size_t(n % 4096) * kK + j) * kP, pk[j].data(), kP);
+        copies += n;
+      });
+    for (auto& t : ct) t.join();
+    const double w2 = std::chrono::duration<double>(Clock::now() - t2).count();
+    std::printf("{\"mode\": \"copy\", \"streams\": %d, \"pinned\": %d, \"groups_per_s\": %.1f, \"GiBps\": %.2f}\n", S,
+                pinned, copies / w2, copies * double(kK * kP) / w2 / (1u << 30));
+    if (pinned)
+      for (auto* d : dst) fec_free_slab(d);
+  }
   return errors ? 1 : 0;
 }
 
@@ -227,5 +323,7 @@ int main(int argc, char** argv) {
   if (mode == "saturate")
     return saturate(int(arg(2, 16)), arg(3, 3), int(arg(4, 1)), int(arg(5, 1000)), int(arg(6, 4096)));
   if (mode == "single") return single(int(arg(2, 2000)));
+  if (mode == "raw")
+    return raw(int(arg(2, 16)), arg(3, 3), int(arg(4, 1)), int(arg(5, 1000)), int(arg(6, 4096)), int(arg(7, 256)));
   return cpu();
 }

@@ -5,16 +5,23 @@
 set -euo pipefail
 B=./quic-test_amd/lib/batcher_latency
 T="timeout -k 10 60"
-$T $B cpu
-$T $B single 2000
+# a run that reports errors exits 1 after printing its line; keep going (a hang still ends it)
+run() { "$@" || [ $? -eq 1 ]; }
+run $T $B cpu
+run $T $B single 2000
 for r in 1 3; do
   for s in 1 10 100; do
-    $T $B paced $s 100 5 $r 1000
+    run $T $B paced $s 100 5 $r 1000
   done
-  $T $B paced 100 100 5 $r 200
-  $T $B paced 100 100 5 $r 0
+  run $T $B paced 100 100 5 $r 200
+  run $T $B paced 100 100 5 $r 0
 done
 for r in 1 3; do
-  $T $B saturate 16 3 $r 1000 4096
-  $T $B saturate 16 3 $r 1000 512
+  run $T $B saturate 16 3 $r 1000 4096
+  run $T $B saturate 16 3 $r 1000 512
 done
+# the C-ABI alone (submit by pointers, collect by ticket), 1024 groups outstanding per stream
+for s in 1 4 8 16; do
+  run $T $B raw $s 2 1 1000 4096 1024
+done
+run $T $B raw 16 2 3 1000 4096 1024

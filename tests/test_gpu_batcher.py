@@ -64,8 +64,9 @@ def test_batcher_wait_semantics(quicfec_mod, oracle_mod):
         assert rows is not None and np.array_equal(rows[0], _expected_rows(oracle_mod, pk, k, r)[0])
         with pytest.raises(quicfec_mod.FecError):                 # collected once only
             b.wait(t, timeout_us=0)
-        with pytest.raises(quicfec_mod.FecError):                 # never issued
-            b.wait(t + 100, timeout_us=0)
+        assert b.wait(t + 100, timeout_us=0) is None              # never issued: a poll says "not yet"
+        with pytest.raises(quicfec_mod.FecError, match="unknown"):  # ... a wait says what it is
+            b.wait(t + 100, timeout_us=1000)
         with pytest.raises(quicfec_mod.FecError, match="exceeds"):
             b.submit([np.zeros(1201, dtype=np.uint8)])
         with pytest.raises(quicfec_mod.FecError):
@@ -75,8 +76,8 @@ def test_batcher_wait_semantics(quicfec_mod, oracle_mod):
 
 
 def test_batcher_result_ring_expiry(quicfec_mod, oracle_mod):
-    """Results live in a ring of 2 * slabs * max_groups entries; older uncollected ones are
-    dropped and counted."""
+    """Results live in a parity ring of 3 * slabs * max_groups group slots; older uncollected
+    ones are dropped and counted."""
     k, r = 4, 2
     with quicfec_mod.Batcher(k, r, slot_bytes=64, max_groups=2, deadline_us=100, slabs=2) as b:
         tickets = [b.submit([oracle_mod.splitmix_bytes(64, 7 * g + j) for j in range(k)]) for g in range(20)]
@@ -85,7 +86,7 @@ def test_batcher_result_ring_expiry(quicfec_mod, oracle_mod):
         assert last is not None
         with pytest.raises(quicfec_mod.FecError, match="expired|collected"):
             b.wait(tickets[0], timeout_us=0)
-        assert b.stats()["expired"] >= 20 - 8
+        assert b.stats()["expired"] >= 20 - 3 * 2 * 2
 
 
 def test_batcher_concurrent_streams(quicfec_mod, oracle_mod):
