@@ -652,6 +652,76 @@ static void TestBatcherDeadline() {
   CHECK(fec_batcher_wait(nullptr, 0, nullptr, 0, 0) == FEC_ERR_NULL);
 }
 
+// Reservation races: 16 threads on the C-ABI, 7-group slabs (filled and closed by a
+// submitter), 2 slabs (submitters wait for a free one), deadlines of 0 and 20 us (the flusher
+// closes slabs while submitters reserve), variable packet counts and lengths, results
+// collected in a random order of polls and blocking waits.  Every row 0 returned must be
+// the XOR; with 42 result slots (3 * 2 slabs * 7) results also expire while waiters read
+// them, and each expiry must surface as FEC_ERR_RANGE, counted once in the stats.
+static void TestBatcherReservationStress() {
+  for (int deadline_us : {0, 20}) {
+    const uint32_t k = 6, r = 2, slot = 256, S = 16, G = 600;
+    FECBatcher* b = fec_batcher_new(-1, k, r, slot, 7, deadline_us, 2);
+    CHECK(b != nullptr);
+    if (!b) return;
+    std::atomic<int> bad{0};
+    std::atomic<uint64_t> expired{0};
+    std::vector<std::thread> th;
+    for (uint32_t s = 0; s < S; ++s)
+      th.emplace_back([&, s] {
+        std::mt19937_64 rng(1234 + s + 100 * deadline_us);
+        std::vector<std::pair<int64_t, Bytes>> pending;  // ticket, expected row 0
+        std::vector<uint8_t> rows(size_t(r) * slot);
+        auto collect = [&](size_t i, int64_t timeout) {
+          const int n = fec_batcher_wait(b, pending[i].first, rows.data(), slot, timeout);
+          if (n == FEC_ERR_AGAIN) return false;
+          if (n == FEC_ERR_RANGE) {
+            ++expired;
+          } else if (n != int(pending[i].second.size()) ||
+              std::memcmp(rows.data(), pending[i].second.data(), pending[i].second.size()) != 0)
+            ++bad;
+          pending.erase(pending.begin() + i);
+          return true;
+        };
+        for (uint32_t g = 0; g < G; ++g) {
+          const uint32_t count = 1 + rng() % k;
+          std::vector<Bytes> pk;
+          std::vector<const uint8_t*> ptrs;
+          std::vector<uint32_t> lens;
+          Bytes x;
+          for (uint32_t j = 0; j < count; ++j) {
+            pk.push_back(rnd(1 + rng() % slot, rng()));
+            if (pk.back().size() > x.size()) x.resize(pk.back().size(), 0);
+            for (size_t i = 0; i < pk.back().size(); ++i) x[i] ^= pk.back()[i];
+          }
+          for (auto& p : pk) {
+            ptrs.push_back(p.data());
+            lens.push_back(uint32_t(p.size()));
+          }
+          const int64_t t = fec_batcher_submit_packets(b, ptrs.data(), lens.data(), count);
+          if (t < 0) {
+            ++bad;
+            continue;
+          }
+          pending.emplace_back(t, x);
+          if (rng() % 3 == 0) collect(rng() % pending.size(), rng() % 2 ? 0 : -1);
+          if (pending.size() > 3) collect(0, -1);
+        }
+        fec_batcher_flush(b);
+        while (!pending.empty()) collect(0, -1);
+      });
+    for (auto& t : th) t.join();
+    CHECK(bad == 0);
+    FECBatcherStats st{};
+    fec_batcher_stats(b, &st);
+    CHECK(st.groups == uint64_t(S) * G && st.max_batch <= 7 && st.expired == expired.load());
+    std::fprintf(stderr, "reservation stress, deadline %d us: %llu batches, %llu full, %llu results expired\n", deadline_us,
+                (unsigned long long)st.batches, (unsigned long long)st.full_flushes, (unsigned long long)st.expired);
+    if (deadline_us == 0) CHECK(st.full_flushes > 0 || st.deadline_flushes > 0);
+    fec_batcher_free(b);
+  }
+}
+
 int main() {
   TestContextErrorAcrossThreads();
   TestNewFECEncoder();
@@ -677,6 +747,7 @@ int main() {
   TestBatchedEncoderRSAsync();
   TestBatcherManyStreams();
   TestBatcherDeadline();
+  TestBatcherReservationStress();
   if (g_fail) {
     std::printf("FAILED %d of %d checks\n", g_fail, g_checks);
     return 1;
