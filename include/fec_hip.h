@@ -41,6 +41,7 @@ extern "C" {
 #define FEC_ERR_NODEV (-4)     /* no usable GPU                                   */
 #define FEC_ERR_NOMEM (-5)     /* device or pinned allocation failed              */
 #define FEC_ERR_AGAIN (-6)     /* fec_batcher_wait: not ready within the timeout   */
+#define FEC_ERR_UNRECOVERABLE (-7) /* fec_batcher_wait_rebuilt: too many shards lost */
 
 /* Number of visible HIP devices (0 when none or the runtime is unusable). */
 int fec_hip_device_count(void);
@@ -205,6 +206,24 @@ int64_t fec_batcher_submit_packets(FECBatcher* b, const uint8_t* const* packets,
  * may be dropped (FEC_ERR_RANGE).  Polling (timeout 0) a ticket never issued returns
  * FEC_ERR_AGAIN; a blocking wait on it returns FEC_ERR_RANGE. */
 int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int64_t timeout_us);
+
+/* ---- decoder batcher: the receiving side's FECDecoder rebuilds one group per call
+ * (decoder.go:216-287); a decoder batcher shares launches across every connection the same
+ * way.  k + r <= 64.  A connection submits a group's k + r shards (data shards, then parity
+ * rows 0..r-1; NULL = lost), each `len` <= slot_bytes bytes (the group's symbol length,
+ * shorter packets zero-padded as decoder.go:62-69 does), and gets a ticket.  The batch runs
+ * fec_recover_batch_rs_dev.  fec_batcher_flush / _stats / _free / _last_error apply. */
+FECBatcher* fec_batcher_new_decoder(int device, uint32_t k, uint32_t r, uint32_t slot_bytes, uint32_t max_groups,
+                                    uint32_t deadline_us, uint32_t slabs);
+int64_t fec_batcher_submit_shards(FECBatcher* b, const uint8_t* const* shards, uint32_t len);
+
+/* Waits as fec_batcher_wait and copies the group's rebuilt data shards, in ascending shard
+ * order, to out (row i at out + i*out_stride, `len` bytes each); *lost_mask (nullable) = the
+ * submitted erasure mask.  Returns the number of rows (0: nothing was lost),
+ * FEC_ERR_UNRECOVERABLE when more shards were lost than parity rows survive, FEC_ERR_AGAIN,
+ * or another negative code. */
+int fec_batcher_wait_rebuilt(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, uint64_t* lost_mask,
+                             int64_t timeout_us);
 
 /* Closes the pending batch now (e.g. at the end of a stream) instead of at its deadline. */
 int fec_batcher_flush(FECBatcher* b);

@@ -31,6 +31,12 @@
 // flusher copies nothing per group.  A result not collected before C newer groups are
 // launched (at least 2 * slabs * max_groups newer groups encoded) is dropped: the late wait
 // gets FEC_ERR_RANGE and stats.expired counts it.
+//
+// Decoder batchers (fec_batcher_new_decoder) do the same for the receiving side, whose
+// FECDecoder rebuilds one group per call (decoder.go:216-287): a connection submits a group's
+// received shards (NULL for the lost ones), the slab also holds the received parity rows and
+// the erasure masks, the batch runs fec_recover_batch_rs_dev, and the rebuilt data packets
+// land in the output ring (ticket t: r slots at t % C) next to a status byte per ticket.
 #include <hip/hip_runtime.h>
 #include <sys/prctl.h>
 
@@ -58,8 +64,9 @@ namespace {
 using Clock = std::chrono::steady_clock;
 
 struct GroupMeta {
-  uint32_t count;    // packets in the group (slots count..k-1 are zero)
-  uint32_t max_len;  // longest packet: the repair payload length
+  uint32_t count;    // packets in the group (slots count..k-1 are zero); decoder: unused
+  uint32_t max_len;  // longest packet: the repair payload length; decoder: the symbol length
+  uint64_t mask;     // decoder: lost shards (bit s = shard s)
 };
 
 // Reservation word of a slab: bit 63 set once the slab is closed, the low bits count the
@@ -69,6 +76,10 @@ constexpr uint64_t kClosed = 1ull << 63;
 struct Slab {
   uint8_t* data = nullptr;    // max_groups * k * slot, page-locked
   uint8_t* d_data = nullptr;  // the same memory as the kernels address it (zero-copy)
+  uint8_t* rparity = nullptr;   // decoder: the received parity rows, max_groups * r * slot
+  uint8_t* d_rparity = nullptr;
+  uint64_t* masks = nullptr;    // decoder: erasure masks, max_groups
+  uint64_t* d_masks = nullptr;
   hipEvent_t done = nullptr;  // the slab's encode has finished
   int rc = FEC_OK;            // its launch status
   std::vector<GroupMeta> groups;       // max_groups entries; entry g written by its submitter
@@ -88,17 +99,21 @@ struct Entry {
   std::atomic<int64_t> ticket{-1};
   int rc = FEC_OK;
   uint32_t len = 0;
+  uint64_t mask = 0;  // decoder: the group's lost shards
 };
 
 }  // namespace
 
 struct FECBatcher {
   uint32_t k = 0, r = 0, slot = 0, max_groups = 0;
+  bool decoder = false;
   std::chrono::microseconds deadline{0};
   FECEncoderCtx* ctx = nullptr;
   std::vector<std::unique_ptr<Slab>> slabs;
-  uint8_t* parity = nullptr;     // the parity ring: C group slots of r * slot bytes, page-locked
-  uint8_t* d_parity = nullptr;   // as the kernels address it
+  uint8_t* parity = nullptr;     // the output ring: C group slots of r * slot bytes, page-locked
+  uint8_t* d_parity = nullptr;   // as the kernels address it (encoder: parity; decoder: rebuilt)
+  uint8_t* status = nullptr;     // decoder: a status byte per ring slot (1 = unrecoverable)
+  uint8_t* d_status = nullptr;
   uint64_t cap = 0;              // C
   std::atomic<int64_t> launched_upto{0};  // encodes of every ticket below this have been launched
   std::atomic<int> open{-1};     // slab accepting groups, -1 while every slab is busy (written under mu)
@@ -126,9 +141,12 @@ struct FECBatcher {
     if (flusher.joinable()) flusher.join();
     for (auto& s : slabs) {
       if (s->data) fec_free_slab(s->data);
+      if (s->rparity) fec_free_slab(s->rparity);
+      if (s->masks) fec_free_slab(s->masks);
       if (s->done) (void)hipEventDestroy(s->done);
     }
     if (parity) fec_free_repair_buffer(parity);
+    if (status) fec_free_slab(status);
     if (stream) (void)hipStreamDestroy(stream);
     if (ctx) fec_encoder_free(ctx);
   }
@@ -188,9 +206,16 @@ struct FECBatcher {
     const uint64_t first_slot = static_cast<uint64_t>(t0) % cap;
     const uint32_t n1 = static_cast<uint32_t>(std::min<uint64_t>(n, cap - first_slot));
     const size_t group_parity = size_t(r) * slot;
-    s.rc = fec_encode_batch_rs_dev(ctx, s.d_data, n1, k, r, slot, d_parity + first_slot * group_parity, stream);
-    if (s.rc == FEC_OK && n1 < n)
-      s.rc = fec_encode_batch_rs_dev(ctx, s.d_data + size_t(n1) * k * slot, n - n1, k, r, slot, d_parity, stream);
+    auto part = [&](uint32_t g0, uint32_t cnt, uint64_t slot0) {
+      if (!decoder)
+        return fec_encode_batch_rs_dev(ctx, s.d_data + size_t(g0) * k * slot, cnt, k, r, slot,
+                                       d_parity + slot0 * group_parity, stream);
+      return fec_recover_batch_rs_dev(ctx, s.d_data + size_t(g0) * k * slot, s.d_rparity + size_t(g0) * r * slot,
+                                      s.d_masks + g0, cnt, k, r, slot, d_parity + slot0 * group_parity,
+                                      d_status + slot0, stream);
+    };
+    s.rc = part(0, n1, first_slot);
+    if (s.rc == FEC_OK && n1 < n) s.rc = part(n1, n - n1, 0);
     if (s.rc == FEC_OK && hipEventRecord(s.done, stream) != hipSuccess) s.rc = FEC_ERR_HIP;
   }
 
@@ -217,6 +242,8 @@ struct FECBatcher {
       if (prev >= 0) ++dropped;  // never collected: dropped
       e.rc = rc;
       e.len = rc == FEC_OK ? m.max_len : 0;
+      e.mask = m.mask;
+      if (decoder && rc == FEC_OK && status[static_cast<uint64_t>(ticket) % cap] != 0) e.rc = FEC_ERR_UNRECOVERABLE;
       e.ticket.store(ticket, std::memory_order_release);
     }
     std::lock_guard<std::mutex> lk(mu);
@@ -296,13 +323,27 @@ void berr(const char* fmt, ...) {
 
 }  // namespace
 
-QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint32_t slot_bytes, uint32_t max_groups,
-                                        uint32_t deadline_us, uint32_t slabs) {
-  if (k == 0 || r == 0 || k + r > 256 || slot_bytes == 0 || max_groups == 0) {
-    berr("fec_batcher_new: unsupported k=%u r=%u slot=%u max_groups=%u", k, r, slot_bytes, max_groups);
+namespace {
+
+// Page-locked allocation and its device address (zero-copy); false on failure.
+template <class T>
+bool alloc_mapped(size_t bytes, T** host, T** dev) {
+  *host = static_cast<T*>(fec_alloc_slab(bytes));
+  void* d = nullptr;
+  if (!*host || hipHostGetDevicePointer(&d, *host, 0) != hipSuccess) return false;
+  *dev = static_cast<T*>(d);
+  return true;
+}
+
+FECBatcher* create(bool decoder, int device, uint32_t k, uint32_t r, uint32_t slot_bytes, uint32_t max_groups,
+                   uint32_t deadline_us, uint32_t slabs) {
+  const char* fn = decoder ? "fec_batcher_new_decoder" : "fec_batcher_new";
+  if (k == 0 || r == 0 || k + r > (decoder ? 64u : 256u) || slot_bytes == 0 || max_groups == 0) {
+    berr("%s: unsupported k=%u r=%u slot=%u max_groups=%u", fn, k, r, slot_bytes, max_groups);
     return nullptr;
   }
   auto* b = new FECBatcher();
+  b->decoder = decoder;
   b->k = k;
   b->r = r;
   b->slot = slot_bytes;
@@ -310,7 +351,7 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
   b->deadline = std::chrono::microseconds(deadline_us);
   b->ctx = device < 0 ? fec_encoder_new(0.10, max_groups) : fec_encoder_new_device(0.10, max_groups, device);
   if (!b->ctx) {
-    berr("fec_batcher_new: %s", fec_hip_last_error());
+    berr("%s: %s", fn, fec_hip_last_error());
     delete b;
     return nullptr;
   }
@@ -322,7 +363,7 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
   };
   if (hipSetDevice(b->device) != hipSuccess ||
       hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
-    berr("fec_batcher_new: cannot create a stream on device %d", b->device);
+    berr("%s: cannot create a stream on device %d", fn, b->device);
     restore();
     delete b;
     return nullptr;
@@ -333,16 +374,17 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
   for (uint32_t i = 0; i < nslabs; ++i) {
     b->slabs.push_back(std::make_unique<Slab>());
     Slab& s = *b->slabs.back();
-    s.data = static_cast<uint8_t*>(fec_alloc_slab(size_t(max_groups) * k * slot_bytes));
-    void* dd = nullptr;
-    if (!s.data || hipHostGetDevicePointer(&dd, s.data, 0) != hipSuccess ||
+    bool ok = alloc_mapped(size_t(max_groups) * k * slot_bytes, &s.data, &s.d_data);
+    if (decoder)
+      ok = ok && alloc_mapped(size_t(max_groups) * r * slot_bytes, &s.rparity, &s.d_rparity) &&
+           alloc_mapped(size_t(max_groups) * sizeof(uint64_t), &s.masks, &s.d_masks);
+    if (!ok ||
         hipEventCreateWithFlags(&s.done, hipEventDisableTiming | (blocking ? hipEventBlockingSync : 0u)) != hipSuccess) {
-      berr("fec_batcher_new: page-locked slab setup failed (%s)", fec_hip_last_error());
+      berr("%s: page-locked slab setup failed (%s)", fn, fec_hip_last_error());
       restore();
       delete b;
       return nullptr;
     }
-    s.d_data = static_cast<uint8_t*>(dd);
     s.groups.resize(max_groups);
     if (i > 0) b->free_slabs.push_back(static_cast<int>(i));
   }
@@ -351,21 +393,35 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
   b->cap = uint64_t(3) * nslabs * max_groups;
   b->parity = static_cast<uint8_t*>(fec_alloc_repair_buffer(b->cap * r * slot_bytes));
   void* dp = nullptr;
-  if (!b->parity || hipHostGetDevicePointer(&dp, b->parity, 0) != hipSuccess) {
-    berr("fec_batcher_new: page-locked parity setup failed (%s)", fec_hip_last_error());
+  if (!b->parity || hipHostGetDevicePointer(&dp, b->parity, 0) != hipSuccess ||
+      (decoder && !alloc_mapped(b->cap, &b->status, &b->d_status))) {
+    berr("%s: page-locked output ring setup failed (%s)", fn, fec_hip_last_error());
     restore();
     delete b;
     return nullptr;
   }
   b->d_parity = static_cast<uint8_t*>(dp);
   b->ring = std::vector<Entry>(b->cap);
-  // Warm-up: the first launch loads the code object and the (k, r) tables; do it here, not
-  // in the first stream's repair delay.
-  std::memset(b->slabs[0]->data, 0, size_t(k) * slot_bytes);
-  if (fec_encode_batch_rs(b->ctx, b->slabs[0]->data, nullptr, 1, k, r, slot_bytes, b->parity) != FEC_OK) {
+  // Warm-up: the first launch loads the code object and the (k, r) tables (decoder: the
+  // recovery codebook too); do it here, not in the first stream's repair delay.
+  Slab& s0 = *b->slabs[0];
+  std::memset(s0.data, 0, size_t(k) * slot_bytes);
+  int wrc;
+  if (!decoder) {
+    wrc = fec_encode_batch_rs(b->ctx, s0.data, nullptr, 1, k, r, slot_bytes, b->parity);
+  } else {
+    std::memset(s0.rparity, 0, size_t(r) * slot_bytes);
+    s0.masks[0] = 1;  // shard 0 lost
+    wrc = fec_decode_prepare(b->ctx, k, r, nullptr);
+    if (wrc == FEC_OK)
+      wrc = fec_recover_batch_rs_dev(b->ctx, s0.d_data, s0.d_rparity, s0.d_masks, 1, k, r, slot_bytes, b->d_parity,
+                                     b->d_status, b->stream);
+    if (wrc == FEC_OK && hipStreamSynchronize(b->stream) != hipSuccess) wrc = FEC_ERR_HIP;
+  }
+  if (wrc != FEC_OK) {
     char buf[512];
     fec_ctx_last_error(b->ctx, buf, sizeof(buf));
-    berr("fec_batcher_new: warm-up encode failed: %s", buf);
+    berr("%s: warm-up launch failed: %s", fn, buf);
     restore();
     delete b;
     return nullptr;
@@ -379,13 +435,88 @@ QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint
   return b;
 }
 
+}  // namespace
+
+QFEC_EXPORT FECBatcher* fec_batcher_new(int device, uint32_t k, uint32_t r, uint32_t slot_bytes, uint32_t max_groups,
+                                        uint32_t deadline_us, uint32_t slabs) {
+  return create(false, device, k, r, slot_bytes, max_groups, deadline_us, slabs);
+}
+
+QFEC_EXPORT FECBatcher* fec_batcher_new_decoder(int device, uint32_t k, uint32_t r, uint32_t slot_bytes,
+                                                uint32_t max_groups, uint32_t deadline_us, uint32_t slabs) {
+  return create(true, device, k, r, slot_bytes, max_groups, deadline_us, slabs);
+}
+
 QFEC_EXPORT void fec_batcher_free(FECBatcher* b) { delete b; }
 
 namespace {
 
 // Shared by both submit forms: packet j is at src(j).
+// A reserved slot of the open slab: group g of slab si.
+struct Slot {
+  Slab* s = nullptr;
+  uint32_t g = 0;
+  int si = -1;
+  int64_t ticket = -1;  // read before the commit: once committed, the slab may be recycled
+};
+
+// Reserves a slot of the open slab with one atomic add, or waits, under the lock, until a
+// slab with room is open.  The slab's first group starts its deadline.  FEC_ERR_RANGE once
+// the batcher is stopping.
+int reserve(FECBatcher* b, Slot* out) {
+  for (;;) {
+    const int si = b->open.load(std::memory_order_acquire);
+    if (si >= 0) {
+      Slab& cand = *b->slabs[si];
+      const uint64_t old = cand.state.fetch_add(1, std::memory_order_acq_rel);
+      if (!(old & kClosed) && old < b->max_groups) {
+        *out = Slot{&cand, static_cast<uint32_t>(old), si, cand.base + static_cast<int64_t>(old)};
+        break;
+      }
+    }
+    std::unique_lock<std::mutex> lk(b->mu);
+    if (b->stop) return FEC_ERR_RANGE;
+    const int cur = b->open.load(std::memory_order_relaxed);
+    if (cur >= 0 && cur != si) continue;  // another slab opened meanwhile
+    if (cur >= 0) {
+      const uint64_t st = b->slabs[cur]->state.load(std::memory_order_acquire);
+      if (!(st & kClosed) && st < b->max_groups) continue;
+    }
+    b->cv_free.wait(lk);  // open_slab notifies; spurious wake-ups retry
+  }
+  if (out->g == 0) {  // a deadline starts
+    std::lock_guard<std::mutex> lk(b->mu);
+    out->s->t_first = Clock::now();
+    out->s->started = true;
+    b->cv_flusher.notify_one();
+  }
+  return FEC_OK;
+}
+
+// The slot's bytes have landed: count it, and close the slab now if this group filled it
+// (rather than at its deadline).  Nothing of the slab may be read after the count: the
+// flusher may encode, publish and reopen it at once.
+int64_t commit(FECBatcher* b, const Slot& sl) {
+  sl.s->committed.fetch_add(1, std::memory_order_release);
+  if (sl.g + 1 == b->max_groups) {
+    std::lock_guard<std::mutex> lk(b->mu);
+    // still this incarnation of the slab (it may have closed at its deadline and reopened)
+    if (b->open.load(std::memory_order_relaxed) == sl.si && sl.s->base == sl.ticket - sl.g &&
+        !(sl.s->state.load(std::memory_order_acquire) & kClosed)) {
+      b->close_open(true);
+      b->cv_flusher.notify_one();
+    }
+  }
+  return sl.ticket;
+}
+
+// Shared by both encoder submit forms: packet j is at src(j).
 template <class Src>
 int64_t submit_group(FECBatcher* b, Src&& src, const uint32_t* lens, uint32_t count) {
+  if (b->decoder) {
+    berr("fec_batcher_submit: a decoder batcher takes fec_batcher_submit_shards");
+    return FEC_ERR_RANGE;
+  }
   if (count == 0 || count > b->k) {
     berr("fec_batcher_submit: %u packets (group size k=%u)", count, b->k);
     return FEC_ERR_RANGE;
@@ -403,57 +534,18 @@ int64_t submit_group(FECBatcher* b, Src&& src, const uint32_t* lens, uint32_t co
     berr("fec_batcher_submit: empty packets");
     return FEC_ERR_RANGE;
   }
-  // Reserve a slot of the open slab with one atomic add ...
-  Slab* s = nullptr;
-  uint32_t g = 0;
-  int si = -1;
-  for (;;) {
-    si = b->open.load(std::memory_order_acquire);
-    if (si >= 0) {
-      Slab& cand = *b->slabs[si];
-      const uint64_t old = cand.state.fetch_add(1, std::memory_order_acq_rel);
-      if (!(old & kClosed) && old < b->max_groups) {
-        s = &cand;
-        g = static_cast<uint32_t>(old);
-        break;
-      }
-    }
-    // ... or wait, under the lock, until a slab with room is open.
-    std::unique_lock<std::mutex> lk(b->mu);
-    if (b->stop) return FEC_ERR_RANGE;
-    const int cur = b->open.load(std::memory_order_relaxed);
-    if (cur >= 0 && cur != si) continue;  // another slab opened meanwhile
-    if (cur >= 0) {
-      const uint64_t st = b->slabs[cur]->state.load(std::memory_order_acquire);
-      if (!(st & kClosed) && st < b->max_groups) continue;
-    }
-    b->cv_free.wait(lk);  // open_slab notifies; spurious wake-ups retry
-  }
-  const int64_t ticket = s->base + g;
-  s->groups[g] = GroupMeta{count, max_len};
-  if (g == 0) {  // a deadline starts
-    std::lock_guard<std::mutex> lk(b->mu);
-    s->t_first = Clock::now();
-    s->started = true;
-    b->cv_flusher.notify_one();
-  }
-  // ... and copy without the lock (the flusher encodes a slab once every reserved copy landed).
-  uint8_t* dst = s->data + size_t(g) * b->k * b->slot;
+  Slot sl;
+  if (reserve(b, &sl) != FEC_OK) return FEC_ERR_RANGE;
+  sl.s->groups[sl.g] = GroupMeta{count, max_len, 0};
+  // copied without the lock (the flusher encodes a slab once every reserved copy landed)
+  uint8_t* dst = sl.s->data + size_t(sl.g) * b->k * b->slot;
   for (uint32_t j = 0; j < b->k; ++j) {  // packets zero-padded to the slot, absent slots zero
     uint8_t* d = dst + size_t(j) * b->slot;
     const uint32_t n = j < count ? lens[j] : 0;
     if (n) std::memcpy(d, src(j), n);
     std::memset(d + n, 0, b->slot - n);
   }
-  s->committed.fetch_add(1, std::memory_order_release);
-  if (g + 1 == b->max_groups) {  // filled it: close it now rather than at its deadline
-    std::lock_guard<std::mutex> lk(b->mu);
-    if (b->open.load(std::memory_order_relaxed) == si && !(s->state.load(std::memory_order_acquire) & kClosed)) {
-      b->close_open(true);
-      b->cv_flusher.notify_one();
-    }
-  }
-  return ticket;
+  return commit(b, sl);
 }
 
 }  // namespace
@@ -476,31 +568,70 @@ QFEC_EXPORT int64_t fec_batcher_submit_packets(FECBatcher* b, const uint8_t* con
   return submit_group(b, [&](uint32_t j) { return packets[j]; }, lens, count);
 }
 
+QFEC_EXPORT int64_t fec_batcher_submit_shards(FECBatcher* b, const uint8_t* const* shards, uint32_t len) {
+  if (!b || !shards) return FEC_ERR_NULL;
+  if (!b->decoder) {
+    berr("fec_batcher_submit_shards: an encoder batcher takes fec_batcher_submit");
+    return FEC_ERR_RANGE;
+  }
+  if (len == 0 || len > b->slot) {
+    berr("fec_batcher_submit_shards: symbol length %u (slot %u bytes)", len, b->slot);
+    return FEC_ERR_RANGE;
+  }
+  uint64_t mask = 0;
+  for (uint32_t j = 0; j < b->k + b->r; ++j)
+    if (!shards[j]) mask |= 1ull << j;
+  Slot sl;
+  if (reserve(b, &sl) != FEC_OK) return FEC_ERR_RANGE;
+  sl.s->groups[sl.g] = GroupMeta{0, len, mask};
+  sl.s->masks[sl.g] = mask;
+  // received shards zero-padded to the slot (decoder.go:62-69); lost ones are never read
+  uint8_t* dd = sl.s->data + size_t(sl.g) * b->k * b->slot;
+  uint8_t* pd = sl.s->rparity + size_t(sl.g) * b->r * b->slot;
+  for (uint32_t j = 0; j < b->k + b->r; ++j) {
+    if (!shards[j]) continue;
+    uint8_t* d = j < b->k ? dd + size_t(j) * b->slot : pd + size_t(j - b->k) * b->slot;
+    std::memcpy(d, shards[j], len);
+    std::memset(d + len, 0, b->slot - len);
+  }
+  return commit(b, sl);
+}
+
 namespace {
 
 // Copies a published result out of the ring and claims it: 1 done, 0 not published yet,
-// negative code on failure.  *len = payload length.
-int take(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int* len) {
+// negative code on failure.  *len = payload length; *rows = rows copied (encoder: r;
+// decoder: the group's lost data shards); *mask = the group's erasure mask (decoder).
+int take(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int* len, uint32_t* rows,
+         uint64_t* mask) {
   Entry& e = b->ring[static_cast<size_t>(ticket) % b->ring.size()];
   if (e.ticket.load(std::memory_order_acquire) != ticket) return 0;
   const int rc = e.rc;
   const uint32_t n = e.len;
+  const uint64_t m = e.mask;
+  const uint32_t nrows = b->decoder ? static_cast<uint32_t>(__builtin_popcountll(m & ((1ull << b->k) - 1))) : b->r;
   bool stale = false;
   if (rc == FEC_OK && out) {
     if (out_stride < n) {
-      berr("fec_batcher_wait: out_stride %u < repair length %u", out_stride, n);
+      berr("fec_batcher_wait: out_stride %u < payload length %u", out_stride, n);
       return FEC_ERR_RANGE;
     }
     const uint8_t* src = b->parity + (static_cast<uint64_t>(ticket) % b->cap) * b->r * b->slot;
-    for (uint32_t i = 0; i < b->r; ++i) std::memcpy(out + size_t(i) * out_stride, src + size_t(i) * b->slot, n);
+    for (uint32_t i = 0; i < nrows; ++i) std::memcpy(out + size_t(i) * out_stride, src + size_t(i) * b->slot, n);
     std::atomic_thread_fence(std::memory_order_acquire);
-    // the slot is rewritten by the encode of ticket + C: launched already?
+    // the slot is rewritten by the batch of ticket + C: launched already?
     stale = b->launched_upto.load(std::memory_order_relaxed) > ticket + static_cast<int64_t>(b->cap);
   }
   int64_t expect = ticket;
   if (stale || !e.ticket.compare_exchange_strong(expect, -1, std::memory_order_acq_rel)) {
     berr("fec_batcher_wait: result of ticket %lld expired while it was read", static_cast<long long>(ticket));
     return FEC_ERR_RANGE;
+  }
+  if (mask) *mask = m;
+  if (rc == FEC_ERR_UNRECOVERABLE) {
+    berr("fec_batcher_wait: ticket %lld lost more shards than parity rows survive (mask 0x%llx)",
+         static_cast<long long>(ticket), static_cast<unsigned long long>(m));
+    return rc;
   }
   if (rc != FEC_OK) {
     std::lock_guard<std::mutex> lk(b->mu);
@@ -509,17 +640,15 @@ int take(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int* 
     return rc;
   }
   *len = static_cast<int>(n);
+  *rows = nrows;
   return 1;
 }
 
-}  // namespace
-
-QFEC_EXPORT int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int64_t timeout_us) {
-  if (!b) return FEC_ERR_NULL;
-  int len = 0;
-  int st = ticket >= 0 ? take(b, ticket, out, out_stride, &len) : 0;
-  if (st == 1) return len;
-  if (st < 0) return st;
+// fec_batcher_wait's body: 1 and the result, or FEC_ERR_AGAIN / another negative code.
+int wait_result(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int64_t timeout_us, int* len,
+                uint32_t* rows, uint64_t* mask) {
+  int st = ticket >= 0 ? take(b, ticket, out, out_stride, len, rows, mask) : 0;
+  if (st != 0) return st;
   // A poll of a ticket not published yet needs no lock.
   if (timeout_us == 0 && ticket >= 0 && ticket >= b->published_upto.load(std::memory_order_acquire))
     return FEC_ERR_AGAIN;
@@ -547,13 +676,39 @@ QFEC_EXPORT int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, ui
     }
   }
   lk.unlock();
-  st = take(b, ticket, out, out_stride, &len);
-  if (st == 1) return len;
+  st = take(b, ticket, out, out_stride, len, rows, mask);
   if (st == 0) {
     berr("fec_batcher_wait: ticket %lld was already collected", static_cast<long long>(ticket));
     return FEC_ERR_RANGE;
   }
   return st;
+}
+
+}  // namespace
+
+QFEC_EXPORT int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int64_t timeout_us) {
+  if (!b) return FEC_ERR_NULL;
+  if (b->decoder) {
+    berr("fec_batcher_wait: a decoder batcher's results are read with fec_batcher_wait_rebuilt");
+    return FEC_ERR_RANGE;
+  }
+  int len = 0;
+  uint32_t rows = 0;
+  const int st = wait_result(b, ticket, out, out_stride, timeout_us, &len, &rows, nullptr);
+  return st == 1 ? len : st;
+}
+
+QFEC_EXPORT int fec_batcher_wait_rebuilt(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride,
+                                         uint64_t* lost_mask, int64_t timeout_us) {
+  if (!b) return FEC_ERR_NULL;
+  if (!b->decoder) {
+    berr("fec_batcher_wait_rebuilt: an encoder batcher's results are read with fec_batcher_wait");
+    return FEC_ERR_RANGE;
+  }
+  int len = 0;
+  uint32_t rows = 0;
+  const int st = wait_result(b, ticket, out, out_stride, timeout_us, &len, &rows, lost_mask);
+  return st == 1 ? static_cast<int>(rows) : st;
 }
 
 QFEC_EXPORT int fec_batcher_flush(FECBatcher* b) {

@@ -13,6 +13,8 @@
 //   batcher_latency single <r> <calls>   (one group per synchronous call, no batcher)
 //   batcher_latency raw <streams> <seconds> <r> <deadline_us> <max_groups> [depth]
 //                                        (the C-ABI without the encoder API, and the copy cost)
+//   batcher_latency decode <streams> <seconds> <r> <deadline_us> <max_groups> [depth]
+//                                        (the decoder batcher at saturation, every packet checked)
 #include <sys/resource.h>
 
 #include <algorithm>
@@ -34,6 +36,8 @@
 extern "C" {
 void oracle_xor_avx2(const uint8_t* const*, size_t, size_t, uint8_t*);
 int oracle_rs_encode_fast(const uint8_t*, uint64_t, uint32_t, uint32_t, uint32_t, uint8_t*, int);
+int64_t oracle_rs_decode_fast(uint8_t*, const uint8_t*, const uint64_t*, uint64_t, uint32_t, uint32_t, uint32_t,
+                              uint8_t*, int);
 void oracle_fill_splitmix(uint8_t*, uint64_t, uint64_t, uint64_t);
 }
 
@@ -261,6 +265,95 @@ int raw(int S, double seconds, int r, int deadline_us, int max_groups, int depth
   return errors ? 1 : 0;
 }
 
+// The decoder batcher at saturation: every connection thread submits coded groups with
+// losses (r = 1: one data shard; else two of the k + r shards, as C3), keeps `depth`
+// outstanding, and checks every rebuilt packet against the original.
+int draw(int S, double seconds, int r, int deadline_us, int max_groups, int depth) {
+  FECBatcher* b = fec_batcher_new_decoder(-1, kK, r, kP, max_groups, deadline_us, 4);
+  if (!b) return 2;
+  constexpr int NG = 64;
+  Bytes data(size_t(NG) * kK * kP), par(size_t(NG) * r * kP);
+  oracle_fill_splitmix(data.data(), data.size(), 0x5EED0E, 0);
+  oracle_rs_encode_fast(data.data(), NG, kK, r, kP, par.data(), 1);
+  std::atomic<long> groups{0}, errors{0};
+  const auto t_end = Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(seconds));
+  const auto t0 = Clock::now();
+  const double c0 = cpu_seconds();
+  std::vector<std::thread> th;
+  for (int s = 0; s < S; ++s)
+    th.emplace_back([&, s] {
+      std::mt19937_64 rng(99 + s);
+      struct Out {
+        int64_t t;
+        int g;
+        uint64_t mask;
+      };
+      std::vector<Out> q;
+      size_t head = 0;
+      std::vector<uint8_t> rows(size_t(r) * kP);
+      long n = 0;
+      auto check = [&](const Out& o, int rc, uint64_t got_mask) {
+        int want = 0;
+        for (int j = 0; j < kK; ++j) {
+          if (!((o.mask >> j) & 1)) continue;
+          if (rc <= want || std::memcmp(rows.data() + size_t(want) * kP, data.data() + (size_t(o.g) * kK + j) * kP, kP))
+            ++errors;
+          ++want;
+        }
+        if (rc != want || got_mask != o.mask) ++errors;
+      };
+      while (Clock::now() < t_end) {
+        const int g = int(rng() % NG);
+        uint64_t mask;
+        if (r == 1) {
+          mask = 1ull << (rng() % kK);
+        } else {
+          const int a = int(rng() % (kK + r));
+          int c = int(rng() % (kK + r - 1));
+          if (c >= a) ++c;
+          mask = (1ull << a) | (1ull << c);
+        }
+        const uint8_t* shards[64];
+        for (int j = 0; j < kK + r; ++j)
+          shards[j] = (mask >> j) & 1 ? nullptr
+                      : j < kK    ? data.data() + (size_t(g) * kK + j) * kP
+                                  : par.data() + (size_t(g) * r + (j - kK)) * kP;
+        const int64_t t = fec_batcher_submit_shards(b, shards, kP);
+        if (t < 0) {
+          ++errors;
+          continue;
+        }
+        q.push_back(Out{t, g, mask});
+        while (head < q.size()) {
+          uint64_t m = 0;
+          const int rc = fec_batcher_wait_rebuilt(b, q[head].t, rows.data(), kP, &m, q.size() - head >= size_t(depth) ? -1 : 0);
+          if (rc == FEC_ERR_AGAIN) break;
+          check(q[head], rc, m);
+          ++head;
+          ++n;
+        }
+      }
+      fec_batcher_flush(b);
+      for (; head < q.size(); ++head, ++n) {
+        uint64_t m = 0;
+        check(q[head], fec_batcher_wait_rebuilt(b, q[head].t, rows.data(), kP, &m, -1), m);
+      }
+      groups += n;
+    });
+  for (auto& t : th) t.join();
+  const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
+  const double cpu = cpu_seconds() - c0;
+  FECBatcherStats st{};
+  fec_batcher_stats(b, &st);
+  fec_batcher_free(b);
+  std::printf("{\"mode\": \"decode_raw\", \"streams\": %d, \"r\": %d, \"deadline_us\": %d, \"max_groups\": %d, "
+              "\"depth\": %d, \"errors\": %ld, \"groups_per_s\": %.1f, \"cpu_us_per_group\": %.3f, \"mean_batch\": %.1f}\n",
+              S, r, deadline_us, max_groups, depth, errors.load(), groups / wall, cpu / groups * 1e6,
+              st.batches ? double(st.groups) / st.batches : 0.0);
+  std::fflush(stdout);
+  return errors ? 1 : 0;
+}
+
 // The one-group call of the reference's pattern without a batcher (HybridFECEncoder ->
 // fec_encode_batch, one launch and synchronize per group), for comparison.
 int single(int calls) {
@@ -308,9 +401,20 @@ int cpu() {
     }
   });
   const double rs3_us = time_it([&] { oracle_rs_encode_fast(data.data(), G, kK, 3, kP, rep.data(), 1); });
+  // receiver side: 2 of the 13 shards lost per group (C3), rebuilt in place
+  std::vector<uint64_t> masks(G);
+  std::mt19937_64 rng(7);
+  for (auto& m : masks) {
+    const int a = int(rng() % 13);
+    int b2 = int(rng() % 12);
+    if (b2 >= a) ++b2;
+    m = (1ull << a) | (1ull << b2);
+  }
+  const double dec3_us = time_it([&] { oracle_rs_decode_fast(data.data(), rep.data(), masks.data(), G, kK, 3, kP, nullptr, 1); });
   std::printf("{\"mode\": \"cpu_one_core\", \"us_per_group_avx2_xor_r1\": %.3f, \"us_per_group_gfni_r3\": %.3f, "
-              "\"groups_per_s_avx2_xor_r1\": %.0f, \"groups_per_s_gfni_r3\": %.0f}\n",
-              xor_us, rs3_us, 1e6 / xor_us, 1e6 / rs3_us);
+              "\"groups_per_s_avx2_xor_r1\": %.0f, \"groups_per_s_gfni_r3\": %.0f, \"us_per_group_gfni_decode_r3_2lost\": %.3f, "
+              "\"groups_per_s_gfni_decode_r3_2lost\": %.0f}\n",
+              xor_us, rs3_us, 1e6 / xor_us, 1e6 / rs3_us, dec3_us, 1e6 / dec3_us);
   return 0;
 }
 
@@ -323,6 +427,8 @@ int main(int argc, char** argv) {
   if (mode == "saturate")
     return saturate(int(arg(2, 16)), arg(3, 3), int(arg(4, 1)), int(arg(5, 1000)), int(arg(6, 4096)));
   if (mode == "single") return single(int(arg(2, 2000)));
+  if (mode == "decode")
+    return draw(int(arg(2, 16)), arg(3, 3), int(arg(4, 3)), int(arg(5, 1000)), int(arg(6, 4096)), int(arg(7, 1024)));
   if (mode == "raw")
     return raw(int(arg(2, 16)), arg(3, 3), int(arg(4, 1)), int(arg(5, 1000)), int(arg(6, 4096)), int(arg(7, 256)));
   return cpu();

@@ -30,6 +30,7 @@ FEC_ERR_RANGE = -3
 FEC_ERR_NODEV = -4
 FEC_ERR_NOMEM = -5
 FEC_ERR_AGAIN = -6
+FEC_ERR_UNRECOVERABLE = -7
 
 # Every function the headers declare (tests check the library exports all of them).
 REFERENCE_SYMBOLS = (
@@ -47,6 +48,7 @@ HIP_SYMBOLS = (
     "fec_group_encode_batch_rs", "fec_group_decode_batch_rs",
     "fec_batcher_new", "fec_batcher_free", "fec_batcher_submit", "fec_batcher_submit_packets",
     "fec_batcher_wait", "fec_batcher_flush", "fec_batcher_stats", "fec_batcher_last_error",
+    "fec_batcher_new_decoder", "fec_batcher_submit_shards", "fec_batcher_wait_rebuilt",
 )
 
 
@@ -128,6 +130,9 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
         "fec_batcher_flush": (_int, [_vp]),
         "fec_batcher_stats": (_int, [_vp, _vp]),
         "fec_batcher_last_error": (ctypes.c_char_p, []),
+        "fec_batcher_new_decoder": (_vp, [_int, _u32, _u32, _u32, _u32, _u32, _u32]),
+        "fec_batcher_submit_shards": (ctypes.c_int64, [_vp, ctypes.POINTER(_vp), _u32]),
+        "fec_batcher_wait_rebuilt": (_int, [_vp, ctypes.c_int64, _vp, _u32, _vp, ctypes.c_int64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -407,6 +412,53 @@ class Batcher:
 
     def __exit__(self, *exc):
         self.close()
+
+
+class DecodeBatcher(Batcher):
+    """A decoder FECBatcher: the groups of many connections recovered in one launch
+    (fec_batcher_new_decoder, include/fec_hip.h)."""
+
+    def __init__(self, k: int, r: int, slot_bytes: int = 1500, max_groups: int = 4096, deadline_us: int = 1000,
+                 device: int = -1, slabs: int = 3):
+        self.lib = load_library()
+        self.k, self.r, self.slot = k, r, slot_bytes
+        h = self.lib.fec_batcher_new_decoder(device, k, r, slot_bytes, max_groups, deadline_us, slabs)
+        if not h:
+            raise FecError("fec_batcher_new_decoder", FEC_ERR_NODEV, self.last_error())
+        self.handle = h
+        self._lens = {}
+
+    def submit(self, shards, length: int) -> int:
+        """k + r shards (data, then parity rows; None = lost), each at most `length` bytes."""
+        if len(shards) != self.k + self.r:
+            raise ValueError(f"expected {self.k + self.r} shards")
+        keep = [np.ascontiguousarray(x, dtype=np.uint8) if x is not None else None for x in shards]
+        for x in keep:
+            if x is not None and x.nbytes < length:
+                raise ValueError("shard shorter than the symbol length")
+        ptrs = (_vp * len(keep))(*[(x.ctypes.data if x is not None else None) for x in keep])
+        t = int(self.lib.fec_batcher_submit_shards(self.handle, ptrs, length))
+        if t < 0:
+            raise FecError("fec_batcher_submit_shards", t, self.last_error())
+        self._lens[t] = length
+        return t
+
+    def wait(self, ticket: int, timeout_us: int = -1):
+        """(lost data shard ids, their rebuilt bytes), or None when not ready in time; raises
+        FecError(FEC_ERR_UNRECOVERABLE) when too many shards were lost."""
+        out = np.zeros(self.r * self.slot, dtype=np.uint8)
+        mask = np.zeros(1, dtype=np.uint64)
+        n = int(self.lib.fec_batcher_wait_rebuilt(self.handle, ticket, out.ctypes.data, self.slot, mask.ctypes.data,
+                                                  timeout_us))
+        if n == FEC_ERR_AGAIN:
+            return None
+        length = getattr(self, "_lens", {}).pop(ticket, self.slot)
+        if n < 0:
+            raise FecError("fec_batcher_wait_rebuilt", n, self.last_error())
+        m = int(mask[0])
+        lost = [j for j in range(self.k) if (m >> j) & 1]
+        assert len(lost) == n
+        return lost, [out[i * self.slot:i * self.slot + length].copy() for i in range(n)]
 
 
 def _nbytes(a) -> int:

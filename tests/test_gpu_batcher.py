@@ -1,6 +1,7 @@
 """The shared batcher's C-ABI (fec_batcher_*, include/fec_hip.h) on the GPU: repair payloads
 equal the oracle's code rows for every group (row 0 = the reference XOR), both submit forms,
-timeouts, the result ring's expiry, errors, concurrent submitters."""
+timeouts, the result ring's expiry, errors, concurrent submitters; the decoder batcher
+rebuilds every lost data shard of every recoverable group exactly."""
 import threading
 
 import numpy as np
@@ -104,6 +105,73 @@ def test_batcher_concurrent_streams(quicfec_mod, oracle_mod):
             except Exception as e:   # noqa: BLE001 - reported below
                 errors.append(repr(e))
         th = [threading.Thread(target=stream, args=(s,)) for s in range(S)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        st = b.stats()
+    assert not errors, errors[:5]
+    assert st["groups"] == S * G and st["batches"] < S * G
+
+
+def _coded_group(oracle_mod, k, r, length, seed):
+    """k data shards of `length` bytes and their r parity rows (the oracle's code)."""
+    P = (length + 15) // 16 * 16
+    data = np.zeros(k * P, dtype=np.uint8)
+    for j in range(k):
+        data[j * P:j * P + length] = oracle_mod.splitmix_bytes(length, seed * 64 + j)
+    par = oracle_mod.rs_encode(data, 1, k, r, P)
+    shards = [data[j * P:j * P + length].copy() for j in range(k)] + [par[i * P:i * P + length].copy() for i in range(r)]
+    return shards
+
+
+@pytest.mark.parametrize("k,r", [(10, 1), (10, 3), (20, 5), (4, 2)])
+def test_decode_batcher_rebuilds_lost_shards(quicfec_mod, oracle_mod, k, r):
+    rng = np.random.default_rng(100 + k * 10 + r)
+    with quicfec_mod.DecodeBatcher(k, r, slot_bytes=1500, max_groups=16, deadline_us=2_000_000) as b:
+        cases = []
+        for g in range(60):
+            length = int(rng.integers(1, 1501))
+            shards = _coded_group(oracle_mod, k, r, length, 1000 * k + g)
+            lost = rng.choice(k + r, size=int(rng.integers(0, r + 2)), replace=False)   # up to r + 1 lost
+            sub = [None if s in lost else shards[s] for s in range(k + r)]
+            cases.append((shards, sorted(int(x) for x in lost), b.submit(sub, length)))
+        b.flush()
+        for shards, lost, t in cases:
+            if len(lost) > r:
+                with pytest.raises(quicfec_mod.FecError) as ei:
+                    b.wait(t)
+                assert ei.value.code == quicfec_mod.FEC_ERR_UNRECOVERABLE
+                continue
+            ids, rows = b.wait(t)
+            assert ids == [s for s in lost if s < k]
+            assert all(np.array_equal(row, shards[j]) for j, row in zip(ids, rows)), (lost, t)
+        assert b.stats()["groups"] == 60
+
+
+def test_decode_batcher_modes_and_threads(quicfec_mod, oracle_mod):
+    k, r, S, G = 10, 3, 6, 30
+    with quicfec_mod.Batcher(k, r, slot_bytes=1200, max_groups=8) as enc:
+        with pytest.raises(quicfec_mod.FecError):   # an encoder batcher has no rebuilt rows
+            quicfec_mod.DecodeBatcher.wait(enc, 0, timeout_us=0)
+    errors = []
+    with quicfec_mod.DecodeBatcher(k, r, slot_bytes=1200, max_groups=16, deadline_us=200) as b:
+        with pytest.raises(quicfec_mod.FecError):   # a decoder batcher takes shards
+            quicfec_mod.Batcher.submit(b, [np.zeros(10, dtype=np.uint8)])
+
+        def conn(s):
+            try:
+                rng = np.random.default_rng(s)
+                for g in range(G):
+                    shards = _coded_group(oracle_mod, k, r, 1200, 7000 + 100 * s + g)
+                    lost = set(int(x) for x in rng.choice(k + r, size=int(rng.integers(1, r + 1)), replace=False))
+                    ids, rows = b.wait(b.submit([None if j in lost else shards[j] for j in range(k + r)], 1200))
+                    if ids != sorted(j for j in lost if j < k) or not all(
+                            np.array_equal(row, shards[j]) for j, row in zip(ids, rows)):
+                        errors.append((s, g))
+            except Exception as e:   # noqa: BLE001 - reported below
+                errors.append(repr(e))
+        th = [threading.Thread(target=conn, args=(s,)) for s in range(S)]
         for t in th:
             t.start()
         for t in th:
