@@ -14,6 +14,7 @@
 #include <sys/syscall.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
@@ -259,6 +260,13 @@ uint64_t pipe_chunk_bytes() {
 // kCompactMaxShare of the batch; above that the whole batch streams through the pipeline.
 constexpr uint64_t kCompactMaxShare = 2;
 
+// A caller stream's decode workspace (stream_workspace).
+struct StreamWorkspace {
+  hipStream_t s = nullptr;
+  DevBuf buf;
+  uint64_t last_use = 0;
+};
+
 struct FECEncoderCtx {
   double redundancy = 0.10;
   uint32_t max_groups = 1024;
@@ -279,9 +287,16 @@ struct FECEncoderCtx {
   // fec_decode_loss_hint: expected share of groups with lost data in device-resident decode
   // calls (< 0: unknown, treated as dense).
   double decode_need_share = -1.0;
+  // per-stream record-offset workspaces of the device-resident decodes (stream_workspace)
+  std::vector<std::unique_ptr<StreamWorkspace>> stream_ws;
+  uint64_t ws_clock = 0;
 
   ~FECEncoderCtx() {
     DeviceGuard g(device);
+    if (!stream_ws.empty()) {  // caller streams may still run decodes that read them
+      (void)hipDeviceSynchronize();
+      stream_ws.clear();
+    }
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& p : pipe)
       if (p.s) (void)hipStreamSynchronize(p.s);
@@ -432,35 +447,49 @@ int encode_dev_locked(FECEncoderCtx* ctx, const uint8_t* d_data, const void* d_o
   return FEC_OK;
 }
 
-// Per-call record-offset workspace, ordered on the call's stream: allocated before the
-// launch and released behind it with the stream-ordered allocator, so decodes in flight on
-// different streams never share one (the context-wide buffer they used to share could be
-// overwritten by the next call's classify before the previous call's decode read it).
-struct StreamScratch {
-  void* ptr = nullptr;
-  hipStream_t s = nullptr;
-  bool async = false;
-  hipError_t alloc(size_t bytes, hipStream_t stream) {
-    s = stream;
-    hipError_t e = hipMallocAsync(&ptr, bytes, s);
-    if (e == hipSuccess) {
-      async = true;
-      return e;
+// Record-offset workspace of device-resident decodes, one buffer per caller stream: calls
+// on one stream run in stream order, so the next call on it may reuse the buffer while the
+// previous call's kernels are still queued; decodes in flight on different streams never
+// share one (the context-wide buffer they used to share could be overwritten by the next
+// call's classify before the previous call's decode read it).  A buffer grows only after
+// its stream has drained; the least recently used of kMaxStreamWorkspaces is dropped after
+// a device synchronize.  (A per-call stream-ordered allocation, hipMallocAsync/hipFreeAsync,
+// handed out memory that a queued decode on the same stream was still reading:
+// tools/batcher_latency.cpp decode mode, ~20% of k=10 r=2 groups wrong.)  Caller holds
+// ctx->mu.
+constexpr size_t kMaxStreamWorkspaces = 16;
+
+hipError_t stream_workspace(FECEncoderCtx* ctx, hipStream_t s, size_t bytes, void** out) {
+  StreamWorkspace* w = nullptr;
+  for (auto& e : ctx->stream_ws)
+    if (e->s == s) {
+      w = e.get();
+      break;
     }
-    (void)hipGetLastError();  // no memory pools: a plain allocation, released after a sync
-    ptr = nullptr;
-    return hipMalloc(&ptr, bytes);
-  }
-  ~StreamScratch() {
-    if (!ptr) return;
-    if (async) {
-      (void)hipFreeAsync(ptr, s);
-    } else {
-      (void)hipStreamSynchronize(s);
-      (void)hipFree(ptr);
+  if (!w) {
+    if (ctx->stream_ws.size() >= kMaxStreamWorkspaces) {
+      auto lru = std::min_element(ctx->stream_ws.begin(), ctx->stream_ws.end(),
+                                  [](const auto& x, const auto& y) { return x->last_use < y->last_use; });
+      const hipError_t e = hipDeviceSynchronize();  // its stream may be gone: drain everything
+      if (e != hipSuccess) return e;
+      ctx->stream_ws.erase(lru);
     }
+    ctx->stream_ws.push_back(std::make_unique<StreamWorkspace>());
+    w = ctx->stream_ws.back().get();
+    w->s = s;
   }
-};
+  w->last_use = ++ctx->ws_clock;
+  if (bytes > w->buf.cap) {
+    if (w->buf.ptr) {
+      const hipError_t e = hipStreamSynchronize(s);  // queued calls may still read the old one
+      if (e != hipSuccess) return e;
+    }
+    const hipError_t e = w->buf.ensure(bytes);
+    if (e != hipSuccess) return e;
+  }
+  *out = w->buf.ptr;
+  return hipSuccess;
+}
 
 int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
                       const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
@@ -517,14 +546,14 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   if (const char* v = std::getenv("QUICFEC_DECODE_SCAN")) a.scan = static_cast<uint32_t>(std::atoi(v));
   // Workspace: the caller's slot buffer (pipeline slots: private stream, calls serialised
   // by the context lock), else one private to this call.
-  StreamScratch scratch;
   if (!plan->dense || qfec::decode_needs_rec_off(a)) {
     if (rec) {
       QFEC_HIP(rec->ensure(G * sizeof(uint32_t)));
       a.rec_off = rec->as<uint32_t>();
     } else {
-      QFEC_HIP(scratch.alloc(G * sizeof(uint32_t), s));
-      a.rec_off = static_cast<uint32_t*>(scratch.ptr);
+      void* ws = nullptr;
+      QFEC_HIP(stream_workspace(ctx, s, G * sizeof(uint32_t), &ws));
+      a.rec_off = static_cast<uint32_t*>(ws);
     }
   }
   std::vector<uint8_t> book, st;

@@ -180,42 +180,55 @@ int saturate(int S, double seconds, int r, int deadline_us, int max_groups) {
 int raw(int S, double seconds, int r, int deadline_us, int max_groups, int depth) {
   FECBatcher* b = fec_batcher_new(-1, kK, r, kP, max_groups, deadline_us, 4);
   if (!b) return 2;
-  const auto pk = packets(kK, 0x5EED0C);
+  // 64 different groups, so a batch that read stale slab bytes would show in row 0
+  constexpr int NG = 64;
+  Bytes data(size_t(NG) * kK * kP), xr(size_t(NG) * kP);
+  oracle_fill_splitmix(data.data(), data.size(), 0x5EED0C, 0);
+  for (int g = 0; g < NG; ++g) {
+    const uint8_t* p[kK];
+    for (int j = 0; j < kK; ++j) p[j] = data.data() + (size_t(g) * kK + j) * kP;
+    oracle_xor_avx2(p, kK, kP, xr.data() + size_t(g) * kP);
+  }
   std::atomic<long> groups{0}, errors{0};
   const auto t_end = Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(seconds));
   const auto t0 = Clock::now();
   const double c0 = cpu_seconds();
   std::vector<std::thread> th;
   for (int s = 0; s < S; ++s)
-    th.emplace_back([&] {
+    th.emplace_back([&, s] {
+      std::mt19937_64 rng(5 + s);
       const uint8_t* ptrs[kK];
       uint32_t lens[kK];
-      for (int j = 0; j < kK; ++j) {
-        ptrs[j] = pk[j].data();
-        lens[j] = kP;
-      }
+      for (int j = 0; j < kK; ++j) lens[j] = kP;
       std::vector<uint8_t> rows(size_t(r) * kP);
-      std::vector<int64_t> q;
+      std::vector<std::pair<int64_t, int>> q;
       size_t head = 0;
       long n = 0;
+      auto check = [&](int rc, int g) {
+        if (rc != kP || std::memcmp(rows.data(), xr.data() + size_t(g) * kP, kP)) ++errors;
+      };
       while (Clock::now() < t_end) {
+        const int g = int(rng() % NG);
+        for (int j = 0; j < kK; ++j) ptrs[j] = data.data() + (size_t(g) * kK + j) * kP;
         const int64_t t = fec_batcher_submit_packets(b, ptrs, lens, kK);
         if (t < 0) {
           ++errors;
           continue;
         }
-        q.push_back(t);
+        q.emplace_back(t, g);
         while (head < q.size()) {
-          const int rc = fec_batcher_wait(b, q[head], rows.data(), kP, q.size() - head >= size_t(depth) ? -1 : 0);
+          const int rc = fec_batcher_wait(b, q[head].first, rows.data(), kP, q.size() - head >= size_t(depth) ? -1 : 0);
           if (rc == FEC_ERR_AGAIN) break;
-          if (rc < 0) ++errors;
+          check(rc, q[head].second);
           ++head;
           ++n;
         }
       }
       fec_batcher_flush(b);
-      for (; head < q.size(); ++head, ++n)
-        if (fec_batcher_wait(b, q[head], rows.data(), kP, -1) < 0) ++errors;
+      for (; head < q.size(); ++head, ++n) {
+        const int rc = fec_batcher_wait(b, q[head].first, rows.data(), kP, -1);
+        check(rc, q[head].second);
+      }
       groups += n;
     });
   for (auto& t : th) t.join();
@@ -252,7 +265,7 @@ int raw(int S, double seconds, int r, int deadline_us, int max_groups, int depth
         while (Clock::now() < e2)
           for (int g = 0; g < 256; ++g, ++n)
             for (int j = 0; j < kK; ++j)
-              std::memcpy(dst[i] + (size_t(n % 4096) * kK + j) * kP, pk[j].data(), kP);
+              std::memcpy(dst[i] + (size_t(n % 4096) * kK + j) * kP, data.data() + size_t(j) * kP, kP);
         copies += n;
       });
     for (auto& t : ct) t.join();
@@ -294,13 +307,32 @@ int draw(int S, double seconds, int r, int deadline_us, int max_groups, int dept
       long n = 0;
       auto check = [&](const Out& o, int rc, uint64_t got_mask) {
         int want = 0;
+        bool ok = true;
+        int first_bad = -1;
         for (int j = 0; j < kK; ++j) {
           if (!((o.mask >> j) & 1)) continue;
-          if (rc <= want || std::memcmp(rows.data() + size_t(want) * kP, data.data() + (size_t(o.g) * kK + j) * kP, kP))
-            ++errors;
+          if (rc > want) {
+            const uint8_t* a = rows.data() + size_t(want) * kP;
+            const uint8_t* e = data.data() + (size_t(o.g) * kK + j) * kP;
+            for (int i = 0; i < kP && first_bad < 0; ++i)
+              if (a[i] != e[i]) first_bad = want * 100000 + i;
+          }
+          if (rc <= want || first_bad >= 0) ok = false;
           ++want;
         }
-        if (rc != want || got_mask != o.mask) ++errors;
+        if (rc != want || got_mask != o.mask) ok = false;
+        if (!ok && ++errors <= 6) {
+          // what came back: zeros, another group's shard, or something else
+          int zeros = 1, other = -1;
+          for (int i = 0; i < kP; ++i) zeros &= rows[i] == 0;
+          for (int gg = 0; gg < NG && other < 0; ++gg)
+            for (int jj = 0; jj < kK; ++jj)
+              if (!std::memcmp(rows.data(), data.data() + (size_t(gg) * kK + jj) * kP, kP)) other = gg * 100 + jj;
+          std::fprintf(stderr, "decode error: stream %d ticket %lld group %d mask 0x%llx got rc %d mask 0x%llx, "
+                               "first bad (row*1e5+byte) %d, row all zero %d, row = shard (g*100+j) %d, row[0..3] %02x%02x%02x%02x\n",
+                       s, (long long)o.t, o.g, (unsigned long long)o.mask, rc, (unsigned long long)got_mask, first_bad, zeros,
+                       other, rows[0], rows[1], rows[2], rows[3]);
+        }
       };
       while (Clock::now() < t_end) {
         const int g = int(rng() % NG);
@@ -336,7 +368,8 @@ int draw(int S, double seconds, int r, int deadline_us, int max_groups, int dept
       fec_batcher_flush(b);
       for (; head < q.size(); ++head, ++n) {
         uint64_t m = 0;
-        check(q[head], fec_batcher_wait_rebuilt(b, q[head].t, rows.data(), kP, &m, -1), m);
+        const int rc = fec_batcher_wait_rebuilt(b, q[head].t, rows.data(), kP, &m, -1);  // before m is read
+        check(q[head], rc, m);
       }
       groups += n;
     });

@@ -705,3 +705,37 @@ def test_recover_scan_form(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, loss, P
     gpu_ctx.synchronize()
     assert np.array_equal(st.cpu().numpy(), st_exp)
     assert np.array_equal(out.cpu().numpy().reshape(G, r, P), exp)
+
+
+@pytest.mark.parametrize("k,r", [(10, 1), (10, 2), (12, 4)])
+def test_recover_back_to_back_on_one_stream(gpu_ctx, oracle_mod, torch_cuda, k, r):
+    """Record-addressed decodes (classify + per-call record offsets) queued back to back on
+    one stream with no synchronize in between, each with its own erasure pattern: every call
+    must read its own record offsets.  (A per-call stream-ordered allocation of that
+    workspace handed out memory a queued decode was still reading.)"""
+    torch = torch_cuda
+    G, P, calls = 1500, 1200, 12
+    data = oracle_mod.splitmix_bytes(G * k * P, SEED + 71 + k + r)
+    par = oracle_mod.rs_encode(data, G, k, r, P, nthreads=8)
+    dd, dp = _dev(torch, data), _dev(torch, par)
+    rng = np.random.default_rng(k + r)
+    runs = []
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        for c in range(calls):
+            masks = np.zeros(G, dtype=np.uint64)
+            for g in range(G):
+                for s in rng.permutation(k + r)[: rng.integers(1, r + 1)]:
+                    masks[g] |= np.uint64(1) << np.uint64(int(s))
+            dm = _dev(torch, masks.view(np.int64))
+            out = torch.zeros(G * r * P, dtype=torch.uint8, device="cuda")
+            gpu_ctx.recover_dev(dd, dp, dm, G, k, r, P, out, None, stream=stream.cuda_stream)
+            runs.append((masks, dm, out))
+    stream.synchronize()
+    d3 = data.reshape(G, k, P)
+    for masks, _, out in runs:
+        o3 = out.cpu().numpy().reshape(G, r, P)
+        for g in range(0, G, 7):
+            lost = [j for j in range(k) if (int(masks[g]) >> j) & 1]
+            for m, j in enumerate(lost):
+                assert np.array_equal(o3[g, m], d3[g, j]), (g, j)
