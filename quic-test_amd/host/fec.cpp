@@ -375,6 +375,18 @@ bool FECDecoder::recoverSingle(Group& g, uint64_t* id, Bytes* out) {
     }
   }
   if (!found) return false;
+  if (shared_ && shared_->r() == 1 && g.packetCount == shared_->k() && g.symbolLen <= shared_->slot()) {
+    // the same XOR, in a batch shared with other connections
+    std::vector<const uint8_t*> shards(static_cast<size_t>(g.packetCount) + 1, nullptr);
+    for (auto& kv : g.packets)
+      if (kv.first != *id && kv.first < static_cast<uint64_t>(g.packetCount)) shards[kv.first] = kv.second.data();
+    shards.back() = g.redundancy.data();
+    std::vector<std::pair<int, Bytes>> rebuilt;
+    const Error e = shared_->Recover(shards, static_cast<uint32_t>(g.symbolLen), &rebuilt);
+    if (!e.ok() || rebuilt.size() != 1 || rebuilt[0].first != static_cast<int>(*id)) return false;
+    *out = std::move(rebuilt[0].second);
+    return true;
+  }
   std::vector<const uint8_t*> srcs;
   srcs.push_back(g.redundancy.data());
   for (auto& kv : g.packets)
@@ -508,6 +520,52 @@ SharedFECBatcher::~SharedFECBatcher() {
 void SharedFECBatcher::Flush() { fec_batcher_flush(b_); }
 
 std::vector<uint64_t> SharedFECBatcher::Stats() {
+  FECBatcherStats st{};
+  fec_batcher_stats(b_, &st);
+  return {st.groups, st.batches, st.full_flushes, st.deadline_flushes, st.max_batch};
+}
+
+std::shared_ptr<SharedFECDecodeBatcher> SharedFECDecodeBatcher::New(int k, int r, int slotBytes, int maxGroups,
+                                                                     int deadlineUs, int device, int slabs) {
+  if (k < 1 || r < 1 || k + r > 64 || slotBytes < 1 || maxGroups < 1 || deadlineUs < 0 || slabs < 0) return nullptr;
+  std::shared_ptr<SharedFECDecodeBatcher> b(new SharedFECDecodeBatcher());
+  b->b_ = fec_batcher_new_decoder(device, static_cast<uint32_t>(k), static_cast<uint32_t>(r),
+                                  static_cast<uint32_t>(slotBytes), static_cast<uint32_t>(maxGroups),
+                                  static_cast<uint32_t>(deadlineUs), static_cast<uint32_t>(slabs));
+  if (!b->b_) return nullptr;
+  b->k_ = k;
+  b->r_ = r;
+  b->slot_ = slotBytes;
+  return b;
+}
+
+SharedFECDecodeBatcher::~SharedFECDecodeBatcher() {
+  if (b_) fec_batcher_free(b_);
+}
+
+Error SharedFECDecodeBatcher::Recover(const std::vector<const uint8_t*>& shards, uint32_t len,
+                                      std::vector<std::pair<int, Bytes>>* out) {
+  out->clear();
+  if (shards.size() != static_cast<size_t>(k_ + r_)) return errorf("expected %d shards, got %zu", k_ + r_, shards.size());
+  const int64_t t = fec_batcher_submit_shards(b_, shards.data(), len);
+  if (t < 0) return errorf("fec_batcher_submit_shards failed with code %lld: %s", static_cast<long long>(t),
+                           fec_batcher_last_error());
+  std::vector<uint8_t> rows(static_cast<size_t>(r_) * slot_);
+  uint64_t mask = 0;
+  const int n = fec_batcher_wait_rebuilt(b_, t, rows.data(), static_cast<uint32_t>(slot_), &mask, -1);
+  if (n < 0) return errorf("fec_batcher_wait_rebuilt failed with code %d: %s", n, fec_batcher_last_error());
+  int row = 0;
+  for (int j = 0; j < k_ && row < n; ++j)
+    if ((mask >> j) & 1) {
+      const uint8_t* src = rows.data() + static_cast<size_t>(row++) * slot_;
+      out->emplace_back(j, Bytes(src, src + len));
+    }
+  return Error{};
+}
+
+void SharedFECDecodeBatcher::Flush() { fec_batcher_flush(b_); }
+
+std::vector<uint64_t> SharedFECDecodeBatcher::Stats() {
   FECBatcherStats st{};
   fec_batcher_stats(b_, &st);
   return {st.groups, st.batches, st.full_flushes, st.deadline_flushes, st.max_batch};
@@ -751,6 +809,11 @@ bool FECDecoder::recoverRS(const std::vector<Group*>& gs, std::vector<std::vecto
     metrics_.RecoveryEvents++;
   }
   return true;
+}
+
+void FECDecoder::SetSharedBatcher(std::shared_ptr<SharedFECDecodeBatcher> batcher) {
+  std::lock_guard<std::mutex> lk(mu_);
+  shared_ = std::move(batcher);
 }
 
 void FECDecoder::SetDeferredRecovery(bool deferred) {

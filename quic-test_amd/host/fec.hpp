@@ -145,6 +145,8 @@ struct FECDecoderMetrics {
 };
 
 // decoder.go:24-343
+class SharedFECDecodeBatcher;
+
 class FECDecoder {
  public:
   static constexpr size_t kMaxActiveGroups = 4096;       // decoder.go:10
@@ -176,6 +178,9 @@ class FECDecoder {
   // call per (k, r) and returns the recovered packets keyed by group id.  Immediate mode
   // (the default) decodes such a group as soon as it is recoverable.
   void SetDeferredRecovery(bool deferred);
+  // New: single-loss rebuilds of groups of the batcher's k (row 0 only, r = 1 batchers) go
+  // through a batch shared with other connections' decoders; results are unchanged.
+  void SetSharedBatcher(std::shared_ptr<SharedFECDecodeBatcher> batcher);
   std::vector<std::pair<uint64_t, std::vector<Recovered>>> RecoverPending(Error* err = nullptr);
   size_t pending() {
     std::lock_guard<std::mutex> lk(mu_);
@@ -205,6 +210,7 @@ class FECDecoder {
   bool recoverRS(const std::vector<Group*>& gs, std::vector<std::vector<Recovered>>* lists);
   bool recoverSingle(Group& g, uint64_t* id, Bytes* out);
   void evictOldestGroup();
+  std::shared_ptr<SharedFECDecodeBatcher> shared_;
 
   std::map<uint64_t, Group> groups_;
   std::mutex mu_;
@@ -310,6 +316,34 @@ class SharedFECBatcher {
 
  private:
   SharedFECBatcher() = default;
+  FECBatcher* b_ = nullptr;
+  int k_ = 0, r_ = 0, slot_ = 0;
+};
+
+// One batch of recoveries for the receivers of every connection (fec_batcher_new_decoder):
+// the reference's FECDecoder rebuilds one group per call (decoder.go:255-287), a GPU launch
+// per group; FECDecoder::SetSharedBatcher routes those rebuilds through this instead.
+class SharedFECDecodeBatcher {
+ public:
+  // nullptr when the GPU library cannot be initialised or the shape is invalid (k + r <= 64).
+  static std::shared_ptr<SharedFECDecodeBatcher> New(int k, int r, int slotBytes = 1500, int maxGroups = 4096,
+                                                     int deadlineUs = 200, int device = -1, int slabs = 3);
+  ~SharedFECDecodeBatcher();
+  SharedFECDecodeBatcher(const SharedFECDecodeBatcher&) = delete;
+  SharedFECDecodeBatcher& operator=(const SharedFECDecodeBatcher&) = delete;
+  int k() const { return k_; }
+  int r() const { return r_; }
+  int slot() const { return slot_; }
+  // Rebuilds a group's lost data shards and waits for its batch (at most the deadline plus
+  // one launch).  shards: k data shards then r parity rows, nullptr = lost, each `len` bytes.
+  // out: (shard id, rebuilt bytes) in ascending shard order.
+  Error Recover(const std::vector<const uint8_t*>& shards, uint32_t len, std::vector<std::pair<int, Bytes>>* out);
+  void Flush();
+  // groups, batches, full_flushes, deadline_flushes, max_batch
+  std::vector<uint64_t> Stats();
+
+ private:
+  SharedFECDecodeBatcher() = default;
   FECBatcher* b_ = nullptr;
   int k_ = 0, r_ = 0, slot_ = 0;
 };

@@ -294,3 +294,97 @@ func (e *BatchedFECEncoder) GetMetrics() FECMetrics {
 	defer e.mu.Unlock()
 	return e.metrics
 }
+
+// SharedDecodeBatcher batches the receivers' recoveries across connections
+// (fec_batcher_new_decoder): FECDecoder.recoverSingle (decoder.go:255-287) rebuilds one
+// group per call; with this, every connection's single-loss rebuild of a k-packet group
+// shares a launch with the others', at most `deadline` plus one launch later.
+type SharedDecodeBatcher struct {
+	b       *C.FECBatcher
+	k, r    int
+	slot    int
+	closeMu sync.RWMutex
+}
+
+// NewSharedDecodeBatcher: groups of k data packets and r repair rows (k + r <= 64), symbols
+// of at most slotBytes.
+func NewSharedDecodeBatcher(k, r, slotBytes, maxGroups int, deadline time.Duration, device int) (*SharedDecodeBatcher, error) {
+	if k < 1 || r < 1 || k+r > 64 || slotBytes < 1 || maxGroups < 1 || deadline < 0 {
+		return nil, fmt.Errorf("unsupported decode batcher k=%d r=%d slot=%d maxGroups=%d", k, r, slotBytes, maxGroups)
+	}
+	runtime.LockOSThread() // the creation error is thread-local
+	defer runtime.UnlockOSThread()
+	b := C.fec_batcher_new_decoder(C.int(device), C.uint32_t(k), C.uint32_t(r), C.uint32_t(slotBytes),
+		C.uint32_t(maxGroups), C.uint32_t(deadline/time.Microsecond), 3)
+	if b == nil {
+		return nil, fmt.Errorf("no usable GPU decode batcher: %s", C.GoString(C.fec_batcher_last_error()))
+	}
+	s := &SharedDecodeBatcher{b: b, k: k, r: r, slot: slotBytes}
+	runtime.SetFinalizer(s, (*SharedDecodeBatcher).Close)
+	return s, nil
+}
+
+// Close frees the batcher; no decoder may use it afterwards.
+func (s *SharedDecodeBatcher) Close() error {
+	s.closeMu.Lock()
+	defer s.closeMu.Unlock()
+	if s.b != nil {
+		C.fec_batcher_free(s.b)
+		s.b = nil
+	}
+	return nil
+}
+
+// Recover rebuilds the lost data shards of one group and waits for its batch.  shards holds
+// the k data symbols then the r repair rows, nil for the lost ones, each symbolLen bytes
+// (zero-padded as decoder.go:62-69 does).  Returns the rebuilt symbols by packet index.
+func (s *SharedDecodeBatcher) Recover(shards [][]byte, symbolLen int) (map[int][]byte, error) {
+	if len(shards) != s.k+s.r {
+		return nil, fmt.Errorf("expected %d shards, got %d", s.k+s.r, len(shards))
+	}
+	if symbolLen < 1 || symbolLen > s.slot {
+		return nil, fmt.Errorf("symbol length %d outside 1..%d", symbolLen, s.slot)
+	}
+	// the shards are copied into C memory: cgo forbids passing Go pointers inside Go memory
+	buf := unsafe.Slice((*byte)(C.malloc(C.size_t(len(shards)*symbolLen))), len(shards)*symbolLen)
+	defer C.free(unsafe.Pointer(&buf[0]))
+	ptrs := unsafe.Slice((**C.uint8_t)(C.malloc(C.size_t(len(shards))*C.size_t(unsafe.Sizeof(uintptr(0))))), len(shards))
+	defer C.free(unsafe.Pointer(&ptrs[0]))
+	for j, sh := range shards {
+		ptrs[j] = nil
+		if sh != nil {
+			if len(sh) < symbolLen {
+				return nil, fmt.Errorf("shard %d shorter than the symbol length", j)
+			}
+			copy(buf[j*symbolLen:(j+1)*symbolLen], sh[:symbolLen])
+			ptrs[j] = (*C.uint8_t)(unsafe.Pointer(&buf[j*symbolLen]))
+		}
+	}
+	s.closeMu.RLock()
+	defer s.closeMu.RUnlock()
+	if s.b == nil {
+		return nil, fmt.Errorf("decode batcher closed")
+	}
+	runtime.LockOSThread()
+	defer runtime.UnlockOSThread()
+	t := C.fec_batcher_submit_shards(s.b, &ptrs[0], C.uint32_t(symbolLen))
+	if t < 0 {
+		return nil, fmt.Errorf("fec_batcher_submit_shards failed with code %d: %s", int64(t), C.GoString(C.fec_batcher_last_error()))
+	}
+	rows := make([]byte, s.r*s.slot)
+	var mask C.uint64_t
+	n := C.fec_batcher_wait_rebuilt(s.b, t, (*C.uint8_t)(unsafe.Pointer(&rows[0])), C.uint32_t(s.slot), &mask, -1)
+	runtime.KeepAlive(rows)
+	if n < 0 {
+		return nil, fmt.Errorf("fec_batcher_wait_rebuilt failed with code %d: %s", int(n), C.GoString(C.fec_batcher_last_error()))
+	}
+	out := make(map[int][]byte, int(n))
+	row := 0
+	for j := 0; j < s.k && row < int(n); j++ {
+		if uint64(mask)>>uint(j)&1 == 1 {
+			out[j] = append([]byte(nil), rows[row*s.slot:row*s.slot+symbolLen]...)
+			row++
+		}
+	}
+	return out, nil
+}

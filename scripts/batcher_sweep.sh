@@ -25,3 +25,8 @@ for s in 1 4 8 16; do
   run $T $B raw $s 2 1 1000 4096 1024
 done
 run $T $B raw 16 2 3 1000 4096 1024
+# the decoder batcher (receivers' recoveries shared across connections), every packet checked
+for s in 1 4 8 16; do
+  run $T $B decode $s 2 3 1000 4096 1024
+done
+run $T $B decode 16 2 1 1000 4096 1024

@@ -722,6 +722,55 @@ static void TestBatcherReservationStress() {
   }
 }
 
+// FECDecoder with a shared decode batcher: 8 connections' decoders rebuild their single
+// losses in shared launches, with exactly the packets and metrics of a plain FECDecoder
+// fed the same way.
+static void TestDecoderSharedBatcher() {
+  auto sb = SharedFECDecodeBatcher::New(10, 1, 1500, 64, 200);
+  CHECK(sb != nullptr);
+  if (!sb) return;
+  std::atomic<int> bad{0}, recovered{0};
+  std::vector<std::thread> th;
+  for (int c = 0; c < 8; ++c)
+    th.emplace_back([&, c] {
+      std::mt19937_64 rng(77 + c);
+      FECDecoder shared, plain;
+      shared.SetSharedBatcher(sb);
+      HybridFECEncoder e(0.10);
+      for (uint64_t gid = 0; gid < 40; ++gid) {
+        std::vector<Bytes> pk;
+        Bytes repair;
+        for (int i = 0; i < 10; ++i) {
+          pk.push_back(rnd(200 + rng() % 1000, 100000 * c + 16 * gid + i));
+          auto r = e.AddPacket(pk.back(), gid * 10 + i);
+          if (r.needsRedundancy) repair = r.redundancy;
+        }
+        const uint64_t lost = rng() % 10;
+        const bool repair_first = rng() % 2;
+        for (FECDecoder* d : {&shared, &plain}) {
+          if (repair_first) d->AddRedundancyPacket(repair);
+          for (uint64_t i = 0; i < 10; ++i)
+            if (i != lost) d->AddPacket(pk[i], i, gid);
+          if (!repair_first) d->AddRedundancyPacket(repair);
+        }
+        const Bytes a = shared.GetPacket(gid, lost), b = plain.GetPacket(gid, lost);
+        if (a.empty() || a != b) ++bad;
+        Bytes want = pk[lost];
+        want.resize(a.size(), 0);
+        if (a != want) ++bad;
+        ++recovered;
+      }
+      const auto ma = shared.GetMetrics(), mb = plain.GetMetrics();
+      if (ma.PacketsRecovered != mb.PacketsRecovered || ma.RecoveryEvents != mb.RecoveryEvents ||
+          ma.FailedRecoveries != mb.FailedRecoveries || ma.PacketsRecovered != 40)
+        ++bad;
+    });
+  for (auto& t : th) t.join();
+  CHECK(bad == 0 && recovered == 8 * 40);
+  auto st = sb->Stats();
+  CHECK(st[0] == 8 * 40 && st[1] < st[0]);  // fewer launches than rebuilds
+}
+
 int main() {
   TestContextErrorAcrossThreads();
   TestNewFECEncoder();
@@ -748,6 +797,7 @@ int main() {
   TestBatcherManyStreams();
   TestBatcherDeadline();
   TestBatcherReservationStress();
+  TestDecoderSharedBatcher();
   if (g_fail) {
     std::printf("FAILED %d of %d checks\n", g_fail, g_checks);
     return 1;
