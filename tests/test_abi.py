@@ -72,6 +72,19 @@ def test_null_arguments_need_no_gpu(quicfec_mod):
     assert lib.fec_group_size(None) == 0
     assert not lib.fec_group_context(None, 0)
     lib.fec_group_free(None)
+    # batchers: NULL handles and arguments are refused before anything touches a device
+    assert lib.fec_batcher_submit(None, None, None, 0) == quicfec_mod.FEC_ERR_NULL
+    assert lib.fec_batcher_submit_shards(None, None, 16) == quicfec_mod.FEC_ERR_NULL
+    assert lib.fec_batcher_wait(None, 0, None, 0, 0) == quicfec_mod.FEC_ERR_NULL
+    assert lib.fec_batcher_wait_rebuilt(None, 0, None, 0, None, 0) == quicfec_mod.FEC_ERR_NULL
+    assert lib.fec_batcher_flush(None) == quicfec_mod.FEC_ERR_NULL
+    assert lib.fec_batcher_stats(None, None) == quicfec_mod.FEC_ERR_NULL
+    lib.fec_batcher_free(None)
+    # unsupported shapes fail in the constructor, with a message, GPU or not
+    assert not lib.fec_batcher_new(-1, 200, 57, 1200, 16, 100, 2)
+    assert "unsupported" in lib.fec_batcher_last_error().decode()
+    assert not lib.fec_batcher_new_decoder(-1, 60, 5, 1200, 16, 100, 2)      # k + r > 64
+    assert "fec_batcher_new_decoder: unsupported" in lib.fec_batcher_last_error().decode()
 
 
 def test_no_gpu_context_is_null_not_abort(quicfec_mod):
@@ -85,6 +98,11 @@ def test_no_gpu_context_is_null_not_abort(quicfec_mod):
     assert not lib.fec_group_new(None, 0)
     with pytest.raises(quicfec_mod.FecError):
         quicfec_mod.DeviceGroup()
+    # the batchers fail loudly too: no CPU fallback
+    with pytest.raises(quicfec_mod.FecError):
+        quicfec_mod.Batcher(10, 3)
+    with pytest.raises(quicfec_mod.FecError):
+        quicfec_mod.DecodeBatcher(10, 3)
 
 
 def test_parity_matrix_matches_oracle_and_fixture(quicfec_mod, oracle_mod, golden_dir):
