@@ -370,8 +370,8 @@ FECBatcher* create(bool decoder, int device, uint32_t k, uint32_t r, uint32_t sl
   }
   const uint32_t nslabs = slabs < 2 ? 2 : slabs;
   // QUICFEC_BATCHER_BLOCKING_SYNC=1: the flusher sleeps in its completion waits instead of
-  // polling (frees a core; adds wake-up latency; A/B in profiles/r02_v5_batcher_latency.jsonl
-  // era runs showed no throughput gain, so polling stays the default)
+  // polling (frees a core, adds wake-up latency; no throughput gain measured,
+  // profiles/r02_ab_batcher_blocking_sync.txt, so polling stays the default)
   const char* bs = std::getenv("QUICFEC_BATCHER_BLOCKING_SYNC");
   const bool blocking = bs && bs[0] == '1';
   for (uint32_t i = 0; i < nslabs; ++i) {
