@@ -1478,8 +1478,10 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
 hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, bool dry = false) {
   const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
 #define QFEC_FUSED_D(KK, RR, NMM, NTT)                                                        \
-  if (direct && !a.compact_out && a.k == KK && a.r == RR && nm == NMM && nt == NTT)           \
-    return dry ? hipSuccess : run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true>(a, s);
+  if (direct && a.k == KK && a.r == RR && nm == NMM && nt == NTT)                             \
+    return dry ? hipSuccess                                                                   \
+           : a.compact_out ? run_decode_fused<KK, RR, kNtStore | kNtLoad | kCompactOut, NMM, NTT, true>(a, s) \
+                           : run_decode_fused<KK, RR, kNtStore | kNtLoad, NMM, NTT, true>(a, s);
   // k=10 r=3 (the BASELINE shape) also has the scan form, for sparse loss (DecodeLaunch::scan),
   // and the compact-output form (DecodeLaunch::compact_out)
 #define QFEC_FUSED_DS(KK, RR, NMM, NTT)                                                       \
@@ -1508,6 +1510,7 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, b
   QFEC_FUSED_R(10, 3, 1, 1)
   QFEC_FUSED_P(QFEC_FUSED_L, 20, 5)
   QFEC_FUSED_P(QFEC_FUSED_D, 10, 1)
+  QFEC_FUSED_P(QFEC_FUSED_D, 10, 2)
   QFEC_FUSED_P(QFEC_FUSED_D, 4, 2)
 #undef QFEC_FUSED_P
 #undef QFEC_FUSED_DS

@@ -115,7 +115,7 @@ def test_select_xor_impl_is_callable(quicfec_mod, oracle_mod):
 # ---------------- batch GF(2^8) API ----------------
 
 SHAPES = [(4, 2, 256), (10, 3, 1200), (20, 5, 1200), (10, 1, 1200), (7, 4, 48), (12, 9, 64),
-          (3, 1, 16), (10, 3, 100), (5, 3, 33), (1, 1, 7), (30, 20, 32)]
+          (3, 1, 16), (10, 3, 100), (5, 3, 33), (1, 1, 7), (30, 20, 32), (10, 2, 1200), (10, 2, 700)]
 
 
 @pytest.mark.parametrize("k,r,P", SHAPES)
@@ -642,7 +642,8 @@ def test_device_decode_scan_form(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, l
 
 
 RECOVER_SHAPES = [(10, 3, 1200), (10, 3, 700), (10, 3, 1400), (20, 5, 1200), (20, 5, 96), (4, 2, 256), (7, 4, 48),
-                  (12, 9, 64), (10, 1, 1200), (5, 3, 33), (3, 2, 7), (30, 20, 32), (10, 3, 2500)]
+                  (12, 9, 64), (10, 1, 1200), (5, 3, 33), (3, 2, 7), (30, 20, 32), (10, 3, 2500),
+                  (10, 2, 1200), (10, 2, 700), (10, 1, 1400), (4, 2, 1200)]
 
 
 @pytest.mark.parametrize("k,r,P", RECOVER_SHAPES)
@@ -707,7 +708,7 @@ def test_recover_scan_form(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, loss, P
     assert np.array_equal(out.cpu().numpy().reshape(G, r, P), exp)
 
 
-@pytest.mark.parametrize("k,r", [(10, 1), (10, 2), (12, 4)])
+@pytest.mark.parametrize("k,r", [(6, 3), (12, 4), (10, 2)])   # record-addressed, and one mask-addressed
 def test_recover_back_to_back_on_one_stream(gpu_ctx, oracle_mod, torch_cuda, k, r):
     """Record-addressed decodes (classify + per-call record offsets) queued back to back on
     one stream with no synchronize in between, each with its own erasure pattern: every call
