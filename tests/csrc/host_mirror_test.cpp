@@ -771,6 +771,67 @@ static void TestDecoderSharedBatcher() {
   CHECK(st[0] == 8 * 40 && st[1] < st[0]);  // fewer launches than rebuilds
 }
 
+// The product's FEC path end to end on both batchers: 12 client streams encode through one
+// shared encode batcher (BatchedFECEncoder, as HybridFECEncoder per stream), a channel
+// drops packets and repairs with p = 0.05 (the mobile profile), 12 server connections
+// decode with FECDecoders on one shared decode batcher.  Every group that lost exactly one
+// data packet and kept its repair is rebuilt byte for byte.  (As decoder.go does, a group
+// whose repair arrives first is also "recovered" when its last packet is merely late: every
+// group with its repair and at most one data loss is rebuilt once.)
+static void TestEndToEndBothBatchers() {
+  auto enc = SharedFECBatcher::New(10, 1, 1500, 256, 300);
+  auto dec = SharedFECDecodeBatcher::New(10, 1, 1500, 256, 300);
+  CHECK(enc != nullptr && dec != nullptr);
+  if (!enc || !dec) return;
+  std::atomic<int> bad{0}, expect{0}, rebuilt{0}, attempts{0};
+  std::vector<std::thread> th;
+  for (int c = 0; c < 12; ++c)
+    th.emplace_back([&, c] {
+      std::mt19937_64 rng(500 + c);
+      BatchedFECEncoder client(enc);
+      FECDecoder server;
+      server.SetSharedBatcher(dec);
+      int64_t mine = 0;  // this connection's rebuilds
+      for (uint64_t gid = 0; gid < 60; ++gid) {
+        std::vector<Bytes> pk;
+        Bytes repair;
+        for (int i = 0; i < 10; ++i) {
+          pk.push_back(rnd(300 + rng() % 1100, 7000000ull * c + 16 * gid + i));
+          AddPacketResult a = client.AddPacket(pk.back(), gid * 10 + i);
+          if (!a.err.ok()) ++bad;
+          if (a.needsRedundancy) repair = a.redundancy;
+        }
+        std::vector<bool> lost(11);
+        int nlost = 0;
+        for (int i = 0; i < 11; ++i) nlost += (lost[i] = (rng() % 1000) < 50);
+        if (!lost[10]) server.AddRedundancyPacket(repair);
+        for (uint64_t i = 0; i < 10; ++i)
+          if (!lost[i]) server.AddPacket(pk[i], i, gid);
+        int lost_data = nlost - (lost[10] ? 1 : 0);
+        if (lost_data <= 1 && !lost[10]) {
+          ++mine;
+          ++attempts;
+        }
+        if (lost_data == 1 && !lost[10]) {
+          ++expect;
+          for (uint64_t i = 0; i < 10; ++i)
+            if (lost[i]) {
+              const Bytes got = server.GetPacket(gid, i);
+              Bytes want = pk[i];
+              want.resize(got.size(), 0);
+              if (got.empty() || got != want) ++bad;
+              else ++rebuilt;
+            }
+        }
+      }
+      if (server.GetMetrics().PacketsRecovered != mine) ++bad;
+    });
+  for (auto& t : th) t.join();
+  CHECK(bad == 0 && rebuilt == expect && expect > 0);
+  CHECK(enc->Stats()[1] < enc->Stats()[0] && dec->Stats()[0] == uint64_t(attempts.load()));
+  CHECK(dec->Stats()[1] < dec->Stats()[0]);  // the connections' rebuilds shared launches
+}
+
 int main() {
   TestContextErrorAcrossThreads();
   TestNewFECEncoder();
@@ -798,6 +859,7 @@ int main() {
   TestBatcherDeadline();
   TestBatcherReservationStress();
   TestDecoderSharedBatcher();
+  TestEndToEndBothBatchers();
   if (g_fail) {
     std::printf("FAILED %d of %d checks\n", g_fail, g_checks);
     return 1;
