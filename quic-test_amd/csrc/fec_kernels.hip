@@ -1288,9 +1288,11 @@ hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
     if (tile > 0) {
       const uint32_t bs = (tile * cpp + 63) / 64 * 64;
       const uint32_t blocks = static_cast<uint32_t>((gn + tile - 1) / tile);
-      // Workgroups per CU: the compile-time-k kernels stream best at 2 (3 when r >= 4 rows of
-      // table arithmetic share each load); the runtime-k loop needs every wave it can get.
-      constexpr int kDefBlocks = K == 0 ? 0 : (R >= 4 ? kEncodeBlocksPerCU + 1 : kEncodeBlocksPerCU);
+      // Workgroups per CU: the compile-time-k kernels with few table rows stream best at 2;
+      // with r >= 4 rows of table arithmetic per load the kernel is VALU-bound and wants more
+      // waves: k=20 r=5 at 4 workgroups 5.22-5.40 ms, 3: 5.35-5.50, uncapped 5.22-5.59
+      // (profiles/r02_ab_encode_blocks_c4.txt, two boxes).  The runtime-k loop runs uncapped.
+      constexpr int kDefBlocks = K == 0 ? 0 : (R >= 4 ? kEncodeBlocksPerCU + 2 : kEncodeBlocksPerCU);
       const int blocks_per_cu = env_waves("QUICFEC_ENCODE_BLOCKS", kDefBlocks);
       const int waves = a.waves_per_cu ? a.waves_per_cu
                                        : env_waves("QUICFEC_ENCODE_WAVES", blocks_per_cu * static_cast<int>(bs / 64));
