@@ -1,0 +1,94 @@
+"""Randomised shapes through every entry point, against the oracle: k, r, packet size, group
+count, erasure patterns (up to r + 1 lost, so some groups are unrecoverable) and the API
+(host pageable, host page-locked, device in place, device recover) drawn from a seeded
+generator.  Each case is small, the whole sweep runs in seconds; it exists to catch the
+interaction bugs that the per-shape parity tests do not pin (form selection, workspace and
+staging reuse across calls of different shapes on one context)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED0F00
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _case(rng):
+    k = int(rng.integers(1, 21))
+    r = int(rng.integers(1, min(8, 64 - k) + 1))
+    P = int(rng.choice([int(rng.integers(1, 64)), int(rng.integers(64, 1600)), 1200, 256, 1024]))
+    G = int(rng.integers(1, 400))
+    api = str(rng.choice(["host", "pinned", "dev_inplace", "dev_recover"]))
+    return k, r, P, G, api
+
+
+def _masks(rng, G, k, r):
+    m = np.zeros(G, dtype=np.uint64)
+    for g in range(G):
+        for s in rng.permutation(k + r)[: int(rng.integers(0, r + 2))]:
+            m[g] |= np.uint64(1) << np.uint64(int(s))
+    return m
+
+
+@pytest.mark.parametrize("block", range(12))
+def test_random_shapes_all_apis(gpu_ctx, oracle_mod, torch_cuda, block):
+    torch = torch_cuda
+    rng = np.random.default_rng(SEED + block)
+    for _ in range(10):   # one context, shapes and APIs interleaved
+        k, r, P, G, api = _case(rng)
+        data = oracle_mod.splitmix_bytes(G * k * P, int(rng.integers(0, 1 << 30)))
+        par_exp = oracle_mod.rs_encode(data, G, k, r, P, nthreads=4)
+        masks = _masks(rng, G, k, r)
+        lost = ((masks[:, None] >> np.arange(k, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+        broken = data.copy().reshape(G, k, P)
+        broken[lost] = 0xEE
+        ref = broken.copy().reshape(-1)
+        bad_exp, st_exp = oracle_mod.rs_decode(ref, par_exp, masks, G, k, r, P, nthreads=4)
+        tag = (k, r, P, G, api)
+        if api in ("host", "pinned"):
+            if api == "pinned":
+                d = torch.from_numpy(data).pin_memory()
+                par = torch.zeros(G * r * P, dtype=torch.uint8).pin_memory()
+                gpu_ctx.encode(d, k, r, P, par, num_groups=G)
+                par_np = par.numpy()
+                dd = torch.from_numpy(broken.reshape(-1)).pin_memory()
+                st = torch.zeros(G, dtype=torch.uint8).pin_memory()
+                bad = gpu_ctx.decode(dd, par, torch.from_numpy(masks.view(np.int64)), k, r, P, st, num_groups=G)
+                got, st_np = dd.numpy(), st.numpy()
+            else:
+                par_np = np.zeros(G * r * P, dtype=np.uint8)
+                gpu_ctx.encode(data, k, r, P, par_np, num_groups=G)
+                got = broken.reshape(-1).copy()
+                st_np = np.zeros(G, dtype=np.uint8)
+                bad = gpu_ctx.decode(got, par_np, masks, k, r, P, st_np, num_groups=G)
+            assert np.array_equal(par_np, par_exp), tag
+            assert bad == bad_exp and np.array_equal(st_np, st_exp), tag
+            assert np.array_equal(got, ref), tag
+            continue
+        dd = torch.from_numpy(broken.reshape(-1)).cuda()
+        d_src = torch.from_numpy(data).cuda()
+        dp = torch.zeros(G * r * P, dtype=torch.uint8, device="cuda")
+        gpu_ctx.encode_dev(d_src, G, k, r, P, dp)
+        dm = torch.from_numpy(masks.view(np.int64)).cuda()
+        st = torch.full((G,), 7, dtype=torch.uint8, device="cuda")
+        if api == "dev_inplace":
+            gpu_ctx.decode_dev(dd, dp, dm, G, k, r, P, st)
+            gpu_ctx.synchronize()
+            assert np.array_equal(dd.cpu().numpy(), ref), tag
+        else:
+            out = torch.full((G * r * P,), 0x5A, dtype=torch.uint8, device="cuda")
+            gpu_ctx.recover_dev(dd, dp, dm, G, k, r, P, out, st)
+            gpu_ctx.synchronize()
+            o3 = out.cpu().numpy().reshape(G, r, P)
+            ref3 = ref.reshape(G, k, P)
+            for g in np.nonzero(st_exp == 0)[0]:
+                for m, j in enumerate(np.nonzero(lost[g])[0]):
+                    assert np.array_equal(o3[g, m], ref3[g, j]), tag + (int(g), int(j))
+        assert np.array_equal(dp.cpu().numpy(), par_exp), tag
+        assert np.array_equal(st.cpu().numpy(), st_exp), tag
