@@ -92,3 +92,59 @@ def test_random_shapes_all_apis(gpu_ctx, oracle_mod, torch_cuda, block):
                     assert np.array_equal(o3[g, m], ref3[g, j]), tag + (int(g), int(j))
         assert np.array_equal(dp.cpu().numpy(), par_exp), tag
         assert np.array_equal(st.cpu().numpy(), st_exp), tag
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_random_batchers(quicfec_mod, oracle_mod, block):
+    """Both batchers with random shapes, slab sizes, deadlines, packet counts and lengths,
+    and erasure patterns; results collected in random order (polls and blocking waits)."""
+    rng = np.random.default_rng(SEED + 100 + block)
+    for _ in range(3):
+        k = int(rng.integers(1, 17))
+        r = int(rng.integers(1, min(6, 64 - k) + 1))
+        slot = int(rng.integers(1, 1601))
+        mg = int(rng.integers(1, 40))
+        dl = int(rng.choice([0, 50, 500]))
+        slabs = int(rng.integers(2, 5))
+        # every result stays collectable while fewer than 2 * slabs * max_groups newer groups
+        # were encoded (include/fec_hip.h); the submissions stay within that
+        n = min(int(rng.integers(1, 90)), 2 * 3 * mg, 2 * slabs * mg)
+        with quicfec_mod.Batcher(k, r, slot_bytes=slot, max_groups=mg, deadline_us=dl, slabs=slabs) as b:
+            subs = []
+            for g in range(n):
+                cnt = int(rng.integers(1, k + 1))
+                pk = [oracle_mod.splitmix_bytes(int(rng.integers(1, slot + 1)), 99 * g + j + 7 * block) for j in range(cnt)]
+                subs.append((b.submit(pk), pk))
+            b.flush()
+            for i in rng.permutation(len(subs)):
+                t, pk = subs[i]
+                rows = b.wait(int(t), timeout_us=5_000_000)
+                L = max(len(p) for p in pk)
+                P = (L + 15) // 16 * 16
+                data = np.zeros(k * P, dtype=np.uint8)
+                for j, p in enumerate(pk):
+                    data[j * P:j * P + len(p)] = p
+                par = oracle_mod.rs_encode(data, 1, k, r, P)
+                assert all(np.array_equal(rows[m], par[m * P:m * P + L]) for m in range(r)), (k, r, slot, mg, dl)
+        with quicfec_mod.DecodeBatcher(k, r, slot_bytes=slot, max_groups=mg, deadline_us=dl) as db:
+            subs = []
+            for g in range(n):
+                L = int(rng.integers(1, slot + 1))
+                P = (L + 15) // 16 * 16
+                data = oracle_mod.splitmix_bytes(k * P, 1000 + g + 13 * block)
+                par = oracle_mod.rs_encode(data, 1, k, r, P)
+                shards = [data[j * P:j * P + L] for j in range(k)] + [par[m * P:m * P + L] for m in range(r)]
+                lost = set(int(x) for x in rng.permutation(k + r)[: int(rng.integers(0, r + 2))])
+                t = db.submit([None if s in lost else shards[s] for s in range(k + r)], L)
+                subs.append((t, shards, lost))
+            db.flush()
+            for i in rng.permutation(len(subs)):
+                t, shards, lost = subs[i]
+                if len(lost) > r:
+                    with pytest.raises(quicfec_mod.FecError) as ei:
+                        db.wait(int(t), timeout_us=5_000_000)
+                    assert ei.value.code == quicfec_mod.FEC_ERR_UNRECOVERABLE
+                    continue
+                ids, rows = db.wait(int(t), timeout_us=5_000_000)
+                assert ids == sorted(s for s in lost if s < k)
+                assert all(np.array_equal(row, shards[j]) for j, row in zip(ids, rows)), (k, r, slot, mg, dl)
