@@ -49,6 +49,14 @@ void run_point(const char* api, const char* mem, uint64_t G, uint32_t k, uint32_
 
 int main(int argc, char** argv) {
   const int calls = argc > 1 ? std::atoi(argv[1]) : 200;
+  // LATENCY_SCHED=spin|yield|blocking: the HIP runtime's wait mode, set before any context
+  // exists (the library leaves the process default, auto)
+  if (const char* m = std::getenv("LATENCY_SCHED")) {
+    const unsigned f = !std::strcmp(m, "spin") ? hipDeviceScheduleSpin
+                       : !std::strcmp(m, "yield") ? hipDeviceScheduleYield
+                                                  : hipDeviceScheduleBlockingSync;
+    if (hipSetDeviceFlags(f) != hipSuccess) std::fprintf(stderr, "hipSetDeviceFlags(%s) failed\n", m);
+  }
   if (fec_hip_device_count() <= 0) {
     std::fprintf(stderr, "no GPU\n");
     return 2;
