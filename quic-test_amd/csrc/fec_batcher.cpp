@@ -95,11 +95,14 @@ struct Slab {
 // ticket whose result it describes (r rows of `len` bytes in the ticket's parity slot).  A
 // reader copies, checks the slot was not rewritten meanwhile, and claims the result by
 // swapping in -1.
+// The fields are atomics (relaxed; `ticket` orders them) because a late reader may still load
+// them while the flusher rewrites the entry for ticket + C; its ticket re-check discards
+// what it read then.
 struct Entry {
   std::atomic<int64_t> ticket{-1};
-  int rc = FEC_OK;
-  uint32_t len = 0;
-  uint64_t mask = 0;  // decoder: the group's lost shards
+  std::atomic<int> rc{FEC_OK};
+  std::atomic<uint32_t> len{0};
+  std::atomic<uint64_t> mask{0};  // decoder: the group's lost shards
 };
 
 }  // namespace
@@ -240,10 +243,10 @@ struct FECBatcher {
       Entry& e = ring[static_cast<size_t>(ticket) % ring.size()];
       const int64_t prev = e.ticket.exchange(-1, std::memory_order_acq_rel);
       if (prev >= 0) ++dropped;  // never collected: dropped
-      e.rc = rc;
-      e.len = rc == FEC_OK ? m.max_len : 0;
-      e.mask = m.mask;
-      if (decoder && rc == FEC_OK && status[static_cast<uint64_t>(ticket) % cap] != 0) e.rc = FEC_ERR_UNRECOVERABLE;
+      const bool unrecoverable = decoder && rc == FEC_OK && status[static_cast<uint64_t>(ticket) % cap] != 0;
+      e.rc.store(unrecoverable ? FEC_ERR_UNRECOVERABLE : rc, std::memory_order_relaxed);
+      e.len.store(rc == FEC_OK ? m.max_len : 0, std::memory_order_relaxed);
+      e.mask.store(m.mask, std::memory_order_relaxed);
       e.ticket.store(ticket, std::memory_order_release);
     }
     std::lock_guard<std::mutex> lk(mu);
@@ -609,9 +612,9 @@ int take(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, int* 
          uint64_t* mask) {
   Entry& e = b->ring[static_cast<size_t>(ticket) % b->ring.size()];
   if (e.ticket.load(std::memory_order_acquire) != ticket) return 0;
-  const int rc = e.rc;
-  const uint32_t n = e.len;
-  const uint64_t m = e.mask;
+  const int rc = e.rc.load(std::memory_order_relaxed);
+  const uint32_t n = e.len.load(std::memory_order_relaxed);
+  const uint64_t m = e.mask.load(std::memory_order_relaxed);
   const uint32_t nrows = b->decoder ? static_cast<uint32_t>(__builtin_popcountll(m & ((1ull << b->k) - 1))) : b->r;
   bool stale = false;
   if (rc == FEC_OK && out) {
