@@ -575,13 +575,23 @@ BatchedFECEncoder::BatchedFECEncoder(std::shared_ptr<SharedFECBatcher> batcher) 
   packets_.reserve(b_ ? b_->k() : 10);
 }
 
+void BatchedFECEncoder::addLocked(const uint8_t* packet, size_t len) {
+  if (npk_ < packets_.size()) {
+    packets_[npk_].assign(packet, packet + len);  // reuses the buffer of an earlier group
+  } else {
+    packets_.emplace_back(packet, packet + len);
+  }
+  ++npk_;
+}
+
 Error BatchedFECEncoder::submitLocked(Ticket* t) {
   if (!b_) return errorf("GPU FEC engine unavailable");
-  if (packets_.empty()) return errorf("no packets in group");  // encoder_hybrid.go:84-86
+  if (npk_ == 0) return errorf("no packets in group");  // encoder_hybrid.go:84-86
   lens_.clear();
   ptrs_.clear();
   size_t maxSize = 0;
-  for (const auto& p : packets_) {
+  for (size_t i = 0; i < npk_; ++i) {
+    const Bytes& p = packets_[i];
     ptrs_.push_back(p.data());
     lens_.push_back(static_cast<uint32_t>(p.size()));
     maxSize = std::max(maxSize, p.size());
@@ -589,19 +599,19 @@ Error BatchedFECEncoder::submitLocked(Ticket* t) {
   // encoder_hybrid.go:95-97.  The reference keeps the packets after this error (every later
   // AddPacket of the stream then fails the same way); the group is dropped here instead.
   if (maxSize == 0) {
-    packets_.clear();
+    npk_ = 0;
     return errorf("empty packets");
   }
   const int64_t tk =
       fec_batcher_submit_packets(b_->raw(), ptrs_.data(), lens_.data(), static_cast<uint32_t>(lens_.size()));
   if (tk < 0) {  // refused (e.g. a packet wider than the slot): the group is dropped
-    packets_.clear();
+    npk_ = 0;
     return errorf("fec_batcher_submit failed with code %lld: %s", static_cast<long long>(tk), fec_batcher_last_error());
   }
   t->ticket = tk;
   t->groupID = groupID_++;
-  t->count = static_cast<int>(packets_.size());
-  packets_.clear();
+  t->count = static_cast<int>(npk_);
+  npk_ = 0;  // the buffers stay for the next group (their capacity is reused)
   return {};
 }
 
@@ -635,8 +645,8 @@ AddPacketResult BatchedFECEncoder::AddPacket(const uint8_t* packet, size_t len, 
   (void)packetID;
   std::lock_guard<std::mutex> lk(mu_);
   AddPacketResult res;
-  packets_.emplace_back(packet, packet + len);  // copied, as encoder_hybrid.go:64-65
-  if (static_cast<int>(packets_.size()) < (b_ ? b_->k() : 10)) return res;
+  addLocked(packet, len);  // copied, as encoder_hybrid.go:64-65
+  if (static_cast<int>(npk_) < (b_ ? b_->k() : 10)) return res;
   Ticket t;
   if ((res.err = submitLocked(&t))) return res;
   std::vector<Bytes> rows;
@@ -651,8 +661,8 @@ AddPacketResult BatchedFECEncoder::AddPacket(const uint8_t* packet, size_t len, 
 Error BatchedFECEncoder::AddPacketAsync(const uint8_t* packet, size_t len, uint64_t packetID) {
   (void)packetID;
   std::lock_guard<std::mutex> lk(mu_);
-  packets_.emplace_back(packet, packet + len);
-  if (static_cast<int>(packets_.size()) < (b_ ? b_->k() : 10)) return {};
+  addLocked(packet, len);
+  if (static_cast<int>(npk_) < (b_ ? b_->k() : 10)) return {};
   Ticket t;
   if (Error e = submitLocked(&t)) return e;
   outstanding_.push_back(t);
@@ -679,7 +689,7 @@ Error BatchedFECEncoder::Poll(std::vector<Bytes>* out, int64_t timeoutUs) {
 AddPacketResult BatchedFECEncoder::Flush() {
   std::lock_guard<std::mutex> lk(mu_);
   AddPacketResult res;
-  if (packets_.empty()) return res;
+  if (npk_ == 0) return res;
   Ticket t;
   if ((res.err = submitLocked(&t))) return res;
   b_->Flush();
@@ -694,7 +704,7 @@ AddPacketResult BatchedFECEncoder::Flush() {
 
 Error BatchedFECEncoder::FlushAsync() {
   std::lock_guard<std::mutex> lk(mu_);
-  if (!packets_.empty()) {
+  if (npk_ != 0) {
     Ticket t;
     if (Error e = submitLocked(&t)) return e;
     outstanding_.push_back(t);

@@ -384,7 +384,9 @@ class BatchedFECEncoder {
   Error collect(const Ticket& t, int64_t timeoutUs, std::vector<Bytes>* rows, bool* ready);
 
   std::shared_ptr<SharedFECBatcher> b_;
-  std::vector<Bytes> packets_;
+  void addLocked(const uint8_t* packet, size_t len);
+  std::vector<Bytes> packets_;  // packet buffers, kept across groups; the first npk_ are this group's
+  size_t npk_ = 0;
   uint64_t groupID_ = 0;
   std::deque<Ticket> outstanding_;
   Bytes rowbuf_;
