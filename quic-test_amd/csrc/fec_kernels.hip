@@ -1123,7 +1123,8 @@ __global__ __launch_bounds__(512) void decode_tiled(const uint8_t* __restrict__ 
   const Tab* tabs = reinterpret_cast<const Tab*>(recp + 128);
   const uint8_t* dg = data + g * K * static_cast<uint64_t>(P);
   const uint8_t* pg = parity + g * r * static_cast<uint64_t>(P);
-  uint8_t* og = out + g * K * static_cast<uint64_t>(P);
+  // in place: the erased shard's slot; kCompactOut: row m of the group's run (g*r + m)*P
+  uint8_t* og = out + g * ((POL & kCompactOut) != 0 ? r : K) * static_cast<uint64_t>(P);
   const size_t coff = col_off16(col, P);
   uint32_t sw[(K + 3) / 4];
 #pragma unroll
@@ -1151,7 +1152,9 @@ __global__ __launch_bounds__(512) void decode_tiled(const uint8_t* __restrict__ 
 #pragma unroll
   for (int m = 0; m < MAXE; ++m) {
     if (static_cast<uint32_t>(m) < e) {
-      const uint32_t eid = m < 4 ? (ew >> (8 * m)) & 0xFFu : rec_byte(rw, 64 + m);
+      const uint32_t eid = (POL & kCompactOut) != 0 ? static_cast<uint32_t>(m)
+                           : m < 4                     ? (ew >> (8 * m)) & 0xFFu
+                                                       : rec_byte(rw, 64 + m);
       st16<POL>(og + eid * static_cast<uint64_t>(P) + coff, acc[m]);
     }
   }
@@ -1465,8 +1468,9 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
 }
 
 // The fused form for this (k, r, P), if instantiated; hipErrorNotSupported otherwise.
-// Instantiated for every P in (256, 2048] of the compiled (k, r) shapes: NM 16-B and NT 4-B
-// pieces per lane.  r <= 3 shapes only in the mask-addressed form (the one auto uses for
+// Instantiated for every P in [16, 2048] of the compiled (k, r) shapes: NM 16-B and NT 4-B
+// pieces per lane (P <= 256: one 4-B piece; the in-place decode of such packets takes the
+// tiled form, the recover layout this one).  r <= 3 shapes only in the mask-addressed form (the one auto uses for
 // them), r > 3 only in the record-addressed one; k=10 r=3 1200 B in both (probes).
 // Measured at k=10 r=3, 2 erasures (tools/probe_decode.hip): 512 B 5.89 TB/s vs 3.12 for
 // the looped wave kernel, 768 B 5.49 vs 3.24 (profiles/r01_probe_decode_small.txt).  The
@@ -1506,7 +1510,7 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, b
            : a.compact_out ? run_decode_fused<KK, RR, kNtStore | kNtLoad | kLdsTabs | kCoefBytes | kCompactOut, NMM, NTT, false>(a, s) \
                            : run_decode_fused<KK, RR, kNtStore | kNtLoad | kLdsTabs | kCoefBytes, NMM, NTT, false>(a, s);
 #define QFEC_FUSED_P(M, KK, RR)                                                               \
-  M(KK, RR, 0, 2) M(KK, RR, 0, 3) M(KK, RR, 0, 4) M(KK, RR, 1, 0) M(KK, RR, 1, 1)            \
+  M(KK, RR, 0, 1) M(KK, RR, 0, 2) M(KK, RR, 0, 3) M(KK, RR, 0, 4) M(KK, RR, 1, 0) M(KK, RR, 1, 1) \
   M(KK, RR, 1, 2) M(KK, RR, 1, 3) M(KK, RR, 1, 4)
   QFEC_FUSED_P(QFEC_FUSED_DS, 10, 3)
   QFEC_FUSED_R(10, 3, 1, 1)
@@ -1538,18 +1542,27 @@ hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s)
     hipLaunchKernelGGL((decode_tiled<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(bs), 0, s,
                        a.data + g0 * a.k * static_cast<uint64_t>(a.P),
                        a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, cpp,
-                       a.P, a.r, tile, (a.out ? a.out : a.data) + g0 * a.k * static_cast<uint64_t>(a.P));
+                       a.P, a.r, tile,
+                       (a.out ? a.out : a.data) + g0 * ((POL & kCompactOut) != 0 ? a.r : a.k) * static_cast<uint64_t>(a.P));
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }
 
+// (k, r) shapes with a compiled tiled form (launch_decode's QFEC_TILED list)
+bool has_tiled(uint32_t k, uint32_t r) {
+  return (k == 10 && (r == 3 || r == 1)) || (k == 20 && r == 5) || (k == 4 && r == 2);
+}
+
 bool decode_tiled_form(const DecodeLaunch& a) {
-  if (a.compact_out) return false;  // in-place only; compact output runs the wave forms
+  // the compact recover layout only where a tiled form is compiled; elsewhere the fused or
+  // wave forms write it
+  if (a.compact_out && !has_tiled(a.k, a.r)) return false;
   const uint32_t tile = a.P >= kVecMinP ? pick_tile((a.P + 15u) / 16u, a.k, a.P) : 0u;
-  return tile > 0 && ((a.variant == kDecodeAuto && a.P <= kTiledMaxP) || a.variant == kDecodeTiledPlain ||
-                      a.variant == kDecodeTiledNt);
+  // auto leaves k=20 r=5 to the LDS-table fused form (P=200: 4.6 vs 2.8 TB/s, same box)
+  const bool auto_tiled = a.variant == kDecodeAuto && a.P <= kTiledMaxP && !(a.k == 20 && a.r == 5);
+  return tile > 0 && (auto_tiled || a.variant == kDecodeTiledPlain || a.variant == kDecodeTiledNt);
 }
 
 // Mask-addressed fused form (r <= 3): +1.2% at k=10 r=3 (tools/probe_decode.hip,
@@ -1571,7 +1584,7 @@ bool decode_compact_tables(const DecodeLaunch& a) {
   if (a.groups == 0 || a.P < kVecMinP || a.rec_ready || decode_tiled_form(a) || decode_direct_form(a)) return false;
   if (a.variant != kDecodeFused && a.variant != kDecodeAuto && a.variant != kDecodeFusedDirect) return false;
   const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
-  return a.k == 20 && a.r == 5 && ((nm == 0 && nt >= 2) || nm == 1);
+  return a.k == 20 && a.r == 5 && ((nm == 0 && nt >= 1) || nm == 1);  // QFEC_FUSED_P's (nm, nt)
 }
 
 hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
@@ -1603,6 +1616,16 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     return hipSuccess;
   }
   if (a.compact_out) {
+    // packets <= 256 B: the tiled form (several groups per wave), compact
+    if (tiled) {
+#define QFEC_TILED_C(KK, RR) \
+  if (a.k == KK && a.r == RR) return run_decode_tiled<KK, RR, kNtStore | kCompactOut>(a, tile, s);
+      QFEC_TILED_C(10, 3)
+      QFEC_TILED_C(10, 1)
+      QFEC_TILED_C(20, 5)
+      QFEC_TILED_C(4, 2)
+#undef QFEC_TILED_C
+    }
     // fused forms were tried above; everything else: the runtime-k wave kernel, compact
     if (a.variant == kDecodeFused || a.variant == kDecodeAuto || a.variant == kDecodeFusedDirect) {
       const hipError_t e = try_decode_fused(a, s, false);

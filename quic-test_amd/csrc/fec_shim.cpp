@@ -519,6 +519,8 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   a.r = r;
   a.P = P;
   a.rec_ready = !plan->dense;
+  // same-box A/B of the decode forms (tuning; the qfec::kDecode* numbers)
+  if (const char* v = std::getenv("QUICFEC_DECODE_VARIANT")) a.variant = std::atoi(v);
   if (plan->dense && qfec::decode_compact_tables(a)) {
     // the form reads bare coefficient bytes: the compact book of the same patterns
     if (!plan->cbook.ptr) {

@@ -643,7 +643,8 @@ def test_device_decode_scan_form(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, l
 
 RECOVER_SHAPES = [(10, 3, 1200), (10, 3, 700), (10, 3, 1400), (20, 5, 1200), (20, 5, 96), (4, 2, 256), (7, 4, 48),
                   (12, 9, 64), (10, 1, 1200), (5, 3, 33), (3, 2, 7), (30, 20, 32), (10, 3, 2500),
-                  (10, 2, 1200), (10, 2, 700), (10, 1, 1400), (4, 2, 1200)]
+                  (10, 2, 1200), (10, 2, 700), (10, 1, 1400), (4, 2, 1200),
+                  (10, 3, 256), (10, 3, 200), (10, 1, 128), (20, 5, 200), (4, 2, 100), (10, 3, 17), (10, 2, 256)]
 
 
 @pytest.mark.parametrize("k,r,P", RECOVER_SHAPES)
