@@ -225,6 +225,23 @@ int64_t fec_batcher_submit_shards(FECBatcher* b, const uint8_t* const* shards, u
 int fec_batcher_wait_rebuilt(FECBatcher* b, int64_t ticket, uint8_t* out, uint32_t out_stride, uint64_t* lost_mask,
                              int64_t timeout_us);
 
+/* Several GPUs behind one handle (SURVEY.md §8(e) for the host-resident path): one batcher
+ * per listed device (ordinals, repeats allowed; NULL / ndevices <= 0: every visible device),
+ * each with its own context, slabs, output ring and flusher thread.  A host-resident batch is
+ * bound by its GPU's PCIe link, so N devices give N links.  Groups are dealt round robin,
+ * passing over a device whose slabs are all busy while another has room; tickets stay unique
+ * (device i of n hands out its ticket t as t * n + i) and every fec_batcher_* call above takes
+ * the handle.  Stats sum over the devices (max_batch: the largest).  With one device this is
+ * fec_batcher_new / fec_batcher_new_decoder.  NULL on failure (fec_batcher_last_error names
+ * the device). */
+FECBatcher* fec_batcher_new_multi(const int* devices, int ndevices, uint32_t k, uint32_t r, uint32_t slot_bytes,
+                                  uint32_t max_groups, uint32_t deadline_us, uint32_t slabs);
+FECBatcher* fec_batcher_new_decoder_multi(const int* devices, int ndevices, uint32_t k, uint32_t r,
+                                          uint32_t slot_bytes, uint32_t max_groups, uint32_t deadline_us,
+                                          uint32_t slabs);
+/* Devices behind a batcher handle (1 for fec_batcher_new / _new_decoder). */
+int fec_batcher_devices(const FECBatcher* b);
+
 /* Closes the pending batch now (e.g. at the end of a stream) instead of at its deadline. */
 int fec_batcher_flush(FECBatcher* b);
 

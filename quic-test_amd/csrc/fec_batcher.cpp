@@ -37,6 +37,13 @@
 // received shards (NULL for the lost ones), the slab also holds the received parity rows and
 // the erasure masks, the batch runs fec_recover_batch_rs_dev, and the rebuilt data packets
 // land in the output ring (ticket t: r slots at t % C) next to a status byte per ticket.
+//
+// Several GPUs (fec_batcher_new_multi / fec_batcher_new_decoder_multi): one such batcher per
+// device, each with its own context, slabs, output ring and flusher, behind one handle.  A
+// host-resident batch is bound by its GPU's PCIe link (the kernels read the page-locked slab
+// over it), so N devices give N links.  Groups are dealt round robin (skipping a device whose
+// slabs are all busy while another has room); ticket t of device i of n is handed out as
+// t * n + i, so a wait goes straight to its device.
 #include <hip/hip_runtime.h>
 #include <sys/prctl.h>
 
@@ -134,8 +141,12 @@ struct FECBatcher {
   std::mutex mu;
   std::condition_variable cv_flusher, cv_done, cv_free;
   std::thread flusher;
+  // Multi-device handle: the per-device batchers (everything above is unused then).
+  std::vector<FECBatcher*> parts;
+  std::atomic<uint64_t> rr{0};
 
   ~FECBatcher() {
+    for (FECBatcher* p : parts) delete p;
     {
       std::lock_guard<std::mutex> lk(mu);
       stop = true;
@@ -453,6 +464,89 @@ QFEC_EXPORT FECBatcher* fec_batcher_new_decoder(int device, uint32_t k, uint32_t
   return create(true, device, k, r, slot_bytes, max_groups, deadline_us, slabs);
 }
 
+namespace {
+
+FECBatcher* create_multi(bool decoder, const int* devices, int ndevices, uint32_t k, uint32_t r, uint32_t slot_bytes,
+                         uint32_t max_groups, uint32_t deadline_us, uint32_t slabs) {
+  const char* fn = decoder ? "fec_batcher_new_decoder_multi" : "fec_batcher_new_multi";
+  std::vector<int> devs;
+  if (devices && ndevices > 0) {
+    devs.assign(devices, devices + ndevices);
+  } else {
+    const int n = fec_hip_device_count();
+    for (int i = 0; i < n; ++i) devs.push_back(i);
+  }
+  if (devs.empty()) {
+    berr("%s: no GPU visible", fn);
+    return nullptr;
+  }
+  if (devs.size() == 1) return create(decoder, devs[0], k, r, slot_bytes, max_groups, deadline_us, slabs);
+  auto* b = new FECBatcher();
+  b->decoder = decoder;
+  b->k = k;
+  b->r = r;
+  b->slot = slot_bytes;
+  b->max_groups = max_groups;
+  for (const int d : devs) {
+    FECBatcher* p = d < 0 ? nullptr : create(decoder, d, k, r, slot_bytes, max_groups, deadline_us, slabs);
+    if (!p) {
+      const std::string why = d < 0 ? "negative device ordinal" : g_batcher_error;
+      delete b;
+      berr("%s: device %d: %s", fn, d, why.c_str());
+      return nullptr;
+    }
+    b->parts.push_back(p);
+  }
+  return b;
+}
+
+// Multi-device routing: the part that owns `ticket` and the part's own ticket.
+FECBatcher* part_of(FECBatcher* b, int64_t ticket, int64_t* local) {
+  if (b->parts.empty()) {
+    *local = ticket;
+    return b;
+  }
+  const int64_t n = static_cast<int64_t>(b->parts.size());
+  *local = ticket < 0 ? ticket : ticket / n;
+  return b->parts[static_cast<size_t>(ticket < 0 ? 0 : ticket % n)];
+}
+
+// The part the next group goes to: round robin, passing over parts whose slabs are all
+// busy (their submitters would wait) while another part has an open slab.
+size_t pick_part(FECBatcher* b) {
+  const size_t n = b->parts.size();
+  const size_t first = static_cast<size_t>(b->rr.fetch_add(1, std::memory_order_relaxed) % n);
+  for (size_t i = 0; i < n; ++i) {
+    const size_t c = (first + i) % n;
+    if (b->parts[c]->open.load(std::memory_order_acquire) >= 0) return c;
+  }
+  return first;
+}
+
+// A part's ticket as the multi-device handle hands it out.
+int64_t global_ticket(const FECBatcher* b, size_t part, int64_t t) {
+  return t < 0 ? t : t * static_cast<int64_t>(b->parts.size()) + static_cast<int64_t>(part);
+}
+
+}  // namespace
+
+QFEC_EXPORT FECBatcher* fec_batcher_new_multi(const int* devices, int ndevices, uint32_t k, uint32_t r,
+                                              uint32_t slot_bytes, uint32_t max_groups, uint32_t deadline_us,
+                                              uint32_t slabs) {
+  return create_multi(false, devices, ndevices, k, r, slot_bytes, max_groups, deadline_us, slabs);
+}
+
+QFEC_EXPORT FECBatcher* fec_batcher_new_decoder_multi(const int* devices, int ndevices, uint32_t k, uint32_t r,
+                                                      uint32_t slot_bytes, uint32_t max_groups, uint32_t deadline_us,
+                                                      uint32_t slabs) {
+  return create_multi(true, devices, ndevices, k, r, slot_bytes, max_groups, deadline_us, slabs);
+}
+
+QFEC_EXPORT int fec_batcher_devices(const FECBatcher* b) {
+  if (!b) return FEC_ERR_NULL;
+  return b->parts.empty() ? 1 : static_cast<int>(b->parts.size());
+}
+
 QFEC_EXPORT void fec_batcher_free(FECBatcher* b) { delete b; }
 
 namespace {
@@ -558,6 +652,10 @@ int64_t submit_group(FECBatcher* b, Src&& src, const uint32_t* lens, uint32_t co
 
 QFEC_EXPORT int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, const uint32_t* lens, uint32_t count) {
   if (!b || !lens || (!packed && count > 0)) return FEC_ERR_NULL;
+  if (!b->parts.empty()) {
+    const size_t i = pick_part(b);
+    return global_ticket(b, i, fec_batcher_submit(b->parts[i], packed, lens, count));
+  }
   // packed back to back: prefix sums of the lengths
   uint64_t offs[256];
   uint64_t o = 0;
@@ -571,11 +669,19 @@ QFEC_EXPORT int64_t fec_batcher_submit(FECBatcher* b, const uint8_t* packed, con
 QFEC_EXPORT int64_t fec_batcher_submit_packets(FECBatcher* b, const uint8_t* const* packets, const uint32_t* lens,
                                                uint32_t count) {
   if (!b || !lens || (!packets && count > 0)) return FEC_ERR_NULL;
+  if (!b->parts.empty()) {
+    const size_t i = pick_part(b);
+    return global_ticket(b, i, fec_batcher_submit_packets(b->parts[i], packets, lens, count));
+  }
   return submit_group(b, [&](uint32_t j) { return packets[j]; }, lens, count);
 }
 
 QFEC_EXPORT int64_t fec_batcher_submit_shards(FECBatcher* b, const uint8_t* const* shards, uint32_t len) {
   if (!b || !shards) return FEC_ERR_NULL;
+  if (!b->parts.empty() && b->decoder) {
+    const size_t i = pick_part(b);
+    return global_ticket(b, i, fec_batcher_submit_shards(b->parts[i], shards, len));
+  }
   if (!b->decoder) {
     berr("fec_batcher_submit_shards: an encoder batcher takes fec_batcher_submit");
     return FEC_ERR_RANGE;
@@ -698,9 +804,11 @@ QFEC_EXPORT int fec_batcher_wait(FECBatcher* b, int64_t ticket, uint8_t* out, ui
     berr("fec_batcher_wait: a decoder batcher's results are read with fec_batcher_wait_rebuilt");
     return FEC_ERR_RANGE;
   }
+  int64_t local = 0;
+  b = part_of(b, ticket, &local);
   int len = 0;
   uint32_t rows = 0;
-  const int st = wait_result(b, ticket, out, out_stride, timeout_us, &len, &rows, nullptr);
+  const int st = wait_result(b, local, out, out_stride, timeout_us, &len, &rows, nullptr);
   return st == 1 ? len : st;
 }
 
@@ -711,14 +819,18 @@ QFEC_EXPORT int fec_batcher_wait_rebuilt(FECBatcher* b, int64_t ticket, uint8_t*
     berr("fec_batcher_wait_rebuilt: an encoder batcher's results are read with fec_batcher_wait");
     return FEC_ERR_RANGE;
   }
+  int64_t local = 0;
+  b = part_of(b, ticket, &local);
   int len = 0;
   uint32_t rows = 0;
-  const int st = wait_result(b, ticket, out, out_stride, timeout_us, &len, &rows, lost_mask);
+  const int st = wait_result(b, local, out, out_stride, timeout_us, &len, &rows, lost_mask);
   return st == 1 ? static_cast<int>(rows) : st;
 }
 
 QFEC_EXPORT int fec_batcher_flush(FECBatcher* b) {
   if (!b) return FEC_ERR_NULL;
+  for (FECBatcher* p : b->parts) fec_batcher_flush(p);
+  if (!b->parts.empty()) return FEC_OK;
   {
     std::lock_guard<std::mutex> lk(b->mu);
     b->close_open(false);
@@ -729,6 +841,21 @@ QFEC_EXPORT int fec_batcher_flush(FECBatcher* b) {
 
 QFEC_EXPORT int fec_batcher_stats(FECBatcher* b, FECBatcherStats* out) {
   if (!b || !out) return FEC_ERR_NULL;
+  if (!b->parts.empty()) {  // sums over the devices (max_batch: the largest)
+    FECBatcherStats sum{};
+    for (FECBatcher* p : b->parts) {
+      FECBatcherStats st{};
+      fec_batcher_stats(p, &st);
+      sum.groups += st.groups;
+      sum.batches += st.batches;
+      sum.full_flushes += st.full_flushes;
+      sum.deadline_flushes += st.deadline_flushes;
+      sum.max_batch = std::max(sum.max_batch, st.max_batch);
+      sum.expired += st.expired;
+    }
+    *out = sum;
+    return FEC_OK;
+  }
   std::lock_guard<std::mutex> lk(b->mu);
   *out = b->stats;
   return FEC_OK;

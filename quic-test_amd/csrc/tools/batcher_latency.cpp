@@ -174,11 +174,33 @@ int saturate(int S, double seconds, int r, int deadline_us, int max_groups) {
   return errors ? 1 : 0;
 }
 
+// QUICFEC_BATCHER_DEVICES="0,1,..." (raw / decode modes): one batcher per listed device behind
+// one handle (fec_batcher_new_multi); unset: fec_batcher_new on the current device.
+std::vector<int> env_devices() {
+  std::vector<int> d;
+  const char* e = std::getenv("QUICFEC_BATCHER_DEVICES");
+  for (const char* p = e; p && *p;) {
+    d.push_back(std::atoi(p));
+    p = std::strchr(p, ',');
+    if (p) ++p;
+  }
+  return d;
+}
+
+FECBatcher* new_batcher(bool decoder, int r, int max_groups, int deadline_us) {
+  const std::vector<int> d = env_devices();
+  if (d.empty())
+    return decoder ? fec_batcher_new_decoder(-1, kK, r, kP, max_groups, deadline_us, 4)
+                   : fec_batcher_new(-1, kK, r, kP, max_groups, deadline_us, 4);
+  return decoder ? fec_batcher_new_decoder_multi(d.data(), int(d.size()), kK, r, kP, max_groups, deadline_us, 4)
+                 : fec_batcher_new_multi(d.data(), int(d.size()), kK, r, kP, max_groups, deadline_us, 4);
+}
+
 // The C-ABI alone (no BatchedFECEncoder): submit by packet pointers, keep up to 256 groups
 // outstanding per stream, collect the oldest (payloads copied out).  And the cost of the
 // submit's copy alone: 12 KB memcpy per group into page-locked or pageable memory.
 int raw(int S, double seconds, int r, int deadline_us, int max_groups, int depth) {
-  FECBatcher* b = fec_batcher_new(-1, kK, r, kP, max_groups, deadline_us, 4);
+  FECBatcher* b = new_batcher(false, r, max_groups, deadline_us);
   if (!b) return 2;
   // 64 different groups, so a batch that read stale slab bytes would show in row 0
   constexpr int NG = 64;
@@ -236,12 +258,14 @@ int raw(int S, double seconds, int r, int deadline_us, int max_groups, int depth
   const double cpu = cpu_seconds() - c0;
   FECBatcherStats st{};
   fec_batcher_stats(b, &st);
+  const int ndev = fec_batcher_devices(b);
   fec_batcher_free(b);
-  std::printf("{\"mode\": \"raw\", \"streams\": %d, \"r\": %d, \"deadline_us\": %d, \"max_groups\": %d, \"errors\": %ld, "
+  std::printf("{\"mode\": \"raw\", \"devices\": %d, \"streams\": %d, \"r\": %d, \"deadline_us\": %d, \"max_groups\": %d, \"errors\": %ld, "
               "\"depth\": %d, \"groups_per_s\": %.1f, \"cpu_us_per_group\": %.3f, \"mean_batch\": %.1f}\n",
-              S, r, deadline_us, max_groups, errors.load(), depth, groups / wall, cpu / groups * 1e6,
+              ndev, S, r, deadline_us, max_groups, errors.load(), depth, groups / wall, cpu / groups * 1e6,
               st.batches ? double(st.groups) / st.batches : 0.0);
   std::fflush(stdout);
+  if (std::getenv("QUICFEC_SKIP_COPY")) return errors ? 1 : 0;
   // the submit's copy alone
   for (int pinned = 0; pinned < 2; ++pinned) {
     const size_t region = size_t(4096) * kK * kP;
@@ -282,7 +306,7 @@ int raw(int S, double seconds, int r, int deadline_us, int max_groups, int depth
 // losses (r = 1: one data shard; else two of the k + r shards, as C3), keeps `depth`
 // outstanding, and checks every rebuilt packet against the original.
 int draw(int S, double seconds, int r, int deadline_us, int max_groups, int depth) {
-  FECBatcher* b = fec_batcher_new_decoder(-1, kK, r, kP, max_groups, deadline_us, 4);
+  FECBatcher* b = new_batcher(true, r, max_groups, deadline_us);
   if (!b) return 2;
   constexpr int NG = 64;
   Bytes data(size_t(NG) * kK * kP), par(size_t(NG) * r * kP);
@@ -378,10 +402,11 @@ int draw(int S, double seconds, int r, int deadline_us, int max_groups, int dept
   const double cpu = cpu_seconds() - c0;
   FECBatcherStats st{};
   fec_batcher_stats(b, &st);
+  const int ndev = fec_batcher_devices(b);
   fec_batcher_free(b);
-  std::printf("{\"mode\": \"decode_raw\", \"streams\": %d, \"r\": %d, \"deadline_us\": %d, \"max_groups\": %d, "
+  std::printf("{\"mode\": \"decode_raw\", \"devices\": %d, \"streams\": %d, \"r\": %d, \"deadline_us\": %d, \"max_groups\": %d, "
               "\"depth\": %d, \"errors\": %ld, \"groups_per_s\": %.1f, \"cpu_us_per_group\": %.3f, \"mean_batch\": %.1f}\n",
-              S, r, deadline_us, max_groups, depth, errors.load(), groups / wall, cpu / groups * 1e6,
+              ndev, S, r, deadline_us, max_groups, depth, errors.load(), groups / wall, cpu / groups * 1e6,
               st.batches ? double(st.groups) / st.batches : 0.0);
   std::fflush(stdout);
   return errors ? 1 : 0;

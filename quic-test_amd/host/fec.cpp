@@ -513,6 +513,23 @@ std::shared_ptr<SharedFECBatcher> SharedFECBatcher::New(int k, int r, int slotBy
   return b;
 }
 
+std::shared_ptr<SharedFECBatcher> SharedFECBatcher::NewMulti(const std::vector<int>& devices, int k, int r,
+                                                              int slotBytes, int maxGroups, int deadlineUs, int slabs) {
+  if (k < 1 || r < 1 || k + r > 256 || k > FECDecoder::kMaxPacketCount || slotBytes < 1 || maxGroups < 1 ||
+      deadlineUs < 0 || slabs < 0)
+    return nullptr;
+  std::shared_ptr<SharedFECBatcher> b(new SharedFECBatcher());
+  b->b_ = fec_batcher_new_multi(devices.empty() ? nullptr : devices.data(), static_cast<int>(devices.size()),
+                                static_cast<uint32_t>(k), static_cast<uint32_t>(r), static_cast<uint32_t>(slotBytes),
+                                static_cast<uint32_t>(maxGroups), static_cast<uint32_t>(deadlineUs),
+                                static_cast<uint32_t>(slabs));
+  if (!b->b_) return nullptr;
+  b->k_ = k;
+  b->r_ = r;
+  b->slot_ = slotBytes;
+  return b;
+}
+
 SharedFECBatcher::~SharedFECBatcher() {
   if (b_) fec_batcher_free(b_);
 }
@@ -532,6 +549,22 @@ std::shared_ptr<SharedFECDecodeBatcher> SharedFECDecodeBatcher::New(int k, int r
   b->b_ = fec_batcher_new_decoder(device, static_cast<uint32_t>(k), static_cast<uint32_t>(r),
                                   static_cast<uint32_t>(slotBytes), static_cast<uint32_t>(maxGroups),
                                   static_cast<uint32_t>(deadlineUs), static_cast<uint32_t>(slabs));
+  if (!b->b_) return nullptr;
+  b->k_ = k;
+  b->r_ = r;
+  b->slot_ = slotBytes;
+  return b;
+}
+
+std::shared_ptr<SharedFECDecodeBatcher> SharedFECDecodeBatcher::NewMulti(const std::vector<int>& devices, int k, int r,
+                                                                          int slotBytes, int maxGroups, int deadlineUs,
+                                                                          int slabs) {
+  if (k < 1 || r < 1 || k + r > 64 || slotBytes < 1 || maxGroups < 1 || deadlineUs < 0 || slabs < 0) return nullptr;
+  std::shared_ptr<SharedFECDecodeBatcher> b(new SharedFECDecodeBatcher());
+  b->b_ = fec_batcher_new_decoder_multi(devices.empty() ? nullptr : devices.data(), static_cast<int>(devices.size()),
+                                        static_cast<uint32_t>(k), static_cast<uint32_t>(r),
+                                        static_cast<uint32_t>(slotBytes), static_cast<uint32_t>(maxGroups),
+                                        static_cast<uint32_t>(deadlineUs), static_cast<uint32_t>(slabs));
   if (!b->b_) return nullptr;
   b->k_ = k;
   b->r_ = r;

@@ -303,6 +303,11 @@ class SharedFECBatcher {
   // nullptr when the GPU library cannot be initialised or the shape is invalid.
   static std::shared_ptr<SharedFECBatcher> New(int k, int r, int slotBytes = 1500, int maxGroups = 4096,
                                                int deadlineUs = 1000, int device = -1, int slabs = 3);
+  // One batcher per listed GPU behind this handle (fec_batcher_new_multi; repeats allowed, empty
+  // = every visible GPU): host-resident batches are bound by their GPU's PCIe link.
+  static std::shared_ptr<SharedFECBatcher> NewMulti(const std::vector<int>& devices, int k, int r,
+                                                    int slotBytes = 1500, int maxGroups = 4096, int deadlineUs = 1000,
+                                                    int slabs = 3);
   ~SharedFECBatcher();
   SharedFECBatcher(const SharedFECBatcher&) = delete;
   SharedFECBatcher& operator=(const SharedFECBatcher&) = delete;
@@ -328,6 +333,10 @@ class SharedFECDecodeBatcher {
   // nullptr when the GPU library cannot be initialised or the shape is invalid (k + r <= 64).
   static std::shared_ptr<SharedFECDecodeBatcher> New(int k, int r, int slotBytes = 1500, int maxGroups = 4096,
                                                      int deadlineUs = 200, int device = -1, int slabs = 3);
+  // One decoder batcher per listed GPU behind this handle (fec_batcher_new_decoder_multi).
+  static std::shared_ptr<SharedFECDecodeBatcher> NewMulti(const std::vector<int>& devices, int k, int r,
+                                                          int slotBytes = 1500, int maxGroups = 4096,
+                                                          int deadlineUs = 200, int slabs = 3);
   ~SharedFECDecodeBatcher();
   SharedFECDecodeBatcher(const SharedFECDecodeBatcher&) = delete;
   SharedFECDecodeBatcher& operator=(const SharedFECDecodeBatcher&) = delete;

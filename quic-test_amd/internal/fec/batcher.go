@@ -61,6 +61,41 @@ func NewSharedBatcher(k, r, slotBytes, maxGroups int, deadline time.Duration, de
 	return s, nil
 }
 
+// devicesArg passes a device list to the *_multi constructors (nil or empty: every visible
+// GPU).  The C side copies the list during the call.
+func devicesArg(devices []int) (*C.int, C.int, func()) {
+	if len(devices) == 0 {
+		return nil, 0, func() {}
+	}
+	p := (*C.int)(C.malloc(C.size_t(len(devices)) * C.size_t(unsafe.Sizeof(C.int(0)))))
+	arr := unsafe.Slice(p, len(devices))
+	for i, d := range devices {
+		arr[i] = C.int(d)
+	}
+	return p, C.int(len(devices)), func() { C.free(unsafe.Pointer(p)) }
+}
+
+// NewSharedBatcherMulti: one batcher per listed GPU behind one handle (fec_batcher_new_multi;
+// repeats allowed, nil = every visible GPU).  Host-resident batches are bound by their GPU's
+// PCIe link, so N GPUs give N links; groups are dealt round robin and tickets stay unique.
+func NewSharedBatcherMulti(k, r, slotBytes, maxGroups int, deadline time.Duration, devices []int) (*SharedBatcher, error) {
+	if k < 1 || r < 1 || k+r > 256 || k > maxPacketCount || slotBytes < 1 || maxGroups < 1 || deadline < 0 {
+		return nil, fmt.Errorf("unsupported batcher k=%d r=%d slot=%d maxGroups=%d", k, r, slotBytes, maxGroups)
+	}
+	runtime.LockOSThread() // the creation error is thread-local
+	defer runtime.UnlockOSThread()
+	dp, dn, free := devicesArg(devices)
+	defer free()
+	b := C.fec_batcher_new_multi(dp, dn, C.uint32_t(k), C.uint32_t(r), C.uint32_t(slotBytes), C.uint32_t(maxGroups),
+		C.uint32_t(deadline/time.Microsecond), 3)
+	if b == nil {
+		return nil, fmt.Errorf("no usable GPU batcher: %s", C.GoString(C.fec_batcher_last_error()))
+	}
+	s := &SharedBatcher{b: b, k: k, r: r, slot: slotBytes}
+	runtime.SetFinalizer(s, (*SharedBatcher).Close)
+	return s, nil
+}
+
 // Flush closes the pending batch now instead of at its deadline.
 func (s *SharedBatcher) Flush() {
 	s.closeMu.RLock()
@@ -315,6 +350,26 @@ func NewSharedDecodeBatcher(k, r, slotBytes, maxGroups int, deadline time.Durati
 	runtime.LockOSThread() // the creation error is thread-local
 	defer runtime.UnlockOSThread()
 	b := C.fec_batcher_new_decoder(C.int(device), C.uint32_t(k), C.uint32_t(r), C.uint32_t(slotBytes),
+		C.uint32_t(maxGroups), C.uint32_t(deadline/time.Microsecond), 3)
+	if b == nil {
+		return nil, fmt.Errorf("no usable GPU decode batcher: %s", C.GoString(C.fec_batcher_last_error()))
+	}
+	s := &SharedDecodeBatcher{b: b, k: k, r: r, slot: slotBytes}
+	runtime.SetFinalizer(s, (*SharedDecodeBatcher).Close)
+	return s, nil
+}
+
+// NewSharedDecodeBatcherMulti: one decoder batcher per listed GPU behind one handle
+// (fec_batcher_new_decoder_multi; nil = every visible GPU).
+func NewSharedDecodeBatcherMulti(k, r, slotBytes, maxGroups int, deadline time.Duration, devices []int) (*SharedDecodeBatcher, error) {
+	if k < 1 || r < 1 || k+r > 64 || slotBytes < 1 || maxGroups < 1 || deadline < 0 {
+		return nil, fmt.Errorf("unsupported decode batcher k=%d r=%d slot=%d maxGroups=%d", k, r, slotBytes, maxGroups)
+	}
+	runtime.LockOSThread() // the creation error is thread-local
+	defer runtime.UnlockOSThread()
+	dp, dn, free := devicesArg(devices)
+	defer free()
+	b := C.fec_batcher_new_decoder_multi(dp, dn, C.uint32_t(k), C.uint32_t(r), C.uint32_t(slotBytes),
 		C.uint32_t(maxGroups), C.uint32_t(deadline/time.Microsecond), 3)
 	if b == nil {
 		return nil, fmt.Errorf("no usable GPU decode batcher: %s", C.GoString(C.fec_batcher_last_error()))

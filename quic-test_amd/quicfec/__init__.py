@@ -49,6 +49,7 @@ HIP_SYMBOLS = (
     "fec_batcher_new", "fec_batcher_free", "fec_batcher_submit", "fec_batcher_submit_packets",
     "fec_batcher_wait", "fec_batcher_flush", "fec_batcher_stats", "fec_batcher_last_error",
     "fec_batcher_new_decoder", "fec_batcher_submit_shards", "fec_batcher_wait_rebuilt",
+    "fec_batcher_new_multi", "fec_batcher_new_decoder_multi", "fec_batcher_devices",
 )
 
 
@@ -133,6 +134,9 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
         "fec_batcher_new_decoder": (_vp, [_int, _u32, _u32, _u32, _u32, _u32, _u32]),
         "fec_batcher_submit_shards": (ctypes.c_int64, [_vp, ctypes.POINTER(_vp), _u32]),
         "fec_batcher_wait_rebuilt": (_int, [_vp, ctypes.c_int64, _vp, _u32, _vp, ctypes.c_int64]),
+        "fec_batcher_new_multi": (_vp, [_vp, _int, _u32, _u32, _u32, _u32, _u32, _u32]),
+        "fec_batcher_new_decoder_multi": (_vp, [_vp, _int, _u32, _u32, _u32, _u32, _u32, _u32]),
+        "fec_batcher_devices": (_int, [_vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -350,13 +354,28 @@ class Batcher:
     STATS = ("groups", "batches", "full_flushes", "deadline_flushes", "max_batch", "expired")
 
     def __init__(self, k: int, r: int, slot_bytes: int = 1500, max_groups: int = 4096, deadline_us: int = 1000,
-                 device: int = -1, slabs: int = 3):
+                 device: int = -1, slabs: int = 3, devices=None):
+        """devices: a list of GPU ordinals (repeats allowed) for one batcher per device behind
+        this handle (fec_batcher_new_multi); None: the single `device`."""
         self.lib = load_library()
         self.k, self.r, self.slot = k, r, slot_bytes
-        h = self.lib.fec_batcher_new(device, k, r, slot_bytes, max_groups, deadline_us, slabs)
+        self.handle = self._create(False, device, devices, k, r, slot_bytes, max_groups, deadline_us, slabs)
+
+    def _create(self, decoder, device, devices, *shape):
+        if devices is None:
+            fn = "fec_batcher_new_decoder" if decoder else "fec_batcher_new"
+            h = getattr(self.lib, fn)(device, *shape)
+        else:
+            fn = "fec_batcher_new_decoder_multi" if decoder else "fec_batcher_new_multi"
+            devs = np.ascontiguousarray(devices, dtype=np.int32)
+            h = getattr(self.lib, fn)(devs.ctypes.data if devs.size else None, int(devs.size), *shape)
         if not h:
-            raise FecError("fec_batcher_new", FEC_ERR_NODEV, self.last_error())
-        self.handle = h
+            raise FecError(fn, FEC_ERR_NODEV, self.last_error())
+        return h
+
+    def devices(self) -> int:
+        """GPUs behind this handle."""
+        return int(self.lib.fec_batcher_devices(self.handle))
 
     def last_error(self) -> str:
         return (self.lib.fec_batcher_last_error() or b"").decode(errors="replace")
@@ -419,13 +438,10 @@ class DecodeBatcher(Batcher):
     (fec_batcher_new_decoder, include/fec_hip.h)."""
 
     def __init__(self, k: int, r: int, slot_bytes: int = 1500, max_groups: int = 4096, deadline_us: int = 1000,
-                 device: int = -1, slabs: int = 3):
+                 device: int = -1, slabs: int = 3, devices=None):
         self.lib = load_library()
         self.k, self.r, self.slot = k, r, slot_bytes
-        h = self.lib.fec_batcher_new_decoder(device, k, r, slot_bytes, max_groups, deadline_us, slabs)
-        if not h:
-            raise FecError("fec_batcher_new_decoder", FEC_ERR_NODEV, self.last_error())
-        self.handle = h
+        self.handle = self._create(True, device, devices, k, r, slot_bytes, max_groups, deadline_us, slabs)
         self._lens = {}
 
     def submit(self, shards, length: int) -> int:

@@ -658,10 +658,15 @@ static void TestBatcherDeadline() {
 // collected in a random order of polls and blocking waits.  Every row 0 returned must be
 // the XOR; with 42 result slots (3 * 2 slabs * 7) results also expire while waiters read
 // them, and each expiry must surface as FEC_ERR_RANGE, counted once in the stats.
-static void TestBatcherReservationStress() {
+// multi: the same through fec_batcher_new_multi with two batchers on device 0 (tickets
+// interleaved over the two, results routed back by ticket).
+static void TestBatcherReservationStress(bool multi = false) {
   for (int deadline_us : {0, 20}) {
     const uint32_t k = 6, r = 2, slot = 256, S = 16, G = 600;
-    FECBatcher* b = fec_batcher_new(-1, k, r, slot, 7, deadline_us, 2);
+    const int devs[2] = {0, 0};
+    FECBatcher* b = multi ? fec_batcher_new_multi(devs, 2, k, r, slot, 7, deadline_us, 2)
+                          : fec_batcher_new(-1, k, r, slot, 7, deadline_us, 2);
+    CHECK(!multi || fec_batcher_devices(b) == 2);
     CHECK(b != nullptr);
     if (!b) return;
     std::atomic<int> bad{0};
@@ -715,7 +720,7 @@ static void TestBatcherReservationStress() {
     FECBatcherStats st{};
     fec_batcher_stats(b, &st);
     CHECK(st.groups == uint64_t(S) * G && st.max_batch <= 7 && st.expired == expired.load());
-    std::fprintf(stderr, "reservation stress, deadline %d us: %llu batches, %llu full, %llu results expired\n", deadline_us,
+    std::fprintf(stderr, "reservation stress%s, deadline %d us: %llu batches, %llu full, %llu results expired\n", multi ? " (2 batchers)" : "", deadline_us,
                 (unsigned long long)st.batches, (unsigned long long)st.full_flushes, (unsigned long long)st.expired);
     if (deadline_us == 0) CHECK(st.full_flushes > 0 || st.deadline_flushes > 0);
     fec_batcher_free(b);
@@ -778,9 +783,11 @@ static void TestDecoderSharedBatcher() {
 // data packet and kept its repair is rebuilt byte for byte.  (As decoder.go does, a group
 // whose repair arrives first is also "recovered" when its last packet is merely late: every
 // group with its repair and at most one data loss is rebuilt once.)
-static void TestEndToEndBothBatchers() {
-  auto enc = SharedFECBatcher::New(10, 1, 1500, 256, 300);
-  auto dec = SharedFECDecodeBatcher::New(10, 1, 1500, 256, 300);
+// multi: both batchers with one batcher per listed device (device 0 twice on a one-GPU box).
+static void TestEndToEndBothBatchers(bool multi = false) {
+  auto enc = multi ? SharedFECBatcher::NewMulti({0, 0}, 10, 1, 1500, 256, 300) : SharedFECBatcher::New(10, 1, 1500, 256, 300);
+  auto dec = multi ? SharedFECDecodeBatcher::NewMulti({0, 0}, 10, 1, 1500, 256, 300)
+                   : SharedFECDecodeBatcher::New(10, 1, 1500, 256, 300);
   CHECK(enc != nullptr && dec != nullptr);
   if (!enc || !dec) return;
   std::atomic<int> bad{0}, expect{0}, rebuilt{0}, attempts{0};
@@ -860,6 +867,8 @@ int main() {
   TestBatcherReservationStress();
   TestDecoderSharedBatcher();
   TestEndToEndBothBatchers();
+  TestBatcherReservationStress(true);
+  TestEndToEndBothBatchers(true);
   if (g_fail) {
     std::printf("FAILED %d of %d checks\n", g_fail, g_checks);
     return 1;

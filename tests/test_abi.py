@@ -85,6 +85,17 @@ def test_null_arguments_need_no_gpu(quicfec_mod):
     assert "unsupported" in lib.fec_batcher_last_error().decode()
     assert not lib.fec_batcher_new_decoder(-1, 60, 5, 1200, 16, 100, 2)      # k + r > 64
     assert "fec_batcher_new_decoder: unsupported" in lib.fec_batcher_last_error().decode()
+    # several devices behind one handle: the same checks, the failing device named
+    assert lib.fec_batcher_devices(None) == quicfec_mod.FEC_ERR_NULL
+    devs = np.array([0, 1], dtype=np.int32)
+    assert not lib.fec_batcher_new_multi(devs.ctypes.data, 2, 200, 57, 1200, 16, 100, 2)
+    msg = lib.fec_batcher_last_error().decode()
+    assert "fec_batcher_new_multi: device 0" in msg and "unsupported" in msg, msg
+    assert not lib.fec_batcher_new_decoder_multi(devs.ctypes.data, 2, 60, 5, 1200, 16, 100, 2)
+    assert "unsupported" in lib.fec_batcher_last_error().decode()
+    neg = np.array([-3, 0], dtype=np.int32)
+    assert not lib.fec_batcher_new_multi(neg.ctypes.data, 2, 10, 3, 1200, 16, 100, 2)
+    assert "negative device ordinal" in lib.fec_batcher_last_error().decode()
 
 
 def test_no_gpu_context_is_null_not_abort(quicfec_mod):
@@ -103,6 +114,10 @@ def test_no_gpu_context_is_null_not_abort(quicfec_mod):
         quicfec_mod.Batcher(10, 3)
     with pytest.raises(quicfec_mod.FecError):
         quicfec_mod.DecodeBatcher(10, 3)
+    with pytest.raises(quicfec_mod.FecError, match="no GPU visible"):
+        quicfec_mod.Batcher(10, 3, devices=[])                 # every visible device: none
+    with pytest.raises(quicfec_mod.FecError, match="device 0"):
+        quicfec_mod.DecodeBatcher(10, 3, devices=[0, 0])
 
 
 def test_parity_matrix_matches_oracle_and_fixture(quicfec_mod, oracle_mod, golden_dir):

@@ -179,3 +179,64 @@ def test_decode_batcher_modes_and_threads(quicfec_mod, oracle_mod):
         st = b.stats()
     assert not errors, errors[:5]
     assert st["groups"] == S * G and st["batches"] < S * G
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_multi_device_batcher_rows_and_tickets(quicfec_mod, oracle_mod, devices):
+    """fec_batcher_new_multi: one batcher per listed device behind one handle (the same GPU
+    listed several times here: a one-GPU box).  Every group's rows equal the oracle's, tickets
+    are unique, and the stats sum over the devices."""
+    k, r = 10, 3
+    rng = np.random.default_rng(len(devices))
+    groups = [[oracle_mod.splitmix_bytes(int(rng.integers(1, 1201)), 5000 * g + j) for j in range(k if g % 5 else 3)]
+              for g in range(90)]
+    with quicfec_mod.Batcher(k, r, slot_bytes=1200, max_groups=8, deadline_us=2_000_000, devices=devices) as b:
+        assert b.devices() == len(devices)
+        tickets = [b.submit(pk) for pk in groups]
+        assert len(set(tickets)) == len(tickets)
+        # round robin: consecutive groups go to different devices (ticket % n = device index)
+        assert sorted(t % len(devices) for t in tickets[:len(devices)]) == list(range(len(devices)))
+        b.flush()
+        for pk, t in reversed(list(zip(groups, tickets))):      # any order
+            rows = b.wait(t, timeout_us=10_000_000)
+            assert rows is not None and all(np.array_equal(a, e) for a, e in zip(rows, _expected_rows(oracle_mod, pk, k, r))), t
+        st = b.stats()
+        assert st["groups"] == 90 and st["max_batch"] <= 8, st
+        with pytest.raises(quicfec_mod.FecError):
+            b.wait(tickets[0], timeout_us=0)                     # collected once only
+        with pytest.raises(quicfec_mod.FecError, match="unknown"):
+            b.wait(max(tickets) + len(devices) * 50, timeout_us=1000)
+
+
+def test_multi_device_batcher_concurrent_streams_and_decoder(quicfec_mod, oracle_mod):
+    k, r, S, G = 10, 3, 8, 30
+    errors = []
+    with quicfec_mod.Batcher(k, r, slot_bytes=1200, max_groups=16, deadline_us=300, devices=[0, 0]) as enc, \
+            quicfec_mod.DecodeBatcher(k, r, slot_bytes=1200, max_groups=16, deadline_us=300, devices=[0, 0]) as dec:
+        assert dec.devices() == 2
+
+        def stream(s):
+            try:
+                rng = np.random.default_rng(s)
+                for g in range(G):
+                    pk = [oracle_mod.splitmix_bytes(1200, s * 10_000 + g * 16 + j) for j in range(k)]
+                    rows = enc.wait(enc.submit(pk))
+                    if not all(np.array_equal(a, e) for a, e in zip(rows, _expected_rows(oracle_mod, pk, k, r))):
+                        errors.append(("enc", s, g))
+                        continue
+                    shards = list(pk) + list(rows)
+                    lost = set(int(x) for x in rng.choice(k + r, size=int(rng.integers(1, r + 1)), replace=False))
+                    ids, rb = dec.wait(dec.submit([None if j in lost else shards[j] for j in range(k + r)], 1200))
+                    if ids != sorted(j for j in lost if j < k) or not all(
+                            np.array_equal(x, shards[j]) for j, x in zip(ids, rb)):
+                        errors.append(("dec", s, g))
+            except Exception as e:   # noqa: BLE001 - reported below
+                errors.append(repr(e))
+        th = [threading.Thread(target=stream, args=(s,)) for s in range(S)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        st_e, st_d = enc.stats(), dec.stats()
+    assert not errors, errors[:5]
+    assert st_e["groups"] == S * G and st_d["groups"] == S * G
