@@ -55,6 +55,13 @@ def quicfec_mod():
 
 
 @pytest.fixture(scope="session")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+@pytest.fixture(scope="session")
 def gpu_ctx(quicfec_mod):
     ctx = quicfec_mod.Context(device=0)
     yield ctx

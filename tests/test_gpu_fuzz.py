@@ -12,13 +12,6 @@ pytestmark = pytest.mark.gpu
 SEED = 0x5EED0F00
 
 
-@pytest.fixture(scope="module")
-def torch_cuda():
-    import torch
-    assert torch.cuda.is_available()
-    return torch
-
-
 def _case(rng):
     k = int(rng.integers(1, 21))
     r = int(rng.integers(1, min(8, 64 - k) + 1))

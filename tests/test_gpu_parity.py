@@ -13,13 +13,6 @@ pytestmark = pytest.mark.gpu
 SEED = 0x5EED0000
 
 
-@pytest.fixture(scope="module")
-def torch_cuda():
-    import torch
-    assert torch.cuda.is_available()
-    return torch
-
-
 def _dev(torch, arr):
     return torch.from_numpy(np.ascontiguousarray(arr)).cuda()
 
