@@ -520,6 +520,8 @@ def main() -> int:
         cfg["workload"] += f" (shape override k={cfg['k']} r={cfg['r']} P={cfg['P']})"
     k, r, P = cfg["k"], cfg["r"], cfg["P"]
     G = args.groups or cfg["groups"]
+    if args.groups:
+        cfg["workload"] += f" (groups override: {G}/GPU)"
     g0, _ = shard_range(G * world, rank, world)
 
     ctx = quicfec.Context(device=local)
