@@ -1295,10 +1295,17 @@ hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
       // with r >= 4 rows of table arithmetic per load the kernel is VALU-bound and wants more
       // waves: k=20 r=5 at 4 workgroups 5.22-5.40 ms, 3: 5.35-5.50, uncapped 5.22-5.59
       // (profiles/r02_ab_encode_blocks_c4.txt, two boxes).  The runtime-k loop runs uncapped.
+      // The XOR-only kernel (r = 1, the reference's computation) streams best at ~15 waves per
+      // CU: k=10 at 1200 B (5-wave workgroups) 2.30 ms at 3 workgroups vs 2.39 at 2 and 2.36 at
+      // 4; at 1400 B (7-wave workgroups) 2 (14 waves) beats 3 (21) by 1.7%
+      // (profiles/r02_ab_encode_blocks_r1.txt, r02_ab_encode_blocks_r2.txt).
       constexpr int kDefBlocks = K == 0 ? 0 : (R >= 4 ? kEncodeBlocksPerCU + 2 : kEncodeBlocksPerCU);
       const int blocks_per_cu = env_waves("QUICFEC_ENCODE_BLOCKS", kDefBlocks);
+      const char* eb = std::getenv("QUICFEC_ENCODE_BLOCKS");
+      const bool xor_waves = K > 0 && FIRST && R == 1 && !(eb && *eb);
       const int waves = a.waves_per_cu ? a.waves_per_cu
-                                       : env_waves("QUICFEC_ENCODE_WAVES", blocks_per_cu * static_cast<int>(bs / 64));
+                                       : env_waves("QUICFEC_ENCODE_WAVES", xor_waves ? kEncodeXorWavesPerCU
+                                                                                     : blocks_per_cu * static_cast<int>(bs / 64));
       const uint32_t smem = occupancy_cap_lds(waves, bs / 64);
       hipLaunchKernelGGL((encode_v16<K, R, OFF, FIRST, POL>), dim3(blocks), dim3(bs), smem, s, a.data,
                          a.offsets, a.parity, g0, n, cpp, a.P, a.k, a.r, row0,
@@ -1371,6 +1378,10 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
       if (a.k == 20 && a.r == 5)
         return pair ? run_encode_v16<20, 5, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<20, 5, 0, true>(a, 0, s);
       if (a.k == 4 && a.r == 2) return run_encode_v16<4, 2, 0, true>(a, 0, s);
+      // k=10 r=2 (the campaign's 20% FEC rate): compile-time k unless QUICFEC_ENCODE_RUNTIME_K=1
+      // (A/B against the runtime-k loop)
+      static const bool rt_k = env_waves("QUICFEC_ENCODE_RUNTIME_K", 0) == 1;
+      if (a.k == 10 && a.r == 2 && !rt_k) return run_encode_v16<10, 2, 0, true, kNtStore | kPairMac>(a, 0, s);
     } else if (a.off_kind == OffsetKind::kU32) {
       if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 1, true>(a, 0, s);
     }

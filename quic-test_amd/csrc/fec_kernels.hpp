@@ -32,6 +32,7 @@ struct EncodeLaunch {
 // for r >= 4 (k=20 r=5: 5.47 at 3 vs 4.99 at 2); none for the runtime-k kernel
 // (k=10 r=2: 5.61 uncapped vs 3.66 at 2).  profiles/r01_encode_blocks_sweep.txt.
 constexpr int kEncodeBlocksPerCU = 2;
+constexpr int kEncodeXorWavesPerCU = 15;  // r = 1 (XOR row only), rounded to whole workgroups
 constexpr int kDecodeWavesPerCU = 0;   // measured: any cap below ~20 waves/CU is slower
 
 // Dynamic LDS bytes that cap a workgroup of `waves_per_block` waves at about
