@@ -1283,7 +1283,10 @@ uint32_t pick_tile(uint32_t cpp, uint32_t k, uint32_t P) {
 template <int K, int R, int OFF, bool FIRST, int POL = kNtStore>
 hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
   const uint32_t cpp = (a.P + 15u) / 16u;
-  const uint32_t tile = pick_tile(cpp, a.k, a.P);
+  // QUICFEC_ENCODE_TILE: groups per workgroup override (tuning A/B; must fit 512 lanes)
+  const int tile_env = env_waves("QUICFEC_ENCODE_TILE", 0);
+  const uint32_t tile = tile_env > 0 && cpp > 0 && uint32_t(tile_env) * cpp <= 512 ? uint32_t(tile_env)
+                                                                                    : pick_tile(cpp, a.k, a.P);
   const uint64_t gchunk = kMaxThreadsPerLaunch / cpp;
   for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
     const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
