@@ -251,6 +251,19 @@ int main(int argc, char** argv) {
   if (k == 10 && r == 3 && P == 1200) {
     PSCAN(2) PSCAN(4) PSCAN(8) PSCAN(16) PSCAN(32) PSCAN(64)
     PSCAN(256) PSCAN(512) PSCAN(1024)
+    // sparse-loss ceilings of the same access pattern: survivor reads alone (no stores, XOR
+    // math), and XOR math with the stores (mismatch by design: rows 1.. not multiplied)
+    vars.push_back({"scan8 reads-only", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
+                      return run_decode_fused<10, 3, kNtLoad | kProbeNoStore | kProbeXorOnly, 1, 1, true, true, 8>(a, nullptr);
+                    }});
+    vars.push_back({"scan8 xor-math", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
+                      return run_decode_fused<10, 3, kNtStore | kNtLoad | kProbeXorOnly, 1, 1, true, true, 8>(a, nullptr);
+                    }});
+    vars.push_back({"scan8 compact-out", kDecodeFused, -1, 1, {}, [cout](const DecodeLaunch& a) {
+                      DecodeLaunch b = a;
+                      b.out = cout;
+                      return run_decode_fused<10, 3, kNtStore | kNtLoad | kCompactOut, 1, 1, true, true, 8>(b, nullptr);
+                    }});
   }
   // record-addressed fused form with the coefficient tables staged through LDS (kLdsTabs)
 #define PLDS(KK, RR, NMM, NTT)                                                                    \
