@@ -487,6 +487,9 @@ def main() -> int:
     ap.add_argument("--decode-api", default="recover", choices=("recover", "in-place"),
                     help="recover: fec_recover_batch_rs_dev (rebuilt packets returned back to back, as the "
                          "reference decoder returns Recovered buffers); in-place: fec_decode_batch_rs_dev")
+    ap.add_argument("--null-stream", action="store_true",
+                    help="launch through stream handle 0 (the context's own stream) with events on torch's "
+                         "default stream, as round-1/2 benches did (A/B of the timing setup)")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -525,7 +528,16 @@ def main() -> int:
     g0, _ = shard_range(G * world, rank, world)
 
     ctx = quicfec.Context(device=local)
-    stream = torch.cuda.current_stream()
+    # One stream for everything: the library's launches, torch's ops and the timing events.
+    # torch's default stream has handle 0, which the C-ABI reads as "the context's own
+    # stream" (a blocking stream); launching there while recording events on the default
+    # stream made every event an implicit cross-stream synchronisation inside the timed steps
+    # (~15-60 us per kernel, profiles/r02_stream_ab.txt).  --null-stream keeps that old setup.
+    if args.null_stream:
+        stream = torch.cuda.current_stream()
+    else:
+        stream = torch.cuda.Stream()
+        torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
     data = torch.empty(G * k * P, dtype=torch.uint8, device="cuda")
@@ -678,7 +690,10 @@ def main() -> int:
                 "read_frac": round(dom_read / (kernels[dom]["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "box_copy_GBps": copy["achieved_GBps"],
                 "frac_of_box_copy": round(kernels[dom]["achieved_GBps"] / copy["achieved_GBps"], 4),
-                "timing": "torch.cuda.Event on the launch stream, averaged over the timed steps"}
+                "timing": ("torch.cuda.Event on torch's default stream, kernels on the context's stream"
+                           if args.null_stream else
+                           "torch.cuda.Event on the launch stream (one torch stream for launches, ops and "
+                           "events), averaged over the timed steps")}
 
     e2e = None
     if args.e2e:
