@@ -490,6 +490,8 @@ def main() -> int:
     ap.add_argument("--null-stream", action="store_true",
                     help="launch through stream handle 0 (the context's own stream) with events on torch's "
                          "default stream, as round-1/2 benches did (A/B of the timing setup)")
+    ap.add_argument("--parity-offset", type=int, default=0, help="parity buffer placement (bytes past an allocation start)")
+    ap.add_argument("--rebuilt-offset", type=int, default=0, help="rebuilt-packet buffer placement (bytes)")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -540,13 +542,19 @@ def main() -> int:
         torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
+    def dev_buffer(nbytes: int, offset: int):
+        """nbytes of HBM starting `offset` bytes into a fresh allocation (buffer placement A/B)."""
+        if offset <= 0:
+            return torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        return torch.empty(nbytes + offset, dtype=torch.uint8, device="cuda")[offset:]
+
     data = torch.empty(G * k * P, dtype=torch.uint8, device="cuda")
-    parity = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
+    parity = dev_buffer(G * r * P, args.parity_offset)
     # this rank's slice of one global synthetic stream
     ctx.fill_random_dev(data, data.numel(), SEED + 2, byte_offset=g0 * k * P, stream=sp)
     dec_bytes = dec_read = 0
     recover = cfg["decode"] and args.decode_api == "recover"
-    rebuilt = torch.empty(G * r * P, dtype=torch.uint8, device="cuda") if recover else None
+    rebuilt = dev_buffer(G * r * P, args.rebuilt_offset) if recover else None
 
     def decode_call(api: str, status=None):
         if api == "recover":
@@ -667,7 +675,7 @@ def main() -> int:
         # the other decode API on the same buffers, for comparison (not in `value`)
         other = "in-place" if recover else "recover"
         if other == "recover" and rebuilt is None:
-            rebuilt = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
+            rebuilt = dev_buffer(G * r * P, args.rebuilt_offset)
         kernels["decode"]["other_api"] = {"api": other, **isolated(lambda: decode_call(other), dec_bytes)}
     # The box's own HBM copy rate (fec_copy_dev: the encode's 16-B-per-lane pattern, no
     # arithmetic), measured the same way: box-to-box spread is a few percent, so the kernels
