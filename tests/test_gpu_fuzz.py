@@ -4,12 +4,17 @@ count, erasure patterns (up to r + 1 lost, so some groups are unrecoverable) and
 generator.  Each case is small, the whole sweep runs in seconds; it exists to catch the
 interaction bugs that the per-shape parity tests do not pin (form selection, workspace and
 staging reuse across calls of different shapes on one context)."""
+import os
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
-SEED = 0x5EED0F00
+# QUICFEC_FUZZ_SEED / QUICFEC_FUZZ_BLOCKS widen the sweep for a long run (the default is the
+# committed 12 blocks of 10 cases)
+SEED = int(os.environ.get("QUICFEC_FUZZ_SEED", str(0x5EED0F00)), 0)
+BLOCKS = int(os.environ.get("QUICFEC_FUZZ_BLOCKS", "12"))
 
 
 def _case(rng):
@@ -29,7 +34,7 @@ def _masks(rng, G, k, r):
     return m
 
 
-@pytest.mark.parametrize("block", range(12))
+@pytest.mark.parametrize("block", range(BLOCKS))
 def test_random_shapes_all_apis(gpu_ctx, oracle_mod, torch_cuda, block):
     torch = torch_cuda
     rng = np.random.default_rng(SEED + block)
