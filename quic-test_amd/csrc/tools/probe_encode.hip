@@ -191,6 +191,56 @@ __global__ __launch_bounds__(((T * 75 + 63) / 64) * 64) void enc_xcd(const uint8
   for (int i = 0; i < R; ++i) st16<POL>(parity + (g * R + i) * P + col * 16u, acc[i]);
 }
 
+// Two groups per lane: a workgroup owns 2T whole groups, lane (gl, col) computes column col
+// of groups 2gl and 2gl+1 (the second group's loads issued with the first's), so each lane
+// has 2K loads in flight and stores 2R rows at once: half the waves for the same bytes in
+// flight, and the writes leave in bursts twice as large.  XCD-aware tile order; R = 1 or 3.
+template <int T, int R, int POL>
+__global__ __launch_bounds__(((T * 75 + 63) / 64) * 64) void enc_2g(const uint8_t* __restrict__ data,
+                                                                  uint8_t* __restrict__ parity, uint32_t groups,
+                                                                  const Tab* __restrict__ tabs) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t cap_lds[];
+  if (groups == 0xFFFFFFFFu) cap_lds[threadIdx.x] = 0;
+  constexpr int K = 10, P = 1200, CPP = 75;
+  const uint32_t nb = gridDim.x, b = blockIdx.x;
+  const uint32_t per = nb / 8;
+  const uint32_t tile = (b < per * 8) ? (b % 8) * per + b / 8 : b;
+  const uint32_t lane = threadIdx.x;
+  if (lane >= T * CPP) return;
+  const uint32_t gl = lane / CPP, col = lane - gl * CPP;
+  const uint64_t g0 = uint64_t(tile) * (2 * T) + 2 * gl;
+  if (g0 >= groups) return;
+  const bool two = g0 + 1 < groups;
+  const uint8_t* src = data + g0 * K * P + col * 16u;
+  u32x4 d[2][K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) d[0][j] = ld16<POL>(src + j * P);
+#pragma unroll
+  for (int j = 0; j < K; ++j) d[1][j] = two ? ld16<POL>(src + (K + j) * P) : d[0][j];
+  u32x4 acc[2][R];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[h][i] = d[h][0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+      acc[h][0] ^= d[h][j];
+      if constexpr (R > 1) {
+        Sel s;
+        prep(d[h][j], s);
+#pragma unroll
+        for (int i = 1; i < R; ++i) mac(acc[h][i], s, tabs[(i - 1) * K + j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) st16<POL>(parity + (g0 * R + i) * P + col * 16u, acc[0][i]);
+  if (two) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) st16<POL>(parity + ((g0 + 1) * R + i) * P + col * 16u, acc[1][i]);
+  }
+}
+
 // enc_blk as a persistent grid: each workgroup walks tiles blockIdx.x, +gridDim.x, ...
 template <int T, int POL>
 __global__ __launch_bounds__(((T * 75 + 63) / 64) * 64) void enc_persist(const uint8_t* __restrict__ data,
@@ -495,6 +545,34 @@ int main(int argc, char** argv) {
                       enc_xcd<4, 2><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab);
                     }, {}});
   }
+  // two groups per lane (enc_2g): 2 x 4 groups per 5-wave workgroup at 1 / 2 / 3 workgroups per CU
+  for (int per_cu : {1, 2, 3, 4}) {
+    const uint32_t smem = per_cu >= 4 ? 0u : 160u * 1024u / (per_cu + 1) + 16u;
+    vars.push_back({"enc_2g<4,3> x" + std::to_string(per_cu), enc_bytes, [=] {
+                      enc_2g<4, 3, 2><<<uint32_t((G + 7) / 8), 320, smem>>>(data, par, uint32_t(G), dtab);
+                    }, {}});
+  }
+  // XOR row only (r = 1): the production kernel at its r = 1 default vs two groups per lane
+  {
+    const uint64_t xor_bytes = (k + 1) * uint64_t(P) * G;
+    EncodeLaunch e1;
+    e1.data = data;
+    e1.offsets = nullptr;
+    e1.off_kind = OffsetKind::kNone;
+    e1.parity = scratch;
+    e1.groups = G;
+    e1.k = k;
+    e1.r = 1;
+    e1.P = P;
+    e1.tables = nullptr;
+    vars.push_back({"xor prod r1", xor_bytes, [=] { CK(launch_encode(e1, nullptr)); }, {}});
+    for (int per_cu : {1, 2, 3, 4}) {
+      const uint32_t smem = per_cu >= 4 ? 0u : 160u * 1024u / (per_cu + 1) + 16u;
+      vars.push_back({"xor_2g r1 x" + std::to_string(per_cu), xor_bytes, [=] {
+                        enc_2g<4, 1, 2><<<uint32_t((G + 7) / 8), 320, smem>>>(data, scratch, uint32_t(G), dtab);
+                      }, {}});
+    }
+  }
   {
     const uint32_t smem = 160 * 1024 / 3 + 16;  // 2 workgroups (10 waves) per CU
     vars.push_back({"algn ld0 st0", enc_bytes, [=] { enc_align<false, false><<<uint32_t((G + 3) / 4), 320, smem>>>(data, par, uint32_t(G), dtab); }, {}});
@@ -597,6 +675,18 @@ int main(int argc, char** argv) {
       CK(hipMemset(par, 0, np));
       v.run();
       CK(hipMemcpy(got.data(), par, np, hipMemcpyDeviceToHost));
+      std::printf("check %-22s %s\n", v.name.c_str(), got == ref ? "OK" : "MISMATCH");
+    }
+  }
+  {  // the r = 1 variants against the production XOR kernel
+    const uint64_t nx = G * uint64_t(P);
+    std::vector<uint8_t> ref, got(nx);
+    for (auto& v : vars) {
+      if (v.name.rfind("xor", 0) != 0) continue;
+      CK(hipMemset(scratch, 0, nx));
+      v.run();
+      CK(hipMemcpy(got.data(), scratch, nx, hipMemcpyDeviceToHost));
+      if (ref.empty()) ref = got;
       std::printf("check %-22s %s\n", v.name.c_str(), got == ref ? "OK" : "MISMATCH");
     }
   }
