@@ -86,7 +86,7 @@ static void TestFECEncoderFullGroup() {
       CHECK(r.needsRedundancy);
       CHECK(r.redundancy.size() == 1211);
       const uint8_t hdr[11] = {0xFE, 0xC0, 0, 0, 0, 0, 0, 0, 0, 0, 10};
-      CHECK(std::memcmp(r.redundancy.data(), hdr, 11) == 0);
+      CHECK(r.redundancy.size() >= 11 && std::memcmp(r.redundancy.data(), hdr, 11) == 0);
       bool ones = true;
       for (size_t b = 11; b < r.redundancy.size(); ++b) ones &= r.redundancy[b] == 1;
       CHECK(ones);
