@@ -2,31 +2,36 @@
 # Host-code AddressSanitizer run of the C++ mirror test (batcher, shim, host mirror).
 #   bash scripts/asan_host.sh build   # in the build container: instrumented copies in build/asan/
 #   bash scripts/asan_host.sh run     # on the GPU box
+#   SAN=thread: the same with ThreadSanitizer into build/tsan/ (HIP runtime frames suppressed)
 # The shim and batcher are compiled with -Xarch_host -fsanitize=address (device code is not
 # instrumented: GPU sanitizers are not available on this pool), the mirror and its test with
 # clang++ -fsanitize=address, against the product's kernel object.  Leak checking is off (the
 # HIP runtime keeps allocations until exit).
 set -euo pipefail
 cd "$(dirname "$0")/.."
-A=build/asan
+SANK=${SAN:-address}
+A=build/$([ "$SANK" = thread ] && echo tsan || echo asan)
 case "${1:-run}" in
   build)
     mkdir -p $A
     H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -fvisibility=hidden -Iinclude -Iquic-test_amd/csrc"
-    SAN="-Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer"
-    $H -x hip -c -o $A/fec_shim.o quic-test_amd/csrc/fec_shim.cpp $SAN
-    $H -x hip -c -o $A/fec_batcher.o quic-test_amd/csrc/fec_batcher.cpp $SAN
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -fsanitize=address -shared-libasan -o $A/libfec_hip.so \
+    SANF="-Xarch_host -fsanitize=$SANK -Xarch_host -fno-omit-frame-pointer"
+    $H -x hip -c -o $A/fec_shim.o quic-test_amd/csrc/fec_shim.cpp $SANF
+    $H -x hip -c -o $A/fec_batcher.o quic-test_amd/csrc/fec_batcher.cpp $SANF
+    RT=$([ "$SANK" = thread ] && echo "" || echo -shared-libasan)
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -fsanitize=$SANK $RT -o $A/libfec_hip.so \
       quic-test_amd/lib/fec_kernels.o $A/fec_shim.o $A/fec_batcher.o
-    C="/opt/rocm/llvm/bin/clang++ -O1 -g -std=c++17 -fsanitize=address -shared-libasan -fno-omit-frame-pointer -Iinclude -Iquic-test_amd/host"
+    C="/opt/rocm/llvm/bin/clang++ -O1 -g -std=c++17 -fsanitize=$SANK $RT -fno-omit-frame-pointer -Iinclude -Iquic-test_amd/host"
     $C -fPIC -shared -o $A/libquicfec_host.so quic-test_amd/host/fec.cpp -L$A -lfec_hip -Wl,-rpath,'$ORIGIN'
     $C -o $A/host_mirror_test tests/csrc/host_mirror_test.cpp -L$A -lquicfec_host -lfec_hip oracle/liboracle.so \
       -Wl,-rpath,'$ORIGIN' -Wl,-rpath,'$ORIGIN/../../oracle' -lpthread
-    cp /opt/rocm/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so $A/
+    [ "$SANK" = thread ] || cp /opt/rocm/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so $A/
+    printf 'called_from_lib:libamdhip64.so\ncalled_from_lib:libhsa-runtime64.so\nrace:libamdhip64.so\nrace:libhsa-runtime64.so\n' > $A/tsan.supp
     ;;
   run)
     export LD_LIBRARY_PATH=$A
     export ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0:verify_asan_link_order=0:halt_on_error=1
+    export TSAN_OPTIONS="suppressions=$A/tsan.supp:report_signal_unsafe=0:second_deadlock_stack=1:history_size=4"
     timeout -k 10 600 $A/host_mirror_test
     ;;
 esac

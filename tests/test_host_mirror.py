@@ -28,3 +28,16 @@ def test_host_mirror_encoder_test_go(tmp_path, oracle_mod, quicfec_mod):
     exe = _build(tmp_path)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0 and out.stdout.strip().startswith("PASS"), out.stdout + out.stderr
+
+
+@pytest.mark.gpu
+def test_contexts_share_no_staging(tmp_path, quicfec_mod):
+    """16 threads, one context each, the reference's one-group fec_encode_batch calls on their
+    own page-locked slabs with shuffled offsets and random sizes: every repair equals the CPU XOR
+    (tests/csrc/ctx_isolation_test.cpp)."""
+    exe = tmp_path / "ctx_isolation_test"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-I", str(REPO / "include"),
+                    str(REPO / "tests" / "csrc" / "ctx_isolation_test.cpp"), "-L", str(LIB), "-lfec_hip",
+                    f"-Wl,-rpath,{LIB}", "-lpthread", "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe), "16", "1500"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.strip().startswith("PASS"), out.stdout + out.stderr
