@@ -583,6 +583,19 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   return FEC_OK;
 }
 
+// A pipelined call that fails part-way returns only after its slots' streams have drained:
+// earlier chunks' copies still read the caller's buffers and write its outputs.
+struct PipeDrain {
+  FECEncoderCtx* ctx;
+  bool done = false;
+  ~PipeDrain() {
+    if (done) return;
+    for (auto& p : ctx->pipe)
+      if (p.s) (void)hipStreamSynchronize(p.s);
+    (void)hipGetLastError();
+  }
+};
+
 int ensure_pipe(FECEncoderCtx* ctx) {
   for (auto& p : ctx->pipe)
     if (!p.s) QFEC_HIP(hipStreamCreateWithFlags(&p.s, hipStreamNonBlocking));
@@ -597,6 +610,7 @@ int encode_host_pipelined(FECEncoderCtx* ctx, const uint8_t* data, uint64_t G, u
                           uint32_t P, uint8_t* parity_out) {
   int rc = ensure_pipe(ctx);
   if (rc != FEC_OK) return rc;
+  PipeDrain drain{ctx};
   const uint64_t in_g = uint64_t(k) * P, out_g = uint64_t(r) * P;
   uint64_t cg = pipe_chunk_bytes() / in_g;
   cg = cg == 0 ? 1 : (cg > G ? G : cg);
@@ -615,6 +629,7 @@ int encode_host_pipelined(FECEncoderCtx* ctx, const uint8_t* data, uint64_t G, u
     QFEC_HIP(hipMemcpyAsync(parity_out + g0 * out_g, sl.par.ptr, n * out_g, hipMemcpyDeviceToHost, sl.s));
   }
   for (auto& p : ctx->pipe) QFEC_HIP(hipStreamSynchronize(p.s));
+  drain.done = true;
   return FEC_OK;
 }
 
@@ -622,6 +637,7 @@ int decode_host_pipelined(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
                           uint64_t G, uint32_t k, uint32_t r, uint32_t P, uint8_t* status_out) {
   int rc = ensure_pipe(ctx);
   if (rc != FEC_OK) return rc;
+  PipeDrain drain{ctx};
   const uint64_t in_g = uint64_t(k) * P, par_g = uint64_t(r) * P;
   uint64_t cg = pipe_chunk_bytes() / in_g;
   cg = cg == 0 ? 1 : (cg > G ? G : cg);
@@ -657,6 +673,7 @@ int decode_host_pipelined(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
     QFEC_HIP(hipMemcpyAsync(status_out + g0, sl.status.ptr, n, hipMemcpyDeviceToHost, sl.s));
   }
   for (auto& p : ctx->pipe) QFEC_HIP(hipStreamSynchronize(p.s));
+  drain.done = true;
   return FEC_OK;
 }
 
@@ -672,6 +689,7 @@ int decode_host_compacted(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
                           const std::vector<uint64_t>& need, uint32_t k, uint32_t r, uint32_t P) {
   int rc = ensure_pipe(ctx);
   if (rc != FEC_OK) return rc;
+  PipeDrain drain{ctx};
   const uint64_t N = need.size();
   const uint64_t in_g = uint64_t(k) * P, par_g = uint64_t(r) * P;
   uint64_t cg = pipe_chunk_bytes() / in_g;
@@ -735,6 +753,7 @@ int decode_host_compacted(FECEncoderCtx* ctx, uint8_t* data, const uint8_t* pari
     rc = scatter(p);
     if (rc != FEC_OK) return rc;
   }
+  drain.done = true;
   return FEC_OK;
 }
 
