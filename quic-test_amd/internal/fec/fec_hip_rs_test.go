@@ -126,3 +126,28 @@ func TestBatchedEncoderMatchesHybrid(t *testing.T) {
 		t.Fatalf("stats %v: expected %d groups in fewer launches", st, 16*21)
 	}
 }
+
+// One batcher per listed device behind one handle (the same GPU listed twice also works):
+// repairs equal HybridFECEncoder's and the stats sum over both batchers.
+func TestBatchedEncoderOnMultiDeviceBatcher(t *testing.T) {
+	sb, err := NewSharedBatcherMulti(10, 1, 1500, 64, time.Millisecond, []int{0, 0})
+	if err != nil {
+		t.Skipf("no GPU: %v", err)
+	}
+	defer sb.Close()
+	be := sb.NewEncoder()
+	hy := NewHybridFECEncoder(0.1)
+	rng := rand.New(rand.NewSource(7))
+	for i := 0; i < 10*30; i++ {
+		pkt := make([]byte, 1+rng.Intn(1400))
+		rng.Read(pkt)
+		a1, r1, e1 := be.AddPacket(pkt, uint64(i))
+		a2, r2, e2 := hy.AddPacket(pkt, uint64(i))
+		if e1 != nil || e2 != nil || a1 != a2 || !bytes.Equal(r1, r2) {
+			t.Fatalf("packet %d: multi-device batched and hybrid repairs differ", i)
+		}
+	}
+	if st := sb.Stats(); st[0] != 30 {
+		t.Fatalf("stats %v: expected 30 groups", st)
+	}
+}
