@@ -30,6 +30,50 @@ __global__ void poison(uint8_t* data, const uint64_t* masks, uint64_t groups, ui
   const uint32_t j = uint32_t((t / P) % k);
   if ((masks[g] >> j) & 1) data[t] = 0xEE;
 }
+// Write-layout probe (k=10 r=3, 1200 B): one wave per group loads its 10 survivors (the mask's
+// surviving data shards, then the lowest surviving parity rows, as the mask-addressed recover
+// does), XORs them (the GF arithmetic is free at this size, r01/r02 probes) and stores the
+// result as each of its e rebuilt rows, either at the recover API's slots (g*3 + m)*P
+// (PACKED = 0) or back to back over all groups, row pre[g] + m (PACKED = 1: no gaps between
+// groups' rows).  Timing only: the bytes are not the recovered packets.
+template <int PACKED>
+__global__ __launch_bounds__(256) void wr_layout(const uint8_t* __restrict__ data, const uint8_t* __restrict__ parity,
+                                                 const uint64_t* __restrict__ masks, const uint32_t* __restrict__ pre,
+                                                 uint8_t* __restrict__ out, uint64_t groups) {
+  constexpr uint32_t K = 10, R = 3, P = 1200;
+  const uint64_t g = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  if (g >= groups) return;
+  const uint64_t m = masks[g];
+  const uint64_t lost = m & 0x3FFu;
+  const uint32_t e = uint32_t(__popcll(lost));
+  if (e == 0 || e > R - uint32_t(__popcll((m >> K) & 7u))) return;
+  uint64_t alive = ~(m >> K) & 7u, rsel = 0;
+  for (uint32_t t = 0; t < e; ++t) {
+    rsel |= alive & (~alive + 1);
+    alive &= alive - 1;
+  }
+  uint64_t surv = (~lost & 0x3FFu) | (rsel << K);
+  const uint8_t* dg = data + g * K * P;
+  const uint8_t* pg = parity + g * R * P;
+  uint32_t toff = 1024u + lane * 4u;
+  if (toff + 4u > P) toff = P - 4u;
+  u32x4 a = {0u, 0u, 0u, 0u};
+  uint32_t t4 = 0;
+#pragma unroll
+  for (int s = 0; s < int(K); ++s) {
+    const uint32_t sid = uint32_t(__builtin_ctzll(surv));
+    surv &= surv - 1;
+    const uint8_t* src = sid < K ? dg + sid * P : pg + (sid - K) * P;
+    a ^= __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + lane * 16u));
+    t4 ^= __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(src + toff));
+  }
+  for (uint32_t i = 0; i < e; ++i) {
+    uint8_t* dst = out + (PACKED ? uint64_t(pre[g]) + i : g * R + i) * P;
+    __builtin_nontemporal_store(a, reinterpret_cast<u32x4*>(dst + lane * 16u));
+    __builtin_nontemporal_store(t4, reinterpret_cast<uint32_t*>(dst + toff));
+  }
+}
 }  // namespace
 }  // namespace qfec
 
@@ -241,6 +285,29 @@ int main(int argc, char** argv) {
                     }});
     vars.push_back({"in-place same form", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
                       return run_decode_fused<10, 3, kNtStore | kNtLoad, 1, 1, true>(a, nullptr);
+                    }});
+  }
+  // write-layout probe: the recover API's slots vs rows packed back to back (prefix sums)
+  if (k == 10 && r == 3 && P == 1200) {
+    std::vector<uint32_t> hpre(G);
+    uint32_t acc = 0;
+    for (uint64_t g = 0; g < G; ++g) {
+      hpre[g] = acc;
+      acc += uint32_t(__builtin_popcountll(hm[g] & 0x3FFu));
+    }
+    uint32_t* dpre = nullptr;
+    CK(hipMalloc(&dpre, G * 4));
+    CK(hipMemcpy(dpre, hpre.data(), G * 4, hipMemcpyHostToDevice));
+    uint8_t* wout = nullptr;
+    CK(hipMalloc(&wout, G * 3 * P));
+    const uint32_t wb = uint32_t((G + 3) / 4);
+    vars.push_back({"wr slots", kDecodeFused, -1, 1, {}, [=](const DecodeLaunch& a) {
+                      hipLaunchKernelGGL(wr_layout<0>, dim3(wb), dim3(256), 0, nullptr, a.data, a.parity, a.masks, dpre, wout, a.groups);
+                      return hipGetLastError();
+                    }});
+    vars.push_back({"wr packed", kDecodeFused, -1, 1, {}, [=](const DecodeLaunch& a) {
+                      hipLaunchKernelGGL(wr_layout<1>, dim3(wb), dim3(256), 0, nullptr, a.data, a.parity, a.masks, dpre, wout, a.groups);
+                      return hipGetLastError();
                     }});
   }
   // SCAN groups per wave (mask-addressed inline form): sparse loss without a wave per group
