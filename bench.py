@@ -445,6 +445,12 @@ def e2e_pinned(ctx, d_data, d_parity, d_masks, G: int, cfg: dict, reps: int = 3)
     return out
 
 
+def packed_supported(k: int, r: int, P: int) -> bool:
+    """Shapes with a mask-addressed (inline-classify) recover form, which the packed API needs
+    (include/fec_hip.h fec_recover_batch_rs_dev_packed)."""
+    return ((k == 10 and r <= 3) or (k == 4 and r == 2)) and 256 < P < 2048
+
+
 def lib_sha256() -> str:
     """Hash of the libfec_hip.so this process loads (the build being timed)."""
     import hashlib
@@ -484,9 +490,11 @@ def main() -> int:
                     help="k,r,P override of the config's code shape (tuning sweeps; not the headline)")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the host-resident path (pinned buffers, H2D -> kernel -> D2H)")
-    ap.add_argument("--decode-api", default="recover", choices=("recover", "in-place"),
-                    help="recover: fec_recover_batch_rs_dev (rebuilt packets returned back to back, as the "
-                         "reference decoder returns Recovered buffers); in-place: fec_decode_batch_rs_dev")
+    ap.add_argument("--decode-api", default="auto", choices=("auto", "packed", "recover", "in-place"),
+                    help="packed: fec_recover_batch_rs_dev_packed (all groups' rebuilt packets back to back, as "
+                         "the reference decoder returns its Recovered list); recover: fec_recover_batch_rs_dev "
+                         "((g*r + m)*P slots); in-place: fec_decode_batch_rs_dev; auto: packed where the shape has "
+                         "a mask-addressed form and the loss is dense, else recover")
     ap.add_argument("--null-stream", action="store_true",
                     help="launch through stream handle 0 (the context's own stream) with events on torch's "
                          "default stream, as round-1/2 benches did (A/B of the timing setup)")
@@ -553,11 +561,20 @@ def main() -> int:
     # this rank's slice of one global synthetic stream
     ctx.fill_random_dev(data, data.numel(), SEED + 2, byte_offset=g0 * k * P, stream=sp)
     dec_bytes = dec_read = 0
-    recover = cfg["decode"] and args.decode_api == "recover"
+    api = args.decode_api
+    if api == "auto":
+        # packed rows where the shape has a mask-addressed form and most groups lose data (its
+        # prefix sum costs ~10-20 us: C3 recover 2.41 vs 2.46 ms, C5's sparse loss 0.274 vs
+        # 0.266 ms, profiles/r02_packed_ab.txt), else the (g*r + m)*P slots
+        api = "packed" if packed_supported(k, r, P) and not cfg.get("loss") else "recover"
+    recover = cfg["decode"] and api in ("recover", "packed")
     rebuilt = dev_buffer(G * r * P, args.rebuilt_offset) if recover else None
+    row_start = torch.empty(G, dtype=torch.int32, device="cuda") if cfg["decode"] and api == "packed" else None
 
     def decode_call(api: str, status=None):
-        if api == "recover":
+        if api == "packed":
+            ctx.recover_packed_dev(data, parity, masks, G, k, r, P, rebuilt, row_start, None, status, stream=sp)
+        elif api == "recover":
             ctx.recover_dev(data, parity, masks, G, k, r, P, rebuilt, status, stream=sp)
         else:
             ctx.decode_dev(data, parity, masks, G, k, r, P, status, stream=sp)
@@ -585,12 +602,18 @@ def main() -> int:
             lost = ((masks.view(G, 1) >> bits.view(1, k)) & 1).bool()
             data.view(G, k, P)[lost] = 0xEE
             st = torch.zeros(G, dtype=torch.uint8, device="cuda")
-            decode_call(args.decode_api, st)
+            decode_call(api, st)
             torch.cuda.synchronize()
             bad_exp = unrecoverable_count(masks_h, k, r)
             n_bad = int(st.sum().item())
             ok_rows = st == 0
-            if recover:
+            if api == "packed":
+                # rows back to back in (g, j ascending) order: boolean indexing's order
+                want = orig.view(G, k, P)[lost & ok_rows.view(G, 1)]
+                got = rebuilt.view(-1, P)[:want.shape[0]]
+                verified = bool(torch.equal(got, want)) and n_bad == bad_exp
+                data.copy_(orig)
+            elif recover:
                 # slot m of group g = its m-th lost data shard: the same (g, j ascending) order
                 # as boolean indexing of the lost shards
                 e_g = lost.sum(dim=1, keepdim=True)
@@ -616,7 +639,7 @@ def main() -> int:
         if ev is not None:
             ev[1].record(stream)
         if cfg["decode"]:
-            decode_call(args.decode_api)
+            decode_call(api)
             if ev is not None:
                 ev[2].record(stream)
 
@@ -670,10 +693,10 @@ def main() -> int:
 
     kernels["encode"]["isolated"] = isolated(lambda: ctx.encode_dev(data, G, k, r, P, parity, stream=sp), enc_bytes)
     if cfg["decode"]:
-        kernels["decode"]["api"] = args.decode_api
-        kernels["decode"]["isolated"] = isolated(lambda: decode_call(args.decode_api), dec_bytes)
+        kernels["decode"]["api"] = api
+        kernels["decode"]["isolated"] = isolated(lambda: decode_call(api), dec_bytes)
         # the other decode API on the same buffers, for comparison (not in `value`)
-        other = "in-place" if recover else "recover"
+        other = {"packed": "recover", "recover": "in-place"}.get(api, "recover")
         if other == "recover" and rebuilt is None:
             rebuilt = dev_buffer(G * r * P, args.rebuilt_offset)
         kernels["decode"]["other_api"] = {"api": other, **isolated(lambda: decode_call(other), dec_bytes)}
@@ -721,8 +744,10 @@ def main() -> int:
             "config": {"workload": cfg["workload"], "k": k, "r": r, "packet_bytes": P,
                        "groups_per_gpu": G, "erasures_per_group": cfg["erasures"] or None,
                        "iid_loss": cfg.get("loss"),
-                       "decode_api": (("fec_recover_batch_rs_dev (rebuilt packets back to back, decoder.go Recovered)"
-                                       if args.decode_api == "recover" else "fec_decode_batch_rs_dev (in place)")
+                       "decode_api": ({"packed": "fec_recover_batch_rs_dev_packed (rebuilt packets of all groups back "
+                                                 "to back with per-group row starts, decoder.go Recovered list)",
+                                       "recover": "fec_recover_batch_rs_dev (rebuilt packets at (g*r + m)*P slots)",
+                                       "in-place": "fec_decode_batch_rs_dev (in place)"}[api]
                                       if cfg["decode"] else None),
                        "parallelism": f"group-sharded x{world} (no collective)"},
             "verified": verified,

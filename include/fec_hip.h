@@ -115,6 +115,21 @@ int fec_recover_batch_rs_dev(FECEncoderCtx* ctx, const uint8_t* d_data, const ui
  * then 0.  FEC_ERR_RANGE if k + r > 64. */
 int fec_decode_prepare(FECEncoderCtx* ctx, uint32_t k, uint32_t r, uint64_t* bytes_out);
 
+/* The same recovery with the rebuilt packets of all groups back to back ("packed"), the
+ * shape of decoder.go's Recovered list (:29-34): group g's m-th lost data shard (ascending
+ * shard id) at d_rebuilt + (d_row_start[g] + m) * packet_size, where d_row_start[g] (u32, one
+ * per group, written by the call) is the number of rows rebuilt for groups 0..g-1;
+ * unrecoverable groups and groups without lost data rebuild none.  *d_total (nullable, device)
+ * = all rows.  d_rebuilt holds at most num_groups * r rows.  No gaps between groups' rows:
+ * the stores stream like encode's parity (C5-style sparse loss: 15% faster than the slot
+ * layout in the probe, profiles/r02_probe_recover_write_layout.txt).  Mask-addressed shapes
+ * only (k + r with an inline-classify form, r <= 3, 256 < P <= 2048); others return
+ * FEC_ERR_RANGE.  Asynchronous on `stream` like the call above. */
+int fec_recover_batch_rs_dev_packed(FECEncoderCtx* ctx, const uint8_t* d_data, const uint8_t* d_parity,
+                                    const uint64_t* d_masks, uint64_t num_groups, uint32_t k, uint32_t r,
+                                    uint32_t packet_size, uint8_t* d_rebuilt, uint32_t* d_row_start,
+                                    uint64_t* d_total, uint8_t* d_status, void* stream);
+
 /* Expected share (0..1) of groups that lost data shards in this context's device-resident
  * decode calls, e.g. 1 - (1 - p)^k for iid loss p (the receiver knows its network profile;
  * satellite p = 0.01, k = 10: ~0.10).  Below 0.25 the decode checks several groups per

@@ -651,7 +651,13 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
   // destination of rebuilt row m (erased data shard `erased(m)`)
   auto dest = [&](uint32_t m, uint32_t eid) -> uint8_t* {
     if constexpr ((POL & kCompactOut) != 0) {
-      return out + (gw * r + m) * static_cast<uint64_t>(P);
+      // packed rows (fec_recover_batch_rs_dev_packed): the group's first row from its prefix
+      // sum, passed in rec_off, which the inline-classify forms do not otherwise read
+      uint64_t row = gw * r + m;
+      if constexpr (INLINE) {
+        if (rec_off != nullptr) row = static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(rec_off[gw])) + m;
+      }
+      return out + row * static_cast<uint64_t>(P);
     } else {
       return og + eid * static_cast<uint64_t>(P);
     }
@@ -938,6 +944,79 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
     }
   }
 
+}
+
+// Packed recover rows: row_start[g] = exclusive prefix sum over groups of the number of rows a
+// group rebuilds (its lost data shards when recoverable, else 0).  Three launches: block sums
+// of kRowsPerBlock groups, a one-block scan of those sums (the total rows at the end), then
+// each block's own scan plus its offset.
+constexpr uint32_t kRowsPerThread = 16;
+constexpr uint32_t kRowsPerBlock = 256 * kRowsPerThread;
+
+__device__ __forceinline__ uint32_t rebuilt_rows(uint64_t m, uint32_t k, uint32_t r) {
+  const uint64_t kmask = k >= 64 ? ~0ull : (1ull << k) - 1;
+  const uint32_t ne = static_cast<uint32_t>(__popcll(m & kmask));
+  const uint32_t pl = static_cast<uint32_t>(__popcll((m >> k) & ((1ull << r) - 1)));
+  return ne > 0 && ne + pl <= r ? ne : 0u;
+}
+
+// Inclusive scan of one value per thread over a 256-thread block (LDS, 8 steps).
+__device__ __forceinline__ uint32_t block_inclusive_scan(uint32_t v, uint32_t* lds) {
+  const uint32_t t = threadIdx.x;
+  lds[t] = v;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    const uint32_t add = t >= d ? lds[t - d] : 0u;
+    __syncthreads();
+    lds[t] += add;
+    __syncthreads();
+  }
+  return lds[t];
+}
+
+__global__ __launch_bounds__(256) void rows_block_sums(const uint64_t* __restrict__ masks, uint64_t groups, uint32_t k,
+                                                       uint32_t r, uint32_t* __restrict__ block_sums) {
+  __shared__ uint32_t lds[256];
+  const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * kRowsPerBlock + threadIdx.x * kRowsPerThread;
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < kRowsPerThread; ++i)
+    if (g0 + i < groups) sum += rebuilt_rows(masks[g0 + i], k, r);
+  const uint32_t incl = block_inclusive_scan(sum, lds);
+  if (threadIdx.x == 255) block_sums[blockIdx.x] = incl;
+}
+
+// One block: block_sums[0, nb) -> exclusive prefix sums, in place; *total = the sum.
+__global__ __launch_bounds__(256) void rows_scan_blocks(uint32_t* __restrict__ block_sums, uint32_t nb,
+                                                        uint64_t* __restrict__ total) {
+  __shared__ uint32_t lds[256];
+  uint32_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint32_t v = i < nb ? block_sums[i] : 0u;
+    const uint32_t incl = block_inclusive_scan(v, lds);
+    if (i < nb) block_sums[i] = carry + incl - v;
+    carry += lds[255];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && total != nullptr) *total = carry;
+}
+
+__global__ __launch_bounds__(256) void rows_write(const uint64_t* __restrict__ masks, uint64_t groups, uint32_t k,
+                                                  uint32_t r, const uint32_t* __restrict__ block_offsets,
+                                                  uint32_t* __restrict__ row_start) {
+  __shared__ uint32_t lds[256];
+  const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * kRowsPerBlock + threadIdx.x * kRowsPerThread;
+  uint32_t rows[kRowsPerThread];
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < kRowsPerThread; ++i) {
+    rows[i] = g0 + i < groups ? rebuilt_rows(masks[g0 + i], k, r) : 0u;
+    sum += rows[i];
+  }
+  uint32_t at = block_offsets[blockIdx.x] + block_inclusive_scan(sum, lds) - sum;
+  for (uint32_t i = 0; i < kRowsPerThread; ++i) {
+    if (g0 + i < groups) row_start[g0 + i] = at;
+    at += rows[i];
+  }
 }
 
 // One wave per group, so the record is wave-uniform (SGPRs).  A packet is covered by
@@ -1599,6 +1678,22 @@ bool decode_compact_tables(const DecodeLaunch& a) {
   if (a.variant != kDecodeFused && a.variant != kDecodeAuto && a.variant != kDecodeFusedDirect) return false;
   const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
   return a.k == 20 && a.r == 5 && ((nm == 0 && nt >= 1) || nm == 1);  // QFEC_FUSED_P's (nm, nt)
+}
+
+uint64_t rows_prefix_workspace_bytes(uint64_t groups) {
+  return ((groups + kRowsPerBlock - 1) / kRowsPerBlock) * sizeof(uint32_t);
+}
+
+hipError_t launch_rows_prefix(const uint64_t* masks, uint64_t groups, uint32_t k, uint32_t r, uint32_t* row_start,
+                              uint32_t* block_sums, uint64_t* total, hipStream_t s) {
+  if (groups == 0) return hipSuccess;
+  const uint64_t nb = (groups + kRowsPerBlock - 1) / kRowsPerBlock;
+  if (nb > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rows_block_sums, dim3(static_cast<uint32_t>(nb)), dim3(256), 0, s, masks, groups, k, r, block_sums);
+  hipLaunchKernelGGL(rows_scan_blocks, dim3(1), dim3(256), 0, s, block_sums, static_cast<uint32_t>(nb), total);
+  hipLaunchKernelGGL(rows_write, dim3(static_cast<uint32_t>(nb)), dim3(256), 0, s, masks, groups, k, r, block_sums,
+                     row_start);
+  return hipGetLastError();
 }
 
 hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {

@@ -104,6 +104,12 @@ constexpr int kDecodeWaveXcdSwizzle = 1;
 
 hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s);
 hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s);
+// Packed recover rows: row_start[g] = exclusive prefix sum of the rows each group rebuilds
+// (lost data shards when recoverable, else 0); *total (nullable) = all rows.  block_sums:
+// rows_prefix_workspace_bytes(groups) of device workspace.
+uint64_t rows_prefix_workspace_bytes(uint64_t groups);
+hipError_t launch_rows_prefix(const uint64_t* masks, uint64_t groups, uint32_t k, uint32_t r, uint32_t* row_start,
+                              uint32_t* block_sums, uint64_t* total, hipStream_t s);
 // Whether launch_decode(a) uses the rec_off workspace (every form but the mask-addressed
 // one, which classifies inline).  The caller then provides a workspace private to the call.
 bool decode_needs_rec_off(const DecodeLaunch& a);

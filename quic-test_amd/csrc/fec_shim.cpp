@@ -494,7 +494,8 @@ hipError_t stream_workspace(FECEncoderCtx* ctx, hipStream_t s, size_t bytes, voi
 int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_parity,
                       const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
                       uint8_t* d_status, hipStream_t s, DevBuf* rec = nullptr,
-                      uint8_t* d_out = nullptr, double need_share = -1.0, bool compact_out = false) {
+                      uint8_t* d_out = nullptr, double need_share = -1.0, bool compact_out = false,
+                      uint32_t* row_start = nullptr) {
   DecodePlan* plan = nullptr;
   int rc = get_decode_plan(ctx, k, r, &plan);
   if (rc != FEC_OK) return rc;
@@ -546,9 +547,18 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   if (need_share < 0.0) need_share = ctx->decode_need_share;
   if (need_share >= 0.0 && need_share < qfec::kDecodeScanMaxShare) a.scan = qfec::kDecodeScanGroups;
   if (const char* v = std::getenv("QUICFEC_DECODE_SCAN")) a.scan = static_cast<uint32_t>(std::atoi(v));
+  if (row_start != nullptr) {
+    // packed rows: only the mask-addressed (inline-classify) forms place rows by row_start,
+    // which they read from rec_off
+    if (!plan->dense || qfec::decode_needs_rec_off(a)) {
+      set_error("packed recover: no mask-addressed form for k=%u r=%u P=%u (use fec_recover_batch_rs_dev)", k, r, P);
+      return FEC_ERR_RANGE;
+    }
+    a.rec_off = row_start;
+  }
   // Workspace: the caller's slot buffer (pipeline slots: private stream, calls serialised
   // by the context lock), else one private to this call.
-  if (!plan->dense || qfec::decode_needs_rec_off(a)) {
+  if (row_start == nullptr && (!plan->dense || qfec::decode_needs_rec_off(a))) {
     if (rec) {
       QFEC_HIP(rec->ensure(G * sizeof(uint32_t)));
       a.rec_off = rec->as<uint32_t>();
@@ -1403,6 +1413,47 @@ static int fec_recover_batch_rs_dev_impl(FECEncoderCtx* ctx, const uint8_t* d_da
   // the kernels only read `data` when the output is compact
   return decode_dev_locked(ctx, const_cast<uint8_t*>(d_data), d_parity, d_masks, G, k, r, P, d_status,
                            pick_stream(ctx, stream), nullptr, d_rebuilt, -1.0, /*compact_out=*/true);
+}
+
+static int fec_recover_batch_rs_dev_packed_impl(FECEncoderCtx* ctx, const uint8_t* d_data, const uint8_t* d_parity,
+                                                const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r,
+                                                uint32_t P, uint8_t* d_rebuilt, uint32_t* d_row_start,
+                                                uint64_t* d_total, uint8_t* d_status, void* stream) {
+  if (!ctx || !d_data || !d_parity || !d_masks || !d_rebuilt || !d_row_start) return FEC_ERR_NULL;
+  int rc = check_shape(G, k, r, P, true);
+  if (rc != FEC_OK) return rc;
+  if (G * r >= (1ull << 32)) {
+    set_error("packed recover: %llu groups x %u rows exceed 32-bit row indices", static_cast<unsigned long long>(G), r);
+    return FEC_ERR_RANGE;
+  }
+  if (G == 0) {
+    if (d_total) {
+      std::lock_guard<std::mutex> lk(ctx->mu);
+      DeviceGuard dg(ctx->device);
+      if (!dg.ok) return FEC_ERR_NODEV;
+      QFEC_HIP(hipMemsetAsync(d_total, 0, sizeof(uint64_t), pick_stream(ctx, stream)));
+    }
+    return FEC_OK;
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return FEC_ERR_NODEV;
+  const hipStream_t s = pick_stream(ctx, stream);
+  // block sums of the prefix scan: the stream's workspace (no record offsets on this path)
+  void* ws = nullptr;
+  QFEC_HIP(stream_workspace(ctx, s, qfec::rows_prefix_workspace_bytes(G), &ws));
+  QFEC_HIP(qfec::launch_rows_prefix(d_masks, G, k, r, d_row_start, static_cast<uint32_t*>(ws), d_total, s));
+  return decode_dev_locked(ctx, const_cast<uint8_t*>(d_data), d_parity, d_masks, G, k, r, P, d_status, s, nullptr,
+                           d_rebuilt, -1.0, /*compact_out=*/true, d_row_start);
+}
+
+QFEC_EXPORT int fec_recover_batch_rs_dev_packed(FECEncoderCtx* ctx, const uint8_t* d_data, const uint8_t* d_parity,
+                                                const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r,
+                                                uint32_t P, uint8_t* d_rebuilt, uint32_t* d_row_start,
+                                                uint64_t* d_total, uint8_t* d_status, void* stream) {
+  g_last_error.clear();
+  return record_ctx_error(ctx, fec_recover_batch_rs_dev_packed_impl(ctx, d_data, d_parity, d_masks, G, k, r, P, d_rebuilt,
+                                                                    d_row_start, d_total, d_status, stream));
 }
 
 QFEC_EXPORT int fec_recover_batch_rs_dev(FECEncoderCtx* ctx, const uint8_t* d_data, const uint8_t* d_parity,

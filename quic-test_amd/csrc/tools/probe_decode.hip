@@ -281,6 +281,7 @@ int main(int argc, char** argv) {
     vars.push_back({"compact-out", kDecodeFused, -1, 1, {}, [cout](const DecodeLaunch& a) {
                       DecodeLaunch b = a;
                       b.out = cout;
+                      b.rec_off = nullptr;  // the inline forms read packed row starts from rec_off
                       return run_decode_fused<10, 3, kNtStore | kNtLoad | kCompactOut, 1, 1, true>(b, nullptr);
                     }});
     vars.push_back({"in-place same form", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
@@ -329,6 +330,7 @@ int main(int argc, char** argv) {
     vars.push_back({"scan8 compact-out", kDecodeFused, -1, 1, {}, [cout](const DecodeLaunch& a) {
                       DecodeLaunch b = a;
                       b.out = cout;
+                      b.rec_off = nullptr;  // the inline forms read packed row starts from rec_off
                       return run_decode_fused<10, 3, kNtStore | kNtLoad | kCompactOut, 1, 1, true, true, 8>(b, nullptr);
                     }});
   }

@@ -50,6 +50,7 @@ HIP_SYMBOLS = (
     "fec_batcher_wait", "fec_batcher_flush", "fec_batcher_stats", "fec_batcher_last_error",
     "fec_batcher_new_decoder", "fec_batcher_submit_shards", "fec_batcher_wait_rebuilt",
     "fec_batcher_new_multi", "fec_batcher_new_decoder_multi", "fec_batcher_devices",
+    "fec_recover_batch_rs_dev_packed",
 )
 
 
@@ -137,6 +138,8 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
         "fec_batcher_new_multi": (_vp, [_vp, _int, _u32, _u32, _u32, _u32, _u32, _u32]),
         "fec_batcher_new_decoder_multi": (_vp, [_vp, _int, _u32, _u32, _u32, _u32, _u32, _u32]),
         "fec_batcher_devices": (_int, [_vp]),
+        "fec_recover_batch_rs_dev_packed": (_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _u32, _u32, _u32, _vp, _vp,
+                                                   _vp, _vp, _vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -272,6 +275,18 @@ class Context:
                                                num_groups, k, r, packet_size, _ptr(d_rebuilt),
                                                _ptr(d_status) if d_status is not None else None, stream)
         _check(rc, "fec_recover_batch_rs_dev")
+
+    def recover_packed_dev(self, d_data, d_parity, d_masks, num_groups: int, k: int, r: int, packet_size: int,
+                           d_rebuilt, d_row_start, d_total=None, d_status=None, stream: Optional[int] = None) -> None:
+        """Rebuilt shards of all groups back to back: group g's m-th lost data shard at row
+        d_row_start[g] + m of d_rebuilt (u32 row starts written by the call); d_total (one u64,
+        nullable) = all rows.  Mask-addressed shapes only."""
+        rc = self.lib.fec_recover_batch_rs_dev_packed(self.handle, _ptr(d_data), _ptr(d_parity), _ptr(d_masks),
+                                                      num_groups, k, r, packet_size, _ptr(d_rebuilt),
+                                                      _ptr(d_row_start),
+                                                      _ptr(d_total) if d_total is not None else None,
+                                                      _ptr(d_status) if d_status is not None else None, stream)
+        _check(rc, "fec_recover_batch_rs_dev_packed")
 
     def decode_prepare(self, k: int, r: int) -> int:
         n = ctypes.c_uint64(0)

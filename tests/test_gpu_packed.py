@@ -1,0 +1,104 @@
+"""fec_recover_batch_rs_dev_packed: the rebuilt packets of all groups back to back (the shape of
+decoder.go's Recovered list, :29-34), group g's rows starting at row_start[g] = the rows rebuilt
+for groups 0..g-1.  Bit-exact against the oracle, row starts against a host prefix sum, the
+total, statuses, `data` untouched; one wave per group and the sparse-loss scan form; prefix
+sums across many 4096-group scan blocks; unsupported shapes refused."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED5000
+
+
+def _dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+
+
+def _case(oracle_mod, k, r, P, G, masks):
+    data = oracle_mod.splitmix_bytes(G * k * P, SEED + k * 31 + r * 7 + P)
+    par = oracle_mod.rs_encode(data, G, k, r, P, nthreads=8)
+    lost = ((masks[:, None] >> np.arange(k, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+    broken = data.copy().reshape(G, k, P)
+    broken[lost] = 0xEE
+    ref = broken.copy().reshape(-1)
+    _, st_exp = oracle_mod.rs_decode(ref, par, masks, G, k, r, P, nthreads=8)
+    ok = st_exp == 0
+    rows = np.where(ok, lost.sum(axis=1), 0).astype(np.int64)
+    start = np.concatenate([[0], np.cumsum(rows)[:-1]]).astype(np.uint32)
+    exp = ref.reshape(G, k, P)[lost & ok[:, None]]          # (g, j ascending) order
+    return broken.reshape(-1), par, st_exp, start, exp
+
+
+def _run(gpu_ctx, torch, broken, par, masks, G, k, r, P):
+    dd, dp, dm = _dev(torch, broken), _dev(torch, par), _dev(torch, masks.view(np.int64))
+    out = torch.full((max(1, G * r) * P,), 0x5A, dtype=torch.uint8, device="cuda")
+    rs = torch.full((max(1, G),), 0x7FFFFFFF, dtype=torch.int32, device="cuda")
+    tot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    st = torch.full((max(1, G),), 7, dtype=torch.uint8, device="cuda")
+    gpu_ctx.recover_packed_dev(dd, dp, dm, G, k, r, P, out, rs, tot, st)
+    gpu_ctx.synchronize()
+    return dd, out, rs, tot, st
+
+
+@pytest.mark.parametrize("k,r,P", [(10, 3, 1200), (10, 3, 700), (10, 3, 1400), (10, 3, 2000), (10, 3, 300),
+                                   (10, 1, 1200), (10, 2, 1200), (10, 2, 700), (4, 2, 1200), (4, 2, 513)])
+def test_packed_rows_match_oracle(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
+    G = 1031
+    rng = np.random.default_rng(k * 1000 + r * 100 + P)
+    masks = np.zeros(G, dtype=np.uint64)
+    for g in range(G):
+        for s in rng.permutation(k + r)[: rng.integers(0, r + 2)]:
+            masks[g] |= np.uint64(1) << np.uint64(int(s))
+    broken, par, st_exp, start, exp = _case(oracle_mod, k, r, P, G, masks)
+    dd, out, rs, tot, st = _run(gpu_ctx, torch_cuda, broken, par, masks, G, k, r, P)
+    n = len(exp)
+    assert int(tot.item()) == n
+    assert np.array_equal(rs.cpu().numpy().view(np.uint32), start)
+    assert np.array_equal(st.cpu().numpy(), st_exp)
+    o = out.cpu().numpy().reshape(G * r, P)
+    assert np.array_equal(o[:n], exp)
+    assert (o[n:] == 0x5A).all()                                   # nothing past the last row
+    assert np.array_equal(dd.cpu().numpy(), broken)                # data untouched
+
+
+@pytest.mark.parametrize("loss,G,scan", [(0.01, 50_000, "8"), (0.3, 20_011, "8"), (0.05, 30_000, None)])
+def test_packed_rows_sparse_and_many_blocks(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, loss, G, scan):
+    """iid loss (the scan form when QUICFEC_DECODE_SCAN=8), row starts across many prefix
+    blocks of 4096 groups."""
+    if scan:
+        monkeypatch.setenv("QUICFEC_DECODE_SCAN", scan)
+    k, r, P = 10, 3, 1200
+    rng = np.random.default_rng(int(loss * 1000) + G)
+    w = np.left_shift(np.uint64(1), np.arange(k + r, dtype=np.uint64))
+    masks = ((rng.random((G, k + r)) < loss) * w).sum(axis=1, dtype=np.uint64)
+    broken, par, st_exp, start, exp = _case(oracle_mod, k, r, P, G, masks)
+    dd, out, rs, tot, st = _run(gpu_ctx, torch_cuda, broken, par, masks, G, k, r, P)
+    n = len(exp)
+    assert int(tot.item()) == n
+    assert np.array_equal(rs.cpu().numpy().view(np.uint32), start)
+    assert np.array_equal(st.cpu().numpy(), st_exp)
+    assert np.array_equal(out.cpu().numpy().reshape(G * r, P)[:n], exp)
+
+
+def test_packed_refusals_and_empty(gpu_ctx, quicfec_mod, torch_cuda):
+    torch = torch_cuda
+    # shapes without a mask-addressed form: record-addressed k=20 r=5, tiled P <= 256, P > 2048
+    for k, r, P in ((20, 5, 1200), (10, 3, 200), (10, 3, 3000), (6, 3, 1200)):
+        G = 4
+        d = torch.zeros(G * k * P, dtype=torch.uint8, device="cuda")
+        p = torch.zeros(G * r * P, dtype=torch.uint8, device="cuda")
+        m = torch.ones(G, dtype=torch.int64, device="cuda")
+        out = torch.full((G * r * P,), 0x5A, dtype=torch.uint8, device="cuda")
+        rs = torch.zeros(G, dtype=torch.int32, device="cuda")
+        with pytest.raises(quicfec_mod.FecError) as ei:
+            gpu_ctx.recover_packed_dev(d, p, m, G, k, r, P, out, rs)
+        assert ei.value.code == quicfec_mod.FEC_ERR_RANGE, (k, r, P)
+        gpu_ctx.synchronize()
+        assert bool((out == 0x5A).all())
+    # no groups: the total is 0
+    z = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    tot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    gpu_ctx.recover_packed_dev(z, z, z, 0, 10, 3, 1200, z, z, tot)
+    gpu_ctx.synchronize()
+    assert int(tot.item()) == 0
