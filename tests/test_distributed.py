@@ -119,3 +119,16 @@ def test_shard_range_single():
     import bench
     assert bench.shard_range(10, 0, 1) == (0, 10)
     assert bench.shard_range(0, 0, 4) == (0, 0)
+
+
+def test_bench_decode_api_shapes():
+    """bench.py's packed-recover shape rule mirrors the library's mask-addressed forms
+    (fec_kernels.hip try_decode_fused QFEC_FUSED_DS / _D; tests/test_gpu_packed.py checks the
+    library refuses the rest)."""
+    import bench
+    assert bench.packed_supported(10, 3, 1200) and bench.packed_supported(10, 1, 700)
+    assert bench.packed_supported(10, 2, 1400) and bench.packed_supported(4, 2, 513)
+    assert not bench.packed_supported(20, 5, 1200)      # record-addressed LDS-table form
+    assert not bench.packed_supported(10, 3, 200)       # tiled form (P <= 256)
+    assert not bench.packed_supported(10, 3, 2048)      # no fused piece layout past 2047 B
+    assert not bench.packed_supported(6, 3, 1200)       # runtime-k wave kernel
