@@ -494,7 +494,7 @@ def main() -> int:
                     help="packed: fec_recover_batch_rs_dev_packed (all groups' rebuilt packets back to back, as "
                          "the reference decoder returns its Recovered list); recover: fec_recover_batch_rs_dev "
                          "((g*r + m)*P slots); in-place: fec_decode_batch_rs_dev; auto: packed where the shape has "
-                         "a mask-addressed form and the loss is dense, else recover")
+                         "a mask-addressed form, else recover")
     ap.add_argument("--null-stream", action="store_true",
                     help="launch through stream handle 0 (the context's own stream) with events on torch's "
                          "default stream, as round-1/2 benches did (A/B of the timing setup)")
@@ -563,10 +563,10 @@ def main() -> int:
     dec_bytes = dec_read = 0
     api = args.decode_api
     if api == "auto":
-        # packed rows where the shape has a mask-addressed form and most groups lose data (its
-        # prefix sum costs ~10-20 us: C3 recover 2.41 vs 2.46 ms, C5's sparse loss 0.274 vs
-        # 0.266 ms, profiles/r02_packed_ab.txt), else the (g*r + m)*P slots
-        api = "packed" if packed_supported(k, r, P) and not cfg.get("loss") else "recover"
+        # packed rows where the shape has a mask-addressed form (C3 recover 2.39 vs 2.42 ms, C5's
+        # sparse loss 0.263 vs 0.267 ms with the two-launch prefix sum,
+        # profiles/r02_packed_ab2.txt), else the (g*r + m)*P slots
+        api = "packed" if packed_supported(k, r, P) else "recover"
     recover = cfg["decode"] and api in ("recover", "packed")
     rebuilt = dev_buffer(G * r * P, args.rebuilt_offset) if recover else None
     row_start = torch.empty(G, dtype=torch.int32, device="cuda") if cfg["decode"] and api == "packed" else None

@@ -2,7 +2,8 @@
 decoder.go's Recovered list, :29-34), group g's rows starting at row_start[g] = the rows rebuilt
 for groups 0..g-1.  Bit-exact against the oracle, row starts against a host prefix sum, the
 total, statuses, `data` untouched; one wave per group and the sparse-loss scan form; prefix
-sums across many 4096-group scan blocks; unsupported shapes refused."""
+sums across many 1024-group scan blocks (both prefix forms), masks at an 8-B-aligned address;
+unsupported shapes refused."""
 import numpy as np
 import pytest
 
@@ -62,12 +63,17 @@ def test_packed_rows_match_oracle(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
     assert np.array_equal(dd.cpu().numpy(), broken)                # data untouched
 
 
-@pytest.mark.parametrize("loss,G,scan", [(0.01, 50_000, "8"), (0.3, 20_011, "8"), (0.05, 30_000, None)])
-def test_packed_rows_sparse_and_many_blocks(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, loss, G, scan):
+@pytest.mark.parametrize("loss,G,scan,direct", [(0.01, 50_000, "8", None), (0.3, 20_011, "8", None),
+                                                (0.05, 30_000, None, None), (0.05, 30_001, None, "4"),
+                                                (0.3, 9_000, "8", "1")])
+def test_packed_rows_sparse_and_many_blocks(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, loss, G, scan, direct):
     """iid loss (the scan form when QUICFEC_DECODE_SCAN=8), row starts across many prefix
-    blocks of 4096 groups."""
+    blocks of 1024 groups, in the two-launch form and (QUICFEC_ROWS_DIRECT_BLOCKS below the
+    block count) the one with a separate scan of the block sums."""
     if scan:
         monkeypatch.setenv("QUICFEC_DECODE_SCAN", scan)
+    if direct:
+        monkeypatch.setenv("QUICFEC_ROWS_DIRECT_BLOCKS", direct)
     k, r, P = 10, 3, 1200
     rng = np.random.default_rng(int(loss * 1000) + G)
     w = np.left_shift(np.uint64(1), np.arange(k + r, dtype=np.uint64))
@@ -102,3 +108,26 @@ def test_packed_refusals_and_empty(gpu_ctx, quicfec_mod, torch_cuda):
     gpu_ctx.recover_packed_dev(z, z, z, 0, 10, 3, 1200, z, z, tot)
     gpu_ctx.synchronize()
     assert int(tot.item()) == 0
+
+
+def test_packed_masks_at_odd_word(gpu_ctx, oracle_mod, torch_cuda):
+    """The prefix kernels read four masks per load: a mask array starting one u64 into an
+    allocation (8-B aligned only) gives the same rows."""
+    torch = torch_cuda
+    k, r, P, G = 10, 3, 700, 5_003
+    rng = np.random.default_rng(77)
+    w = np.left_shift(np.uint64(1), np.arange(k + r, dtype=np.uint64))
+    masks = ((rng.random((G, k + r)) < 0.1) * w).sum(axis=1, dtype=np.uint64)
+    broken, par, st_exp, start, exp = _case(oracle_mod, k, r, P, G, masks)
+    dd, dp = _dev(torch, broken), _dev(torch, par)
+    dm_all = _dev(torch, np.concatenate([[np.uint64(0)], masks]).view(np.int64))
+    dm = dm_all[1:]
+    out = torch.full((G * r * P,), 0x5A, dtype=torch.uint8, device="cuda")
+    rs = torch.zeros(G, dtype=torch.int32, device="cuda")
+    tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+    gpu_ctx.recover_packed_dev(dd, dp, dm, G, k, r, P, out, rs, tot)
+    gpu_ctx.synchronize()
+    n = len(exp)
+    assert int(tot.item()) == n
+    assert np.array_equal(rs.cpu().numpy().view(np.uint32), start)
+    assert np.array_equal(out.cpu().numpy().reshape(G * r, P)[:n], exp)
