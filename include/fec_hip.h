@@ -265,6 +265,27 @@ int fec_batcher_stats(FECBatcher* b, FECBatcherStats* out);
 /* Message of the calling thread's last failing fec_batcher_* call. */
 const char* fec_batcher_last_error(void);
 
+/* ---- legacy-call coalescing (fec_coalesce.cpp) ----
+ * The reference's unchanged call site encodes one group per fec_encode_batch call, each stream
+ * on its own context (encoder_hybrid.go:115 via fec_cgo.go:138, client.go:783).  Host-resident
+ * legacy calls of at most QUICFEC_COALESCE_MAX_GROUPS groups (default 64) are joined, across
+ * every context of the process, into shared launches on their device: a caller records its
+ * packets' addresses (page-locked slabs are read in place, pageable ones copied to page-locked
+ * staging), the first caller to find no launch slot busy closes the batch and launches it
+ * (group commit: no flusher thread, so a lone caller pays no hand-off), and every caller gets
+ * its own repair rows back with the legacy return codes (fec_xor_simd.cpp:556-594).
+ * QUICFEC_COALESCE=0 turns it off (one launch and synchronize per call on the caller's context). */
+typedef struct {
+  uint64_t calls;      /* legacy calls that went through the coalescer */
+  uint64_t groups;     /* their groups */
+  uint64_t batches;    /* launches */
+  uint64_t max_batch;  /* groups in the largest launch */
+  uint64_t max_calls;  /* calls in the largest launch */
+} FECCoalesceStats;
+
+/* Process-wide totals over every device and packet size; reset = 1 zeroes them after the read. */
+int fec_coalesce_stats(FECCoalesceStats* out, int reset);
+
 #ifdef __cplusplus
 }
 #endif

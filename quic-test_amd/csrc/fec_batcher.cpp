@@ -181,8 +181,12 @@ struct FECBatcher {
   // free one (or none).  Caller holds mu.
   void close_open(bool full) {
     const int si = open.load(std::memory_order_relaxed);
-    if (si < 0 || !slabs[si]->started) return;
+    if (si < 0) return;
     Slab& s = *slabs[si];
+    // A slab closes once its first group has started the deadline or, when full, as soon as
+    // every slot is reserved: the first reserver records its start under mu only after its
+    // lock-free reservation, and a full slab must not wait out the deadline meanwhile.
+    if (!s.started && !(full && (s.state.load(std::memory_order_acquire) & ~kClosed) >= max_groups)) return;
     const uint64_t old = s.state.fetch_or(kClosed, std::memory_order_acq_rel);
     s.n = static_cast<uint32_t>(std::min<uint64_t>(old & ~kClosed, max_groups));
     next_base = s.base + s.n;
@@ -584,11 +588,13 @@ int reserve(FECBatcher* b, Slot* out) {
     }
     b->cv_free.wait(lk);  // open_slab notifies; spurious wake-ups retry
   }
-  if (out->g == 0) {  // a deadline starts
+  if (out->g == 0) {  // a deadline starts (unless the slab filled and closed meanwhile)
     std::lock_guard<std::mutex> lk(b->mu);
-    out->s->t_first = Clock::now();
-    out->s->started = true;
-    b->cv_flusher.notify_one();
+    if (!(out->s->state.load(std::memory_order_acquire) & kClosed)) {
+      out->s->t_first = Clock::now();
+      out->s->started = true;
+      b->cv_flusher.notify_one();
+    }
   }
   return FEC_OK;
 }

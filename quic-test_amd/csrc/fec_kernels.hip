@@ -177,8 +177,10 @@ __device__ __forceinline__ const uint8_t* packet_ptr(const uint8_t* data, const 
     return data + (g * k + j) * static_cast<uint64_t>(P);
   } else if constexpr (OFF == 1) {
     return data + static_cast<const uint32_t*>(offsets)[g * k + j];
-  } else {
+  } else if constexpr (OFF == 2) {
     return data + static_cast<const uint64_t*>(offsets)[g * k + j];
+  } else {  // absolute packet addresses (OffsetKind::kAddr)
+    return reinterpret_cast<const uint8_t*>(static_cast<const uint64_t*>(offsets)[g * k + j]);
   }
 }
 
@@ -953,6 +955,8 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
 // the sums runs in between.  rocprof at C5 (1M groups): the first form with 4096-group blocks
 // took 23 us in three launches (rows_write 11.5, block sums 6.9, one-block scan 4.9).
 constexpr uint32_t kRowsPerThread = 4;
+// thread_rows loads the masks as one u64x4 and the scans add rows[0..3]
+static_assert(kRowsPerThread == 4, "thread_rows and the rows_* kernels are written for 4 groups per thread");
 constexpr uint32_t kRowsPerBlock = 256 * kRowsPerThread;
 constexpr uint32_t kRowsDirectBlocks = 4096;
 
@@ -1354,6 +1358,13 @@ constexpr uint32_t kMaxThreadsPerLaunch = 1u << 30;
 // Wave-per-group decode launches: 256-thread workgroups, so at most 2^22 of them keep the
 // grid's work-item count (blocks * 256) inside 32 bits with room to spare.
 constexpr uint64_t kMaxWaveBlocks = kMaxThreadsPerLaunch / 256u;
+// Blocks per wave-per-group decode launch: kMaxWaveBlocks, or QUICFEC_MAX_WAVE_BLOCKS (tests
+// force the chunked launches, which otherwise start only past 16.7M groups).
+uint64_t max_wave_blocks() {  // read per launch: tests switch it inside one process
+  const char* e = std::getenv("QUICFEC_MAX_WAVE_BLOCKS");
+  const long long n = e && *e ? std::atoll(e) : 0;
+  return n > 0 && static_cast<uint64_t>(n) < kMaxWaveBlocks ? static_cast<uint64_t>(n) : kMaxWaveBlocks;
+}
 constexpr uint32_t kVecMinP = 16;  // shorter packets take the byte kernels
 
 inline uint32_t blocks_for(uint64_t n) { return static_cast<uint32_t>((n + 255) / 256); }
@@ -1506,6 +1517,8 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
       if (a.k == 10 && a.r == 2 && !rt_k) return run_encode_v16<10, 2, 0, true, kNtStore | kPairMac>(a, 0, s);
     } else if (a.off_kind == OffsetKind::kU32) {
       if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 1, true>(a, 0, s);
+    } else if (a.off_kind == OffsetKind::kAddr) {
+      if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 3, true>(a, 0, s);
     }
   }
   switch (a.off_kind) {
@@ -1513,8 +1526,10 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
       return run_encode_generic<0>(a, s);
     case OffsetKind::kU32:
       return run_encode_generic<1>(a, s);
-    default:
+    case OffsetKind::kU64:
       return run_encode_generic<2>(a, s);
+    default:
+      return run_encode_generic<3>(a, s);
   }
 }
 
@@ -1527,13 +1542,14 @@ hipError_t run_decode_v16(const DecodeLaunch& a, hipStream_t s) {
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t m0 = p * MAXE;
     const uint64_t blocks = (a.groups + 3) / 4;
-    for (uint64_t b0 = 0; b0 < blocks; b0 += kMaxWaveBlocks) {
-      const uint64_t bn = (blocks - b0 < kMaxWaveBlocks) ? blocks - b0 : kMaxWaveBlocks;
+    const uint64_t max_blocks = max_wave_blocks();
+    for (uint64_t b0 = 0; b0 < blocks; b0 += max_blocks) {
+      const uint64_t bn = (blocks - b0 < max_blocks) ? blocks - b0 : max_blocks;
       const uint64_t g0 = b0 * 4;
       const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
       hipLaunchKernelGGL((decode_v16<K, MAXE>), dim3(static_cast<uint32_t>(bn)), dim3(256), 0, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
-                         a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook,
+                         a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off ? a.rec_off + g0 : nullptr, a.codebook,
                          gn, cpp, a.P, a.k, a.r, m0);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
@@ -1553,13 +1569,14 @@ hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
     const uint32_t slice = (POL & kLdsTabs) != 0 ? (rows * a.k * 2u + 63u) / 64u * 1024u : 0u;
     const uint32_t smem = cap > 4 * slice ? cap : 4 * slice;
     const uint64_t blocks = (a.groups + 3) / 4;
-    for (uint64_t b0 = 0; b0 < blocks; b0 += kMaxWaveBlocks) {
-      const uint64_t bn = (blocks - b0 < kMaxWaveBlocks) ? blocks - b0 : kMaxWaveBlocks;
+    const uint64_t max_blocks = max_wave_blocks();
+    for (uint64_t b0 = 0; b0 < blocks; b0 += max_blocks) {
+      const uint64_t bn = (blocks - b0 < max_blocks) ? blocks - b0 : max_blocks;
       const uint64_t g0 = b0 * 4;
       const uint64_t gn = (a.groups - g0 < bn * 4) ? a.groups - g0 : bn * 4;
       hipLaunchKernelGGL((decode_wave<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
-                         a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
+                         a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off ? a.rec_off + g0 : nullptr, a.codebook, gn, a.P,
                          a.k, a.r, m0, (a.out ? a.out : a.data) + g0 * ((POL & kCompactOut) != 0 ? a.r : a.k) * static_cast<uint64_t>(a.P), 0u,
                          decode_swizzle(a, kDecodeWaveXcdSwizzle), slice);
       const hipError_t e = hipGetLastError();
@@ -1580,18 +1597,24 @@ hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
     rm.stride[e] = a.meta.stride[e];
     rm.count_r[e] = a.meta.count_r[e];
   }
+  // Output of the chunk starting at group g0: packed rows are placed by their global row
+  // start (rec_off), so every chunk gets the base; the other layouts are offset per chunk.
+  auto out_at = [&](uint64_t g0) -> uint8_t* {
+    if (a.packed_rows) return a.out;
+    return (a.out ? a.out : a.data) + g0 * ((POL & kCompactOut) != 0 ? a.r : a.k) * static_cast<uint64_t>(a.P);
+  };
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t m0 = p * MAXE;
     const uint64_t blocks = (a.groups + kGroupsPerBlock - 1) / kGroupsPerBlock;
-    for (uint64_t b0 = 0; b0 < blocks; b0 += kMaxWaveBlocks) {
-      const uint64_t bn = (blocks - b0 < kMaxWaveBlocks) ? blocks - b0 : kMaxWaveBlocks;
+    const uint64_t max_blocks = max_wave_blocks();
+    for (uint64_t b0 = 0; b0 < blocks; b0 += max_blocks) {
+      const uint64_t bn = (blocks - b0 < max_blocks) ? blocks - b0 : max_blocks;
       const uint64_t g0 = b0 * kGroupsPerBlock;
       const uint64_t gn = (a.groups - g0 < bn * kGroupsPerBlock) ? a.groups - g0 : bn * kGroupsPerBlock;
       hipLaunchKernelGGL((decode_fused<K, MAXE, POL, NM, NT, DIRECT, INLINE, SCAN>), dim3(static_cast<uint32_t>(bn)), dim3(256), smem, s,
                          a.data + g0 * a.k * static_cast<uint64_t>(a.P),
-                         a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, a.P,
-                         a.r, m0, (a.out ? a.out : a.data) + g0 * ((POL & kCompactOut) != 0 ? a.r : a.k) * static_cast<uint64_t>(a.P), 0u,
-                         decode_swizzle(a, kDecodeFusedXcdSwizzle), DIRECT ? a.masks + g0 : nullptr, rm,
+                         a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off ? a.rec_off + g0 : nullptr, a.codebook, gn, a.P,
+                         a.r, m0, out_at(g0), 0u, decode_swizzle(a, kDecodeFusedXcdSwizzle), DIRECT ? a.masks + g0 : nullptr, rm,
                          INLINE && a.status ? a.status + g0 : nullptr);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
@@ -1674,7 +1697,7 @@ hipError_t run_decode_tiled(const DecodeLaunch& a, uint32_t tile, hipStream_t s)
     const uint64_t gn = (a.groups - g0 < bn * tile) ? a.groups - g0 : bn * tile;
     hipLaunchKernelGGL((decode_tiled<K, MAXE, POL>), dim3(static_cast<uint32_t>(bn)), dim3(bs), 0, s,
                        a.data + g0 * a.k * static_cast<uint64_t>(a.P),
-                       a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off + g0, a.codebook, gn, cpp,
+                       a.parity + g0 * a.r * static_cast<uint64_t>(a.P), a.rec_off ? a.rec_off + g0 : nullptr, a.codebook, gn, cpp,
                        a.P, a.r, tile,
                        (a.out ? a.out : a.data) + g0 * ((POL & kCompactOut) != 0 ? a.r : a.k) * static_cast<uint64_t>(a.P));
     const hipError_t e = hipGetLastError();
@@ -1754,7 +1777,7 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
   for (uint64_t g0 = 0; !a.rec_ready && g0 < a.groups; g0 += kMaxThreadsPerLaunch) {
     const uint64_t gn = (a.groups - g0 < kMaxThreadsPerLaunch) ? a.groups - g0 : kMaxThreadsPerLaunch;
     hipLaunchKernelGGL(classify, dim3(blocks_for(gn)), dim3(256), 0, s, a.masks + g0, gn, a.k, a.r,
-                       a.binom, a.meta, a.rec_off + g0, a.status ? a.status + g0 : nullptr);
+                       a.binom, a.meta, a.rec_off ? a.rec_off + g0 : nullptr, a.status ? a.status + g0 : nullptr);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

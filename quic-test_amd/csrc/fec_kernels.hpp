@@ -9,7 +9,9 @@
 namespace qfec {
 
 // Byte offsets of packets, when the data shards are not contiguous.
-enum class OffsetKind : int { kNone = 0, kU32 = 1, kU64 = 2 };
+// kAddr: `offsets` holds one absolute device address per packet (u64), `data` is unused --
+// the legacy-call coalescer (fec_coalesce.cpp) gathers packets from many callers' buffers.
+enum class OffsetKind : int { kNone = 0, kU32 = 1, kU64 = 2, kAddr = 3 };
 
 // Packets of any size P >= 16 at any byte address run on the 16-byte-column kernels
 // (fec_kernels.hip header); shorter ones on the byte kernels.
@@ -93,6 +95,9 @@ struct DecodeLaunch {
   // Rebuilt shards go to out + (g * r + m) * P (m-th lost data shard of group g, ascending),
   // `data` is only read (fec_recover_batch_rs_dev); else in place / at `out` like `data`.
   bool compact_out = false;
+  // compact_out with rec_off = the packed rows' row_start (fec_recover_batch_rs_dev_packed):
+  // rows are placed by global row index, so chunked launches must not offset `out`.
+  bool packed_rows = false;
 };
 
 constexpr uint32_t kDecodeScanGroups = 8;

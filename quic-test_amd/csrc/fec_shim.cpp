@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "fec_hip.h"
+#include "fec_internal.hpp"
 #include "fec_kernels.hpp"
 #include "gf256.hpp"
 
@@ -495,7 +496,7 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
                       const uint64_t* d_masks, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
                       uint8_t* d_status, hipStream_t s, DevBuf* rec = nullptr,
                       uint8_t* d_out = nullptr, double need_share = -1.0, bool compact_out = false,
-                      uint32_t* row_start = nullptr) {
+                      uint32_t* row_start = nullptr, uint64_t* row_total = nullptr) {
   DecodePlan* plan = nullptr;
   int rc = get_decode_plan(ctx, k, r, &plan);
   if (rc != FEC_OK) return rc;
@@ -555,6 +556,12 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
       return FEC_ERR_RANGE;
     }
     a.rec_off = row_start;
+    a.packed_rows = true;
+    // the form exists: now the row starts (two small launches ahead of the recover; the block
+    // sums use the stream's workspace, which this path does not otherwise take)
+    void* ws = nullptr;
+    QFEC_HIP(stream_workspace(ctx, s, qfec::rows_prefix_workspace_bytes(G), &ws));
+    QFEC_HIP(qfec::launch_rows_prefix(d_masks, G, k, r, row_start, static_cast<uint32_t*>(ws), row_total, s));
   }
   // Workspace: the caller's slot buffer (pipeline slots: private stream, calls serialised
   // by the context lock), else one private to this call.
@@ -992,11 +999,44 @@ QFEC_EXPORT void fec_free_slab(void* ptr) {
 
 QFEC_EXPORT void fec_free_repair_buffer(void* ptr) { fec_free_slab(ptr); }
 
+// What fec_coalesce.cpp borrows (fec_internal.hpp).
+namespace qfec {
+
+HostMem classify_host_pointer(const void* p, void** dev) {
+  switch (classify_ptr(p, dev)) {
+    case Mem::kDevice:
+      return HostMem::kDevice;
+    case Mem::kPinned:
+      return HostMem::kPinned;
+    default:
+      return HostMem::kPageable;
+  }
+}
+
+int encode_addr_batch(FECEncoderCtx* ctx, const uint64_t* d_addr, uint64_t G, uint32_t k, uint32_t r, uint32_t P,
+                      uint8_t* d_parity, hipStream_t s) {
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) {
+    set_error("fec_encode_batch: cannot bind device %d", ctx->device);
+    return FEC_ERR_NODEV;
+  }
+  return encode_dev_locked(ctx, nullptr, d_addr, OffsetKind::kAddr, G, k, r, P, d_parity, s);
+}
+
+void set_last_error(const char* msg) { g_last_error = msg ? msg : ""; }
+
+}  // namespace qfec
+
 static int fec_encode_batch_impl(FECEncoderCtx* ctx, const uint8_t* slab, const uint32_t* offsets,
                                  uint32_t num_groups, uint32_t packet_size, uint8_t* repair_out) {
   // fec_xor_simd.cpp:564-570, same order
   if (ctx == nullptr || slab == nullptr || offsets == nullptr || repair_out == nullptr) return -1;
   if (num_groups == 0 || packet_size == 0) return 0;
+  // Small host-resident calls -- the reference's one group per call from each stream's own
+  // context -- share launches with every other context's (fec_coalesce.cpp).
+  int crc = 0;
+  if (qfec::coalesce_legacy_encode(ctx->device, slab, offsets, num_groups, packet_size, repair_out, &crc)) return crc;
   constexpr uint32_t kPackets = 10;  // fec_xor_simd.cpp:580
   std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard dg(ctx->device);
@@ -1438,13 +1478,11 @@ static int fec_recover_batch_rs_dev_packed_impl(FECEncoderCtx* ctx, const uint8_
   std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard dg(ctx->device);
   if (!dg.ok) return FEC_ERR_NODEV;
-  const hipStream_t s = pick_stream(ctx, stream);
-  // block sums of the prefix scan: the stream's workspace (no record offsets on this path)
-  void* ws = nullptr;
-  QFEC_HIP(stream_workspace(ctx, s, qfec::rows_prefix_workspace_bytes(G), &ws));
-  QFEC_HIP(qfec::launch_rows_prefix(d_masks, G, k, r, d_row_start, static_cast<uint32_t*>(ws), d_total, s));
-  return decode_dev_locked(ctx, const_cast<uint8_t*>(d_data), d_parity, d_masks, G, k, r, P, d_status, s, nullptr,
-                           d_rebuilt, -1.0, /*compact_out=*/true, d_row_start);
+  // decode_dev_locked checks the form first and only then launches the row prefix, so an
+  // unsupported shape returns FEC_ERR_RANGE with d_row_start / d_total untouched
+  return decode_dev_locked(ctx, const_cast<uint8_t*>(d_data), d_parity, d_masks, G, k, r, P, d_status,
+                           pick_stream(ctx, stream), nullptr, d_rebuilt, -1.0, /*compact_out=*/true, d_row_start,
+                           d_total);
 }
 
 QFEC_EXPORT int fec_recover_batch_rs_dev_packed(FECEncoderCtx* ctx, const uint8_t* d_data, const uint8_t* d_parity,

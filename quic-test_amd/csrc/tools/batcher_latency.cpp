@@ -15,6 +15,10 @@
 //                                        (the C-ABI without the encoder API, and the copy cost)
 //   batcher_latency decode <streams> <seconds> <r> <deadline_us> <max_groups> [depth]
 //                                        (the decoder batcher at saturation, every packet checked)
+//   batcher_latency legacy <streams> <rate_pps> <seconds>
+//                                        (the reference's unchanged call site: every stream its own
+//                                        HybridFECEncoder -> fec_encode_batch with one group; rate 0 =
+//                                        back to back; QUICFEC_COALESCE=0/1 picks the library path)
 #include <sys/resource.h>
 
 #include <algorithm>
@@ -434,6 +438,74 @@ int single(int calls) {
   return 0;
 }
 
+// The unchanged HybridFECEncoder of every stream (its own FECEncoderCXX and context, one group
+// per fec_encode_batch call, encoder_hybrid.go:115): paced at `rate` packets/s per stream, or
+// back to back (rate 0).  Delay = the 10th packet's AddPacket; every repair payload is checked
+// against the AVX2 XOR restatement.  Whether concurrent streams' calls share launches is the
+// library's choice (QUICFEC_COALESCE, fec_coalesce.cpp); its stats are printed.
+int legacy(int S, double rate, double seconds) {
+  constexpr int NG = 16;
+  Bytes data(size_t(NG) * kK * kP), xr(size_t(NG) * kP);
+  oracle_fill_splitmix(data.data(), data.size(), 0x5EED0F, 0);
+  for (int g = 0; g < NG; ++g) {
+    const uint8_t* p[kK];
+    for (int j = 0; j < kK; ++j) p[j] = data.data() + (size_t(g) * kK + j) * kP;
+    oracle_xor_avx2(p, kK, kP, xr.data() + size_t(g) * kP);
+  }
+  FECCoalesceStats cs{};
+  fec_coalesce_stats(&cs, 1);
+  std::mutex mu;
+  std::vector<double> all;
+  std::atomic<long> groups{0}, errors{0}, fallback{0};
+  const auto t0 = Clock::now() + std::chrono::milliseconds(rate > 0 ? 200 : 0);
+  const auto t_end = t0 + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(seconds));
+  const double c0 = cpu_seconds();
+  std::vector<std::thread> th;
+  for (int s = 0; s < S; ++s)
+    th.emplace_back([&, s] {
+      HybridFECEncoder h(0.1);
+      if (!h.UseCXX()) ++fallback;
+      std::vector<double> lat;
+      const double phase = rate > 0 ? double(s) / S / rate : 0.0;
+      for (long i = 0;; ++i) {
+        if (rate > 0) {
+          const auto due = t0 + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(phase + i / rate));
+          if (due > t_end) break;
+          std::this_thread::sleep_until(due);
+        } else if ((i % kK) == 0 && Clock::now() >= t_end) {
+          break;
+        }
+        const int g = int((uint64_t(s) * 7 + uint64_t(i / kK)) % NG);
+        const auto a = Clock::now();
+        AddPacketResult res = h.AddPacket(data.data() + (size_t(g) * kK + i % kK) * kP, kP, uint64_t(i));
+        if (!res.err.ok()) ++errors;
+        if (res.needsRedundancy) {
+          lat.push_back(std::chrono::duration<double, std::micro>(Clock::now() - a).count());
+          ++groups;
+          if (res.redundancy.size() != 11u + kP || std::memcmp(res.redundancy.data() + 11, xr.data() + size_t(g) * kP, kP))
+            ++errors;
+        }
+      }
+      h.Close();
+      std::lock_guard<std::mutex> lk(mu);
+      all.insert(all.end(), lat.begin(), lat.end());
+    });
+  for (auto& t : th) t.join();
+  const double wall = rate > 0 ? seconds : std::chrono::duration<double>(Clock::now() - t0).count();
+  const double cpu = cpu_seconds() - c0;
+  fec_coalesce_stats(&cs, 0);
+  const char* co = std::getenv("QUICFEC_COALESCE");
+  char cfg[512];
+  std::snprintf(cfg, sizeof(cfg),
+                "\"streams\": %d, \"rate_pps\": %.0f, \"r\": 1, \"coalesce\": %d, \"errors\": %ld, \"go_fallback\": %ld, "
+                "\"coalesced_calls\": %llu, \"launches\": %llu, \"mean_batch\": %.2f, \"max_batch\": %llu",
+                S, rate, co && co[0] == '0' ? 0 : 1, errors.load(), fallback.load(), (unsigned long long)cs.calls,
+                (unsigned long long)cs.batches, cs.batches ? double(cs.groups) / cs.batches : 0.0,
+                (unsigned long long)cs.max_batch);
+  print_lat("legacy", cfg, all, double(groups), wall, cpu, nullptr);
+  return errors || fallback ? 1 : 0;
+}
+
 // One core: the reference's computation per group (AVX2 XOR, xor_packets_avx2 restated) and
 // the r = 3 code with GFNI (oracle fast form); 4096 groups of fresh data per pass.
 int cpu() {
@@ -485,6 +557,7 @@ int main(int argc, char** argv) {
   if (mode == "saturate")
     return saturate(int(arg(2, 16)), arg(3, 3), int(arg(4, 1)), int(arg(5, 1000)), int(arg(6, 4096)));
   if (mode == "single") return single(int(arg(2, 2000)));
+  if (mode == "legacy") return legacy(int(arg(2, 16)), arg(3, 0), arg(4, 3));
   if (mode == "decode")
     return draw(int(arg(2, 16)), arg(3, 3), int(arg(4, 3)), int(arg(5, 1000)), int(arg(6, 4096)), int(arg(7, 1024)));
   if (mode == "raw")

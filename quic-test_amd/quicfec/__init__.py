@@ -50,7 +50,7 @@ HIP_SYMBOLS = (
     "fec_batcher_wait", "fec_batcher_flush", "fec_batcher_stats", "fec_batcher_last_error",
     "fec_batcher_new_decoder", "fec_batcher_submit_shards", "fec_batcher_wait_rebuilt",
     "fec_batcher_new_multi", "fec_batcher_new_decoder_multi", "fec_batcher_devices",
-    "fec_recover_batch_rs_dev_packed",
+    "fec_recover_batch_rs_dev_packed", "fec_coalesce_stats",
 )
 
 
@@ -138,6 +138,7 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
         "fec_batcher_new_multi": (_vp, [_vp, _int, _u32, _u32, _u32, _u32, _u32, _u32]),
         "fec_batcher_new_decoder_multi": (_vp, [_vp, _int, _u32, _u32, _u32, _u32, _u32, _u32]),
         "fec_batcher_devices": (_int, [_vp]),
+        "fec_coalesce_stats": (_int, [_vp, _int]),
         "fec_recover_batch_rs_dev_packed": (_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _u32, _u32, _u32, _vp, _vp,
                                                    _vp, _vp, _vp]),
     }
@@ -505,3 +506,14 @@ def xor_packets(packets, packet_size: int, repair, variant: str = "avx2") -> Non
     lib = load_library()
     arr = (_vp * max(1, len(packets)))(*[_ptr(p) for p in packets])
     getattr(lib, f"xor_packets_{variant}")(arr, len(packets), packet_size, _ptr(repair))
+
+
+COALESCE_STATS = ("calls", "groups", "batches", "max_batch", "max_calls")
+
+
+def coalesce_stats(reset: bool = False) -> dict:
+    """Process-wide totals of the legacy-call coalescer (fec_coalesce_stats)."""
+    lib = load_library()
+    st = np.zeros(len(COALESCE_STATS), dtype=np.uint64)
+    _check(lib.fec_coalesce_stats(st.ctypes.data, 1 if reset else 0), "fec_coalesce_stats")
+    return dict(zip(COALESCE_STATS, (int(x) for x in st)))

@@ -1,0 +1,168 @@
+"""Legacy-call coalescing (fec_coalesce.cpp): the reference's unchanged call pattern -- one
+group per fec_encode_batch call, every stream on its own context (encoder_hybrid.go:115 via
+fec_cgo.go:138) -- from many threads at once, joined into shared launches.
+
+Row 0 is pinned by the reference: the expected repair rows are the golden fixture
+`batch_k10_p1200_g64` that `tests/golden/make_golden.py` produced with the reference's own
+fec_encode_batch (oracle/_ref); other sizes are checked against the oracle's XOR restatement.
+"""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _pinned_copy(lib, arr):
+    p = lib.fec_alloc_slab(max(arr.nbytes, 1))
+    assert p
+    ctypes.memmove(p, arr.ctypes.data, arr.nbytes)
+    return p
+
+
+def _read(p, n):
+    return np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p)).copy()
+
+
+def _run_threads(n, fn):
+    errs = []
+
+    def wrap(i):
+        try:
+            fn(i)
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=wrap, args=(i,)) for i in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
+@pytest.mark.parametrize("pinned", [True, False], ids=["pinned_slab", "pageable_slab"])
+def test_concurrent_one_group_calls_match_reference(quicfec_mod, oracle_mod, xor_golden, manifest, pinned, monkeypatch):
+    """16 streams, each with its own context (the Go wrapper's FECEncoderCXX), 1 group per call."""
+    monkeypatch.setenv("QUICFEC_COALESCE", "1")
+    c = next(c for c in manifest["cases"] if c["name"] == "batch_k10_p1200_g64")
+    G, P = c["G"], c["P"]
+    slab = oracle_mod.splitmix_bytes(G * 10 * P, c["seed"])
+    exp = xor_golden["batch_k10_p1200_g64"].reshape(G, P)
+    lib = quicfec_mod.load_library()
+    quicfec_mod.coalesce_stats(reset=True)
+    S, CALLS = 16, 96
+
+    def stream(i):
+        ctx = quicfec_mod.Context(device=0)
+        rng = np.random.default_rng(100 + i)
+        # the Go wrapper packs the group's 10 packets back to back into its page-locked slab
+        sp = lib.fec_alloc_slab(10 * P) if pinned else None
+        rp = lib.fec_alloc_repair_buffer(P)
+        host = np.zeros(10 * P, dtype=np.uint8)
+        offs = (np.arange(10, dtype=np.uint32) * P).astype(np.uint32)
+        try:
+            for _ in range(CALLS):
+                g = int(rng.integers(G))
+                grp = slab[g * 10 * P:(g + 1) * 10 * P]
+                if pinned:
+                    ctypes.memmove(sp, grp.ctypes.data, grp.nbytes)
+                    src = sp
+                else:
+                    host[:] = grp
+                    src = host.ctypes.data
+                assert lib.fec_encode_batch(ctx.handle, src, offs.ctypes.data, 1, P, rp) == 0
+                assert np.array_equal(_read(rp, P), exp[g]), (i, g)
+        finally:
+            if sp:
+                lib.fec_free_slab(sp)
+            lib.fec_free_repair_buffer(rp)
+            ctx.close()
+
+    _run_threads(S, stream)
+    st = quicfec_mod.coalesce_stats()
+    assert st["calls"] == S * CALLS and st["groups"] == S * CALLS
+    # calls from different contexts shared launches
+    assert st["batches"] < st["calls"] and st["max_calls"] >= 2, st
+
+
+@pytest.mark.parametrize("P", [8, 17, 100, 1200, 1201, 1500])
+def test_concurrent_mixed_calls_match_oracle(quicfec_mod, oracle_mod, P, monkeypatch):
+    """Calls of 1..64 groups, scattered u32 offsets, pinned and pageable slabs, one batch."""
+    monkeypatch.setenv("QUICFEC_COALESCE", "1")
+    lib = quicfec_mod.load_library()
+    quicfec_mod.coalesce_stats(reset=True)
+    S = 8
+
+    def stream(i):
+        ctx = quicfec_mod.Context(device=0)
+        rng = np.random.default_rng(7 * P + i)
+        try:
+            for call in range(24):
+                G = int(rng.integers(1, 65))
+                slab = oracle_mod.splitmix_bytes(G * 10 * P + 4096, 1000 * P + 37 * i + call)
+                # each packet at an arbitrary byte offset (packet_size bytes read from each)
+                offs = rng.integers(0, slab.nbytes - P + 1, size=G * 10).astype(np.uint32)
+                pk = [[slab[o:o + P] for o in offs[g * 10:(g + 1) * 10]] for g in range(G)]
+                exp = np.concatenate([oracle_mod.xor_packets(p, P) for p in pk])
+                pinned = bool(call % 2)
+                if pinned:
+                    sp, rp = _pinned_copy(lib, slab), lib.fec_alloc_repair_buffer(G * P)
+                    try:
+                        assert lib.fec_encode_batch(ctx.handle, sp, offs.ctypes.data, G, P, rp) == 0
+                        got = _read(rp, G * P)
+                    finally:
+                        lib.fec_free_slab(sp)
+                        lib.fec_free_repair_buffer(rp)
+                else:
+                    got = np.full(G * P, 0xEE, dtype=np.uint8)
+                    assert ctx.encode_batch_legacy(slab, offs, G, P, got) == 0
+                assert np.array_equal(got, exp), (i, call, G, pinned)
+        finally:
+            ctx.close()
+
+    _run_threads(S, stream)
+    st = quicfec_mod.coalesce_stats()
+    assert st["calls"] == S * 24, st
+
+
+@pytest.mark.parametrize("coalesce", ["0", "1"])
+def test_coalesce_switch_same_bytes(gpu_ctx, oracle_mod, xor_golden, manifest, coalesce, monkeypatch, quicfec_mod):
+    """QUICFEC_COALESCE=0 runs the call alone on its context; both give the reference's bytes."""
+    monkeypatch.setenv("QUICFEC_COALESCE", coalesce)
+    quicfec_mod.coalesce_stats(reset=True)
+    c = next(c for c in manifest["cases"] if c["name"] == "batch_scattered_p100_g16")
+    slab = oracle_mod.splitmix_bytes(c["slab_bytes"], c["seed"])
+    offs = xor_golden["batch_scattered_p100_g16_offsets"]
+    rep = np.zeros(c["G"] * c["P"], dtype=np.uint8)
+    assert gpu_ctx.encode_batch_legacy(slab, offs, c["G"], c["P"], rep) == 0
+    assert np.array_equal(rep, xor_golden["batch_scattered_p100_g16"])
+    assert quicfec_mod.coalesce_stats()["calls"] == (1 if coalesce == "1" else 0)
+
+
+def test_large_and_device_calls_bypass(gpu_ctx, oracle_mod, quicfec_mod, torch_cuda, monkeypatch):
+    """Calls above QUICFEC_COALESCE_MAX_GROUPS and device-resident calls run alone."""
+    monkeypatch.setenv("QUICFEC_COALESCE", "1")
+    monkeypatch.setenv("QUICFEC_COALESCE_MAX_GROUPS", "4")
+    quicfec_mod.coalesce_stats(reset=True)
+    G, P = 5, 300
+    slab = oracle_mod.splitmix_bytes(G * 10 * P, 99)
+    offs = (np.arange(G * 10, dtype=np.uint32) * P).astype(np.uint32)
+    exp = np.concatenate([oracle_mod.xor_packets([slab[(g * 10 + j) * P:(g * 10 + j + 1) * P] for j in range(10)], P)
+                          for g in range(G)])
+    rep = np.zeros(G * P, dtype=np.uint8)
+    assert gpu_ctx.encode_batch_legacy(slab, offs, G, P, rep) == 0
+    assert np.array_equal(rep, exp)
+    ds = torch_cuda.from_numpy(slab).cuda()
+    do = torch_cuda.from_numpy(offs.view(np.int32)).cuda()
+    dr = torch_cuda.zeros(4 * P, dtype=torch_cuda.uint8, device="cuda")
+    assert gpu_ctx.encode_batch_legacy(ds, do, 4, P, dr) == 0
+    assert np.array_equal(dr.cpu().numpy(), exp[:4 * P])
+    assert quicfec_mod.coalesce_stats()["calls"] == 0
+    rep4 = np.zeros(4 * P, dtype=np.uint8)
+    assert gpu_ctx.encode_batch_legacy(slab, offs, 4, P, rep4) == 0
+    assert np.array_equal(rep4, exp[:4 * P])
+    assert quicfec_mod.coalesce_stats()["calls"] == 1

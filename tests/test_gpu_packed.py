@@ -96,12 +96,15 @@ def test_packed_refusals_and_empty(gpu_ctx, quicfec_mod, torch_cuda):
         p = torch.zeros(G * r * P, dtype=torch.uint8, device="cuda")
         m = torch.ones(G, dtype=torch.int64, device="cuda")
         out = torch.full((G * r * P,), 0x5A, dtype=torch.uint8, device="cuda")
-        rs = torch.zeros(G, dtype=torch.int32, device="cuda")
+        rs = torch.full((G,), 0x3C3C3C3C, dtype=torch.int32, device="cuda")
+        tot = torch.full((1,), -5, dtype=torch.int64, device="cuda")
         with pytest.raises(quicfec_mod.FecError) as ei:
-            gpu_ctx.recover_packed_dev(d, p, m, G, k, r, P, out, rs)
+            gpu_ctx.recover_packed_dev(d, p, m, G, k, r, P, out, rs, tot)
         assert ei.value.code == quicfec_mod.FEC_ERR_RANGE, (k, r, P)
         gpu_ctx.synchronize()
+        # refused before anything ran: rebuilt rows, row starts and total untouched
         assert bool((out == 0x5A).all())
+        assert bool((rs == 0x3C3C3C3C).all()) and int(tot.item()) == -5
     # no groups: the total is 0
     z = torch.zeros(16, dtype=torch.uint8, device="cuda")
     tot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
@@ -131,3 +134,55 @@ def test_packed_masks_at_odd_word(gpu_ctx, oracle_mod, torch_cuda):
     assert int(tot.item()) == n
     assert np.array_equal(rs.cpu().numpy().view(np.uint32), start)
     assert np.array_equal(out.cpu().numpy().reshape(G * r, P)[:n], exp)
+
+
+@pytest.mark.parametrize("api", ["packed", "packed_scan", "slots", "in_place"])
+@pytest.mark.parametrize("k,r,P", [(10, 3, 1200), (10, 2, 700), (20, 5, 1200)])
+def test_chunked_launches(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, api, k, r, P):
+    """Launches split into chunks of QUICFEC_MAX_WAVE_BLOCKS workgroups (otherwise only past
+    16.7M groups): packed rows keep their global row starts in every chunk, and the forms that
+    take no record offsets get none in later chunks."""
+    if k == 20 and api.startswith("packed"):
+        pytest.skip("no packed form for the record-addressed shape")
+    monkeypatch.setenv("QUICFEC_MAX_WAVE_BLOCKS", "7")
+    if api == "packed_scan":
+        monkeypatch.setenv("QUICFEC_DECODE_SCAN", "8")
+    torch = torch_cuda
+    G = 1_237
+    rng = np.random.default_rng(k * 100 + r + P)
+    masks = np.zeros(G, dtype=np.uint64)
+    for g in range(G):
+        for sh in rng.permutation(k + r)[: rng.integers(0, r + 2)]:
+            masks[g] |= np.uint64(1) << np.uint64(int(sh))
+    broken, par, st_exp, start, exp = _case(oracle_mod, k, r, P, G, masks)
+    if api.startswith("packed"):
+        dd, out, rs, tot, st = _run(gpu_ctx, torch, broken, par, masks, G, k, r, P)
+        n = len(exp)
+        assert int(tot.item()) == n
+        assert np.array_equal(rs.cpu().numpy().view(np.uint32), start)
+        o = out.cpu().numpy().reshape(G * r, P)
+        assert np.array_equal(o[:n], exp)
+        assert (o[n:] == 0x5A).all()
+        assert np.array_equal(st.cpu().numpy(), st_exp)
+        return
+    dd, dp, dm = _dev(torch, broken), _dev(torch, par), _dev(torch, masks.view(np.int64))
+    st = torch.full((G,), 7, dtype=torch.uint8, device="cuda")
+    lost = ((masks[:, None] >> np.arange(k, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+    ok = st_exp == 0
+    if api == "slots":
+        out = torch.full((G * r * P,), 0x5A, dtype=torch.uint8, device="cuda")
+        gpu_ctx.recover_dev(dd, dp, dm, G, k, r, P, out, st)
+        gpu_ctx.synchronize()
+        o = out.cpu().numpy().reshape(G, r, P)
+        ref = broken.copy().reshape(G, k, P)
+        oracle_mod.rs_decode(ref.reshape(-1), par, masks, G, k, r, P, nthreads=8)
+        for g in np.nonzero(ok & lost.any(axis=1))[0]:
+            ids = np.nonzero(lost[g])[0]
+            assert np.array_equal(o[g, :len(ids)], ref[g, ids]), g
+    else:
+        gpu_ctx.decode_dev(dd, dp, dm, G, k, r, P, st)
+        gpu_ctx.synchronize()
+        ref = broken.copy()
+        oracle_mod.rs_decode(ref, par, masks, G, k, r, P, nthreads=8)
+        assert np.array_equal(dd.cpu().numpy(), ref)
+    assert np.array_equal(st.cpu().numpy(), st_exp)
