@@ -78,11 +78,45 @@ def launch_plan(gpus: int, env) -> tuple[str, int]:
     return ("run", 1) if gpus == 1 else ("spawn", gpus)
 
 
-def visible_gpus() -> int:
-    """Visible GPU count without initialising the GPU in this process (on this image
-    torch.cuda.device_count() does not create a HIP context)."""
-    import torch
-    return int(torch.cuda.device_count())
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+VISIBLE_VARS = ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+
+
+def visible_gpus(env=None, nodes: str = KFD_NODES) -> int:
+    """Visible GPU count without loading the HIP runtime in this process: the KFD topology's
+    GPU nodes (gpu_id != 0; CPU nodes have 0), narrowed by ROCR_/HIP_/CUDA_VISIBLE_DEVICES
+    (each lists the devices the next layer sees; set but empty = none).  The spawning parent
+    of `bench.py --gpus N` must stay off the GPU (its children bind their devices; a process
+    that initialised the GPU must never fork-exec), so it never imports torch."""
+    env = os.environ if env is None else env
+    phys = None
+    try:
+        ids = []
+        for nd in sorted(os.listdir(nodes)):
+            try:
+                ids.append(int(open(os.path.join(nodes, nd, "gpu_id")).read().split()[0]))
+            except (OSError, ValueError, IndexError):
+                pass
+        phys = sum(1 for i in ids if i != 0)
+    except OSError:
+        pass
+    n = phys
+    for var in VISIBLE_VARS:
+        v = env.get(var)
+        if v is None:
+            continue
+        listed = len([x for x in v.split(",") if x.strip()])
+        n = listed if n is None else min(n, listed)
+    return n or 0
+
+
+def hip_runtime_mapped() -> bool:
+    """Whether this process has the HIP runtime (libamdhip64) mapped, e.g. through torch."""
+    try:
+        with open("/proc/self/maps") as f:
+            return any("libamdhip64" in ln for ln in f)
+    except OSError:
+        return False
 
 
 def bind_local_device(local: int, world: int, ndev: int) -> int:
@@ -109,6 +143,8 @@ def spawn_ranks(n: int, argv: list[str], check_devices: bool = True) -> int:
     of this script on 127.0.0.1, one per GPU, and return the worst exit code.  This parent
     makes no GPU call (children bind their device before RCCL init); only rank 0 prints."""
     import subprocess
+    if hip_runtime_mapped():
+        raise SystemExit("bench.py: the spawning parent has the HIP runtime loaded; it must make no GPU call")
     if check_devices and dist_backend() != "gloo":
         ndev = visible_gpus()
         if n > ndev:
@@ -185,6 +221,10 @@ def reduce_sum(x: float) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def reduce_min(x: float) -> float:
+    return -reduce_max(-x)
 
 
 def barrier() -> None:
@@ -367,10 +407,7 @@ def cpu_baseline(cfg: dict, seconds: float = 10.0) -> dict:
         ref1 = _rate(lambda: ref_range(0, Gr), Gr * 10 * P, leg)
         refn = _rate(lambda: _threaded(threads, Gr, ref_range), Gr * 10 * P, leg)
         ref.fec_encoder_free(h)
-        ref_block = {"threads_1": round(ref1, 3), f"threads_{threads}": round(refn, 3),
-                     "note": "oracle/_ref: /root/reference internal/fec/fec_xor_simd.cpp compiled by "
-                             "oracle/Makefile; fec_encode_batch (XOR parity row 0 only, the reference's "
-                             "whole computation), one call per thread over disjoint group ranges"}
+        ref_block = (round(ref1, 3), round(refn, 3))
     cpu_model = ""
     try:
         for ln in open("/proc/cpuinfo"):
@@ -393,10 +430,20 @@ def cpu_baseline(cfg: dict, seconds: float = 10.0) -> dict:
         "cpu_model": cpu_model, "nproc": os.cpu_count(),
         "affinity_cores": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
         "cgroup_cpu_quota": cgroup_cpu_quota(),
-        "reference_fec_encode_batch_gib_s": ref_block,
-        "xor_avx2_row0_gib_s": {"threads_1": round(xor1, 3), f"threads_{threads}": round(xorn, 3),
-                                "note": "AVX2 restatement of xor_packets_avx2 (fec_xor_simd.cpp:74-204), "
-                                        "bit-identical to it (tests/test_oracle_golden.py)"},
+        # the reference itself (XOR parity row 0 only, its whole computation): oracle/_ref =
+        # /root/reference internal/fec/fec_xor_simd.cpp compiled by oracle/Makefile,
+        # fec_encode_batch on 1 thread as written and on every core over disjoint group ranges
+        "ref_encode_batch_1t_GiBps": ref_block[0] if ref_block else None,
+        "ref_encode_batch_nt_GiBps": ref_block[1] if ref_block else None,
+        "ref_encode_batch_threads": threads if ref_block else None,
+        # AVX2 restatement of xor_packets_avx2 (fec_xor_simd.cpp:74-204), bit-identical to it
+        # (tests/test_oracle_golden.py)
+        "xor_avx2_row0_1t_GiBps": round(xor1, 3),
+        "xor_avx2_row0_nt_GiBps": round(xorn, 3),
+        "ref_note": ("ref_encode_batch_*: the reference library (oracle/_ref, built from /root/reference's "
+                     "internal/fec/fec_xor_simd.cpp) fec_encode_batch, XOR row 0 only, 1 thread and "
+                     f"{threads} threads; value: the GF(2^8) port, r={r} rows"
+                     + (" + decode" if cfg["decode"] else "")),
     }
 
 
@@ -404,43 +451,60 @@ def e2e_pinned(ctx, d_data, d_parity, d_masks, G: int, cfg: dict, reps: int = 3)
     """The path as the QUIC client/server sees it: packets start and end in host memory.
     Page-locked host buffers (the same allocator kind as fec_alloc_slab) go through the
     synchronous API, whose kernels then read and write them in place over PCIe (zero-copy;
-    QUICFEC_SMALL_CALL_BYTES=0 selects the 3-stream H2D -> kernel -> D2H pipeline instead)."""
+    QUICFEC_SMALL_CALL_BYTES=0 selects the 3-stream H2D -> kernel -> D2H pipeline instead).
+
+    Every rank runs each leg after a barrier; a leg's job time is the MAX over ranks and its
+    rate the payload of ALL ranks over that time (best of `reps`), with the per-rank rates'
+    spread beside it -- with N GPUs this is the node's host-resident rate, each GPU on its own
+    PCIe link.  Never `value`."""
     import torch
     k, r, P = cfg["k"], cfg["r"], cfg["P"]
     h_data = torch.empty(d_data.numel(), dtype=torch.uint8, pin_memory=True)
     h_par = torch.empty(d_parity.numel(), dtype=torch.uint8, pin_memory=True)
     h_data.copy_(d_data)
     torch.cuda.synchronize()
-    out = {}
-    # raw copy rates on this box for reference
-    t0 = time.perf_counter()
-    d_data.copy_(h_data, non_blocking=True)
-    torch.cuda.synchronize()
-    out["h2d_GBps"] = round(h_data.numel() / (time.perf_counter() - t0) / 1e9, 2)
-    t0 = time.perf_counter()
-    h_data.copy_(d_data, non_blocking=True)
-    torch.cuda.synchronize()
-    out["d2h_GBps"] = round(h_data.numel() / (time.perf_counter() - t0) / 1e9, 2)
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        ctx.encode(h_data, k, r, P, h_par, num_groups=G)
-        ts.append(time.perf_counter() - t0)
-    te = min(ts)
-    out["encode_GiBps"] = round(k * P * G / te / 2**30, 2)
-    out["encode_ms"] = round(te * 1e3, 2)
+    payload = k * P * G
+    total = reduce_sum(float(payload))
+    ranks = int(reduce_sum(1.0))
+
+    def leg(fn, nbytes_local: float, nbytes_total: float) -> dict:
+        best = None
+        for _ in range(reps):
+            barrier()
+            t0 = time.perf_counter()
+            fn()
+            t = time.perf_counter() - t0
+            tj = reduce_max(t)
+            if best is None or tj < best[0]:
+                best = (tj, t)
+        tj, t = best
+        mine = nbytes_local / t / 2**30
+        return {"job_s": tj, "GiBps": nbytes_total / tj / 2**30,
+                "rank_GiBps": {"min": round(reduce_min(mine), 2), "max": round(reduce_max(mine), 2)}}
+
+    def sync_copy(dst, src):
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+
+    out = {"ranks": ranks}
+    nb = float(h_data.numel())
+    nb_all = reduce_sum(nb)
+    for name, dst, src in (("h2d", d_data, h_data), ("d2h", h_data, d_data)):
+        x = leg(lambda: sync_copy(dst, src), nb, nb_all)
+        out[f"{name}_GBps"] = round(x["GiBps"] * 2**30 / 1e9, 2)
+    enc = leg(lambda: ctx.encode(h_data, k, r, P, h_par, num_groups=G), payload, total)
+    out["encode_GiBps"] = round(enc["GiBps"], 2)
+    out["encode_ms"] = round(enc["job_s"] * 1e3, 2)
+    out["encode_rank_GiBps"] = enc["rank_GiBps"]
     if d_masks is not None:
         h_masks = d_masks.cpu().numpy().view("uint64")
-        ts = []
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            ctx.decode(h_data, h_par, h_masks, k, r, P, num_groups=G)
-            ts.append(time.perf_counter() - t0)
-        td = min(ts)
-        out["decode_GiBps"] = round(k * P * G / td / 2**30, 2)
-        out["decode_ms"] = round(td * 1e3, 2)
-        out["roundtrip_GiBps"] = round(k * P * G / (te + td) / 2**30, 2)
-    out["note"] = "payload k*P*G per second, host page-locked in/out, best of %d" % reps
+        dec = leg(lambda: ctx.decode(h_data, h_par, h_masks, k, r, P, num_groups=G), payload, total)
+        out["decode_GiBps"] = round(dec["GiBps"], 2)
+        out["decode_ms"] = round(dec["job_s"] * 1e3, 2)
+        out["decode_rank_GiBps"] = dec["rank_GiBps"]
+        out["roundtrip_GiBps"] = round(total / (enc["job_s"] + dec["job_s"]) / 2**30, 2)
+    out["note"] = (f"payload k*P*G of all {ranks} rank(s) per second of the slowest rank (barrier before "
+                   f"each leg), host page-locked in/out, best of {reps}; *_rank_GiBps = per-rank spread")
     del h_data, h_par
     return out
 
@@ -719,6 +783,11 @@ def main() -> int:
                 "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes"],
                 "traffic_source": pmc_note,
                 "read_frac": round(dom_read / (kernels[dom]["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "read_frac_of_box_copy": round(dom_read / (kernels[dom]["ms"] * 1e-3) / 1e9 / copy["achieved_GBps"], 4),
+                # north_star's "70% of the HBM-read roofline": reads at 0.70 x 8 TB/s while this
+                # kernel also writes its bytes needs this much total traffic -- above the box's
+                # copy ceiling (box_copy_GBps), so that literal target is out of reach
+                "read_target_total_GBps": round(0.70 * HBM_PEAK_GBS * kernels[dom]["algorithmic_bytes"] / dom_read, 1),
                 "box_copy_GBps": copy["achieved_GBps"],
                 "frac_of_box_copy": round(kernels[dom]["achieved_GBps"] / copy["achieved_GBps"], 4),
                 "timing": ("torch.cuda.Event on torch's default stream, kernels on the context's stream"

@@ -123,6 +123,16 @@ void oracle_xor_encode_contig(const uint8_t* data, uint64_t G, uint32_t k, uint3
     run_ranges(xor_contig_range, &a, G, nthreads);
 }
 
+void oracle_xor_groups(oracle_xor_fn xor_fn, const uint8_t* data, uint64_t G, uint32_t k, uint32_t P,
+                       uint8_t* repair) {
+    const uint8_t* pk[256];
+    if (xor_fn == NULL || k == 0 || k > 256) return;
+    for (uint64_t g = 0; g < G; ++g) {
+        for (uint32_t j = 0; j < k; ++j) pk[j] = data + (g * k + j) * (uint64_t)P;
+        xor_fn(pk, k, P, repair + g * (uint64_t)P);
+    }
+}
+
 /* ------------------------------------------------------------------------- */
 /* GF(2^8), x^8 + x^4 + x^3 + x^2 + 1 (0x11D), generator 2                    */
 /* ------------------------------------------------------------------------- */

@@ -53,6 +53,13 @@ int oracle_encode_batch_legacy(const uint8_t* slab, const uint32_t* offsets, uin
 void oracle_xor_encode_contig(const uint8_t* data, uint64_t G, uint32_t k, uint32_t P,
                               uint8_t* repair, int nthreads);
 
+/* Calls xor_fn (an xor_packets_* of the reference's signature, fec_xor_simd.h:22-24) once per
+ * group over the G groups of k contiguous packets -- the C1 leg's driver, so the reference's
+ * own AVX2 function is timed without a foreign-call cost per group. */
+typedef void (*oracle_xor_fn)(const uint8_t* const* pkts, size_t n, size_t packet_size, uint8_t* out);
+void oracle_xor_groups(oracle_xor_fn xor_fn, const uint8_t* data, uint64_t G, uint32_t k, uint32_t P,
+                       uint8_t* repair);
+
 /* ---- GF(2^8), polynomial 0x11D, generator 2 ---- */
 uint8_t oracle_gf_mul(uint8_t a, uint8_t b);
 uint8_t oracle_gf_inv(uint8_t a);        /* a != 0 */

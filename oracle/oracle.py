@@ -37,6 +37,7 @@ def lib() -> ctypes.CDLL:
             "oracle_xor_avx2": (None, [ctypes.POINTER(_vp), _sz, _sz, _vp]),
             "oracle_encode_batch_legacy": (_int, [_vp, _vp, _u32, _u32, _vp, _int]),
             "oracle_xor_encode_contig": (None, [_vp, _u64, _u32, _u32, _vp, _int]),
+            "oracle_xor_groups": (None, [_vp, _vp, _u64, _u32, _u32, _vp]),
             "oracle_gf_mul": (ctypes.c_uint8, [ctypes.c_uint8, ctypes.c_uint8]),
             "oracle_gf_inv": (ctypes.c_uint8, [ctypes.c_uint8]),
             "oracle_parity_matrix": (_int, [_u32, _u32, _vp]),

@@ -38,7 +38,9 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
+#include <chrono>
 #include <vector>
 
 #include "fec_hip.h"
@@ -102,18 +104,18 @@ struct Pinned {
 
 struct Batch {
   enum State { kFree, kOpen, kClosed, kLaunched, kDone };
-  State state = kFree;
+  std::atomic<int> state{kFree};  // transitions under the coalescer's lock, except kDone (leader)
   Pinned addr;    // cap * kPackets packet addresses (u64), read by the kernel in place
   Pinned stage;   // cap * kPackets * P bytes: packets of pageable callers (allocated on first need)
   Pinned out;     // cap * P: repair row of every group, written by the kernel in place
   hipEvent_t done = nullptr;
   uint32_t used = 0;     // groups reserved
   uint32_t calls = 0;    // callers in the batch
-  uint32_t copying = 0;  // callers whose addresses / packets are not written yet
+  std::atomic<uint32_t> copying{0};  // callers whose addresses / packets are not written yet
   uint32_t readers = 0;  // callers that have not copied their rows out
   int rc = FEC_OK;
   std::string err;
-  std::condition_variable cv;  // the batch's callers: copies landed, launched, done, lead chance
+  std::condition_variable cv;  // callers that stopped spinning: done, or a launch slot came free
 };
 
 std::atomic<uint64_t> g_calls{0}, g_groups{0}, g_batches{0}, g_max_batch{0}, g_max_calls{0};
@@ -179,7 +181,7 @@ class Coalescer {
     const uint32_t g0 = b.used;
     b.used += G;
     ++b.calls;
-    ++b.copying;
+    b.copying.fetch_add(1, std::memory_order_relaxed);
     ++b.readers;
     lk.unlock();
     // the packets' addresses (and, from pageable memory, the packets); packet_size bytes from
@@ -196,23 +198,39 @@ class Coalescer {
         a[i] = reinterpret_cast<uint64_t>(b.stage.dev + (first + i) * P);
       }
     }
-    lk.lock();
-    if (--b.copying == 0) b.cv.notify_all();
-    for (;;) {
-      if (b.state == Batch::kDone) break;
-      if (b.state == Batch::kOpen && inflight < max_inflight) {
-        lead(b, lk);
+    b.copying.fetch_sub(1, std::memory_order_release);
+    // Wait for the batch, or lead it once a launch slot is free.  Callers spin first (a
+    // condition-variable wake costs several microseconds per hand-off, as much as the launch
+    // itself), then yield, then sleep in short timed waits.
+    for (uint32_t spins = 0;; ++spins) {
+      const int st = b.state.load(std::memory_order_acquire);
+      if (st == Batch::kDone) break;
+      if (st == Batch::kOpen && inflight.load(std::memory_order_acquire) < max_inflight) {
+        lk.lock();
+        if (b.state.load(std::memory_order_relaxed) == Batch::kOpen &&
+            inflight.load(std::memory_order_relaxed) < max_inflight)
+          lead(b, lk);  // returns with the lock released
+        else
+          lk.unlock();
+        spins = 0;
         continue;
       }
-      b.cv.wait(lk);
+      if (spins < 256) {
+        for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
+      } else if (spins < 4096) {
+        std::this_thread::yield();
+      } else {
+        lk.lock();
+        b.cv.wait_for(lk, std::chrono::microseconds(200));
+        lk.unlock();
+      }
     }
-    const int rc = b.rc;
+    const int rc = b.rc;  // written before kDone was stored (release)
     if (rc != FEC_OK) set_last_error(b.err.c_str());
-    lk.unlock();
     if (rc == FEC_OK) std::memcpy(repair_out, b.out.host + uint64_t(g0) * P, uint64_t(G) * P);
     lk.lock();
     if (--b.readers == 0) {
-      b.state = Batch::kFree;
+      b.state.store(Batch::kFree, std::memory_order_relaxed);
       if (open < 0) open_free();
     }
     return rc;
@@ -228,40 +246,52 @@ class Coalescer {
   std::condition_variable cv_room;  // callers waiting for an open batch with room
   std::vector<std::unique_ptr<Batch>> batches;
   int open = -1;                    // the batch taking callers, -1 while none is free
-  int inflight = 0;                 // batches closed by a leader and not done yet
+  std::atomic<int> inflight{0};     // batches closed by a leader and not done yet
   bool staging_ready = false;
 
   // Opens a free batch for new callers, if there is one.  Caller holds mu.
   void open_free() {
     for (size_t i = 0; i < batches.size(); ++i) {
       Batch& b = *batches[i];
-      if (b.state != Batch::kFree) continue;
-      b.state = Batch::kOpen;
-      b.used = b.calls = b.copying = b.readers = 0;
+      if (b.state.load(std::memory_order_relaxed) != Batch::kFree) continue;
+      b.used = b.calls = b.readers = 0;
+      b.copying.store(0, std::memory_order_relaxed);
       b.rc = FEC_OK;
       b.err.clear();
+      b.state.store(Batch::kOpen, std::memory_order_release);
       open = static_cast<int>(i);
       cv_room.notify_all();
       return;
     }
   }
 
-  // Closes, launches and completes batch b (its caller holds mu through `lk`).
+  // Closes, launches and completes batch b.  Called with mu held through `lk`; returns with it
+  // released.
   void lead(Batch& b, std::unique_lock<std::mutex>& lk) {
-    b.state = Batch::kClosed;
+    b.state.store(Batch::kClosed, std::memory_order_relaxed);
     open = -1;
     open_free();
-    ++inflight;
-    while (b.copying > 0) b.cv.wait(lk);
-    b.state = Batch::kLaunched;
-    const uint32_t n = b.used, calls = b.calls;
+    inflight.fetch_add(1, std::memory_order_acq_rel);
+    const uint32_t n = b.used, calls = b.calls;  // closed: no more reservations
     lk.unlock();
+    while (b.copying.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
+    b.state.store(Batch::kLaunched, std::memory_order_relaxed);
     int rc = encode_addr_batch(ctx, reinterpret_cast<const uint64_t*>(b.addr.dev), n, kPackets, 1, P, b.out.dev, stream);
     std::string err;
     if (rc == FEC_OK) {
       BindDevice bd(device);
       hipError_t e = bd.ok ? hipEventRecord(b.done, stream) : hipErrorInvalidDevice;
-      if (e == hipSuccess) e = hipEventSynchronize(b.done);
+      // poll (a blocking wait adds its wake-up to every batch); yield once it takes a while
+      for (uint32_t i = 0; e == hipSuccess; ++i) {
+        e = hipEventQuery(b.done);
+        if (e != hipErrorNotReady) break;
+        e = hipSuccess;
+        if (i < 4096) {
+          for (int j = 0; j < 16; ++j) __builtin_ia32_pause();
+        } else {
+          std::this_thread::yield();
+        }
+      }
       if (e != hipSuccess) {
         (void)hipGetLastError();
         rc = FEC_ERR_HIP;
@@ -275,13 +305,14 @@ class Coalescer {
     g_groups.fetch_add(n, std::memory_order_relaxed);
     atomic_max(g_max_batch, n);
     atomic_max(g_max_calls, calls);
-    lk.lock();
     b.rc = rc;
     b.err = err;
-    b.state = Batch::kDone;
-    --inflight;
+    b.state.store(Batch::kDone, std::memory_order_release);
+    inflight.fetch_sub(1, std::memory_order_acq_rel);
+    lk.lock();
     b.cv.notify_all();
     if (open >= 0) batches[open]->cv.notify_all();  // a launch slot is free: the open batch may go
+    lk.unlock();
   }
 };
 

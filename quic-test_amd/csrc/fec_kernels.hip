@@ -47,9 +47,6 @@ typedef uint32_t u32u __attribute__((aligned(1)));
 constexpr int kNtLoad = 1;        // non-temporal loads (data read once)
 constexpr int kNtStore = 2;       // non-temporal stores
 constexpr int kNoCoefBranch = 4;  // decode: multiply by every coefficient, no 0/1 branches
-constexpr int kProbeXorOnly = 8;   // probes only: decode_fused XORs instead of multiplying
-constexpr int kProbeNoStore = 16; // probes only: decode_fused never stores (read pattern alone, xor-only path too)
-constexpr int kProbeDense = 32;   // probes only: decode_fused reads data shards 0..K-1, no parity
 // decode_fused: coefficient tables through LDS.  A record-addressed wave reads e*K 32-B
 // table entries of its group's record.  For large codebooks (k=20 r=5: 53,130 records,
 // 143 MB) the records miss the scalar cache, and one scalar load per coefficient — a few
@@ -57,9 +54,6 @@ constexpr int kProbeDense = 32;   // probes only: decode_fused reads data shards
 // this bit the wave fetches its rows with vector loads issued next to its survivor loads
 // (one round trip) and reads them from a per-wave LDS slice.
 constexpr int kLdsTabs = 64;
-constexpr int kProbeWin10 = 128;  // probes only: kLdsTabs survivor window of 10 (default 6)
-constexpr int kProbeWin14 = 256;  // probes only: window of 14
-constexpr int kProbeWindowed = 512;  // probes only: windowed body, tables from the record
 // decode_fused / decode_wave: the m-th rebuilt shard of group g (erased data shards in
 // ascending order) goes to out + (g * r + m) * P -- one contiguous run of rebuilt packets
 // per group, groups back to back, like encode's parity rows -- instead of its place among
@@ -641,9 +635,7 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
   uint32_t sid[K];
 #pragma unroll
   for (int s = 0; s < K; ++s) {
-    if constexpr ((POL & kProbeDense) != 0) {
-      sid[s] = static_cast<uint32_t>(s);
-    } else if constexpr (DIRECT) {
+    if constexpr (DIRECT) {
       sid[s] = static_cast<uint32_t>(__builtin_ctzll(surv));
       surv &= surv - 1;
     } else {
@@ -681,9 +673,6 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
       load(shard(sid[s]), v);
 #pragma unroll
       for (int q = 0; q < NW; ++q) acc[q] ^= v[q];
-    }
-    if constexpr ((POL & kProbeNoStore) != 0) {
-      if (acc[0] != 0x9E3779B9u || acc[NW - 1] != 0x7F4A7C15u) return;
     }
     store(dest(0, erased(0)), acc);
     return;
@@ -728,10 +717,8 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
   // 4 waves per SIMD at 1200 B (window 10: 153, 3 waves; 5-erasure decode 4.73 vs 4.28-4.50
   // TB/s, profiles/r01_probe_decode_window.txt).  The first window is in flight with the
   // table loads.
-  // kProbeWindowed: the same windowed straight-line body with the tables read from the
-  // record (scalar loads) instead of LDS (probes).
-  constexpr bool kWinPath = kLds || (POL & kProbeWindowed) != 0;
-  constexpr int kWinW = (POL & kProbeWin10) != 0 ? 10 : (POL & kProbeWin14) != 0 ? 14 : 6;
+  constexpr bool kWinPath = kLds;
+  constexpr int kWinW = 6;
   constexpr int kWin = kWinPath ? (K < kWinW ? K : kWinW) : K;
   uint32_t x[K][NW];
 #pragma unroll
@@ -823,7 +810,7 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
     for (int m = 0; m < MAXE; ++m) {
       if (m0 + m < e) {
         const Tab& t = rt[m * K + s];
-        if (((POL & kProbeXorOnly) != 0) || t.coef == 1u) {
+        if (t.coef == 1u) {
 #pragma unroll
           for (int q = 0; q < NW; ++q) acc[m][q] ^= x[s][q];
         } else if (t.coef != 0u) {
@@ -832,9 +819,6 @@ __device__ __forceinline__ void fused_group(uint64_t gw, uint64_t m, uint32_t la
         }
       }
     }
-  }
-  if constexpr ((POL & kProbeNoStore) != 0) {
-    if (acc[0][0] != 0x9E3779B9u || acc[MAXE - 1][NW - 1] != 0x7F4A7C15u) return;
   }
 #pragma unroll
   for (int m = 0; m < MAXE; ++m)

@@ -204,19 +204,6 @@ int main(int argc, char** argv) {
                        a.binom, a.meta, a.rec_off, a.status);
     return hipSuccess;
   };
-#define PV(NAME, CAP, POLX, NM, NT)                                                              \
-  vars.push_back({NAME, kDecodeFused, CAP, 1, {}, [probe](const DecodeLaunch& a) {               \
-                    probe(a);                                                                    \
-                    return run_decode_fused<10, 3, kNtStore | (POLX), NM, NT>(a, nullptr);       \
-                  }});
-#define PSET(NM, NT)                                                                             \
-  PV("xor-only math", -1, kProbeXorOnly, NM, NT)                                                 \
-  PV("reads only (xor)", -1, kProbeNoStore | kProbeXorOnly, NM, NT)                              \
-  PV("reads dense", -1, kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)                     \
-  PV("reads dense cap8", 8, kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)                 \
-  PV("reads dense cap12", 12, kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)               \
-  PV("reads dense cap16", 16, kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)               \
-  PV("reads dense nt-load", -1, kNtLoad | kProbeNoStore | kProbeXorOnly | kProbeDense, NM, NT)
   if (P < 1024) vars.push_back({"tiled nt", kDecodeTiledNt, -1, -1, {}});
 #define PF(NAME, NT)                                                                             \
   {                                                                                              \
@@ -255,9 +242,6 @@ int main(int argc, char** argv) {
     PVD("pol direct nt-load", -1, kNtLoad, 1, 1)
     PVD("pol direct plain", -1, 0, 1, 1)
     PVD("pol direct nt-load+store cap12", 12, kNtStore | kNtLoad, 1, 1)
-    PVD("pol direct reads-only", -1, kProbeNoStore | kProbeXorOnly, 1, 1)
-    PVD("pol direct reads-only nt-load", -1, kNtLoad | kProbeNoStore | kProbeXorOnly, 1, 1)
-    PVD("pol dense reads-only", -1, kProbeNoStore | kProbeXorOnly | kProbeDense, 1, 1)
     vars.push_back({"pol encode (same buffers)", kDecodeFused, -1, 1, {}, [el](const DecodeLaunch&) {
                       return launch_encode(el, nullptr);  // rewrites identical parity
                     }});
@@ -267,11 +251,6 @@ int main(int argc, char** argv) {
                       b.out = oop;
                       return run_decode_fused<10, 3, kNtStore, 1, 1, true>(b, nullptr);
                     }});
-    PSET(1, 1)
-  } else if (k == 10 && r == 3 && P == 1024) {
-    PSET(1, 0)
-  } else if (k == 10 && r == 3 && P == 2048) {
-    PSET(2, 0)
   }
   // rebuilt packets written out of place, compact (group g's rows at (g*3+m)*P): the write
   // pattern of encode's parity instead of scattered in-place packets.  Unchecked (out of place).
@@ -319,14 +298,6 @@ int main(int argc, char** argv) {
   if (k == 10 && r == 3 && P == 1200) {
     PSCAN(2) PSCAN(4) PSCAN(8) PSCAN(16) PSCAN(32) PSCAN(64)
     PSCAN(256) PSCAN(512) PSCAN(1024)
-    // sparse-loss ceilings of the same access pattern: survivor reads alone (no stores, XOR
-    // math), and XOR math with the stores (mismatch by design: rows 1.. not multiplied)
-    vars.push_back({"scan8 reads-only", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
-                      return run_decode_fused<10, 3, kNtLoad | kProbeNoStore | kProbeXorOnly, 1, 1, true, true, 8>(a, nullptr);
-                    }});
-    vars.push_back({"scan8 xor-math", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
-                      return run_decode_fused<10, 3, kNtStore | kNtLoad | kProbeXorOnly, 1, 1, true, true, 8>(a, nullptr);
-                    }});
     vars.push_back({"scan8 compact-out", kDecodeFused, -1, 1, {}, [cout](const DecodeLaunch& a) {
                       DecodeLaunch b = a;
                       b.out = cout;
@@ -344,14 +315,6 @@ int main(int argc, char** argv) {
     vars.push_back({"lds-tabs nt-load", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) { \
                       probe(a);                                                                   \
                       return run_decode_fused<KK, RR, kNtStore | kNtLoad | kLdsTabs, NMM, NTT, false>(a, nullptr); \
-                    }});                                                                          \
-    vars.push_back({"lds-tabs win10", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {    \
-                      probe(a);                                                                   \
-                      return run_decode_fused<KK, RR, kNtStore | kLdsTabs | kProbeWin10, NMM, NTT, false>(a, nullptr); \
-                    }});                                                                          \
-    vars.push_back({"lds-tabs win14", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {   \
-                      probe(a);                                                                   \
-                      return run_decode_fused<KK, RR, kNtStore | kLdsTabs | kProbeWin14, NMM, NTT, false>(a, nullptr); \
                     }});                                                                          \
     vars.push_back({"lds-tabs xcd0", kDecodeFused, -1, 0, {}, [probe](const DecodeLaunch& a) {    \
                       probe(a);                                                                   \
@@ -372,22 +335,9 @@ int main(int argc, char** argv) {
                       return run_decode_fused<20, 5, kNtStore | kNtLoad | kLdsTabs | kCoefBytes, 1, 1, false>(b, nullptr);
                     }});
   }
-  // windowed straight-line body (6-deep survivor window) with tables from the record
   if (k == 10 && r == 3 && P == 1200) {
-    vars.push_back({"winbody direct w6", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
-                      return run_decode_fused<10, 3, kNtStore | kNtLoad | kProbeWindowed, 1, 1, true>(a, nullptr);
-                    }});
-    vars.push_back({"winbody direct w10", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
-                      return run_decode_fused<10, 3, kNtStore | kNtLoad | kProbeWindowed | kProbeWin10, 1, 1, true>(a, nullptr);
-                    }});
     vars.push_back({"winbody direct w6 lds", kDecodeFused, -1, 1, {}, [](const DecodeLaunch& a) {
                       return run_decode_fused<10, 3, kNtStore | kNtLoad | kLdsTabs, 1, 1, true>(a, nullptr);
-                    }});
-  }
-  if (k == 20 && r == 5 && P == 1200) {
-    vars.push_back({"winbody scalar-tabs", kDecodeFused, -1, 1, {}, [probe](const DecodeLaunch& a) {
-                      probe(a);
-                      return run_decode_fused<20, 5, kNtStore | kProbeWindowed, 1, 1, false>(a, nullptr);
                     }});
   }
   // runtime-k wave kernel (any k, r): tables through the scalar cache vs through LDS

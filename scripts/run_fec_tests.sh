@@ -13,7 +13,8 @@
 #     -- and is skipped with a note otherwise.  --dry-run prints the exact
 #    commands without running anything.
 # 2. Engine legs (BASELINE.json configs) through bench.py:
-#      C1  k=4 r=2, 256 B, 1k groups      host CPU only (the CPU checker, plumbing; no GPU)
+#      C1  k=4 r=2, 256 B, 1k groups      host CPU: the reference's xor_packets_avx2 (oracle/_ref)
+#                                         timed, byte-compared with the restatement and the GPU
 #      C2  k=10 r=3, 1200 B, 1M groups    encode, device-resident           } bench.py c2c3
 #      C3  same, 2 erasures per group      decode, bit-exact vs the original }
 #      C4  k=20 r=5, 1200 B, 1M groups per GPU, encode                         bench.py c4
@@ -99,20 +100,10 @@ fi
 echo "== build"
 python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1
 
-echo "== C1 (host CPU, k=4 r=2, 256 B, 1k groups)"
-python - <<'EOF' | tee "$OUT/c1.json"
-import json, sys, time
-sys.path.insert(0, "oracle")
-import numpy as np, oracle
-k, r, P, G = 4, 2, 256, 1024
-d = oracle.splitmix_bytes(G * k * P, 0x5EED0001)
-t0 = time.perf_counter(); par = oracle.rs_encode(d, G, k, r, P); t = time.perf_counter() - t0
-row0 = par.reshape(G, r, P)[:, 0, :].reshape(-1)
-xr = np.concatenate([oracle.xor_packets([d[(g*k+j)*P:(g*k+j+1)*P] for j in range(k)], P) for g in range(G)])
-ref = oracle.ref_lib()
-print(json.dumps({"config": "C1", "k": k, "r": r, "P": P, "groups": G, "encode_GiBps": round(G*k*P/t/2**30, 3),
-                  "row0_equals_xor": bool((row0 == xr).all()), "reference_lib_present": ref is not None}))
-EOF
+echo "== C1 (host CPU via the reference's AVX2 path: k=4 r=2, 256 B, 1k groups)"
+# oracle/_ref's xor_packets_avx2 timed and byte-compared with the restatement (and with
+# libfec_hip.so when a GPU is usable); scripts/c1_leg.py
+python scripts/c1_leg.py $([ "$CPU_ONLY" = "1" ] && echo --no-gpu) | tee "$OUT/c1.json"
 [ "$CPU_ONLY" = "1" ] && exit 0
 
 run_bench() {

@@ -35,3 +35,18 @@ def test_campaign_quic_leg_skips_without_binary(tmp_path):
     r = subprocess.run(["bash", str(SCRIPT), "--quic-only", "--out", str(tmp_path)], capture_output=True,
                        text=True, timeout=60, env={"PATH": "/usr/bin:/bin", "QUIC_TEST_BIN": str(tmp_path / "none")})
     assert r.returncode == 0 and "skipped" in r.stderr
+
+
+def test_c1_leg_runs_reference_avx2_path():
+    """C1 (BASELINE configs[0]): the reference's xor_packets_avx2 from oracle/_ref (when built
+    here) byte-equal to the restatement; GPU part off on this CPU container."""
+    import json
+    import sys
+    r = subprocess.run([sys.executable, str(REPO / "scripts" / "c1_leg.py"), "--no-gpu"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["config"] == "C1" and (out["k"], out["r"], out["P"], out["groups"]) == (4, 2, 256, 1024)
+    assert out["restatement_row0_equals_xor"]
+    if out["reference_lib_present"]:
+        assert out["reference_xor_avx2_equals_restatement"] and out["reference_xor_avx2_GiBps"] > 0

@@ -132,3 +132,40 @@ def test_bench_decode_api_shapes():
     assert not bench.packed_supported(10, 3, 200)       # tiled form (P <= 256)
     assert not bench.packed_supported(10, 3, 2048)      # no fused piece layout past 2047 B
     assert not bench.packed_supported(6, 3, 1200)       # runtime-k wave kernel
+
+
+def test_visible_gpus_without_hip(tmp_path):
+    """The spawning parent counts GPUs from the KFD topology and the *_VISIBLE_DEVICES lists,
+    never through the HIP runtime."""
+    import bench
+    nodes = tmp_path / "nodes"
+    for i, gid in enumerate((0, 4321, 8765, 0, 1111)):      # CPU nodes have gpu_id 0
+        (nodes / str(i)).mkdir(parents=True)
+        (nodes / str(i) / "gpu_id").write_text(f"{gid}\n")
+    assert bench.visible_gpus({}, str(nodes)) == 3
+    assert bench.visible_gpus({"HIP_VISIBLE_DEVICES": "1"}, str(nodes)) == 1
+    assert bench.visible_gpus({"ROCR_VISIBLE_DEVICES": "0,2", "HIP_VISIBLE_DEVICES": "0,1"}, str(nodes)) == 2
+    assert bench.visible_gpus({"ROCR_VISIBLE_DEVICES": ""}, str(nodes)) == 0
+    assert bench.visible_gpus({"CUDA_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7"}, str(tmp_path / "absent")) == 8
+    assert bench.visible_gpus({}, str(tmp_path / "absent")) == 0
+
+
+def test_spawn_parent_never_maps_hip_runtime():
+    """`bench.py --gpus 2` under RCCL: the parent checks the device count and starts the ranks
+    with libamdhip64 unmapped (spawn_ranks refuses otherwise); here the ranks run the gloo
+    launch self-test."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "QUICFEC_DIST_BACKEND")}
+    env["HIP_VISIBLE_DEVICES"] = "0,1"
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--launch-selftest"],
+                         env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["n_gpus"] == 2
+    # a parent that did load the runtime (torch) is refused before any rank starts
+    code = ("import sys; sys.path.insert(0, %r); import torch, bench; bench.spawn_ranks(2, ['--launch-selftest'])"
+            % str(REPO))
+    bad = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+    assert bad.returncode != 0 and "HIP runtime" in bad.stderr
