@@ -515,6 +515,13 @@ def packed_supported(k: int, r: int, P: int) -> bool:
     return ((k == 10 and r <= 3) or (k == 4 and r == 2)) and 256 < P < 2048
 
 
+def pmc_key(kernel: str, api: str) -> str:
+    """Key of a kernel's entry in profiles/pmc_<config>.json (scripts/pmc_summary.py --tag)."""
+    if kernel != "decode":
+        return kernel
+    return {"packed": "recover_packed", "recover": "recover_slots"}.get(api, "decode")
+
+
 def lib_sha256() -> str:
     """Hash of the libfec_hip.so this process loads (the build being timed)."""
     import hashlib
@@ -564,6 +571,8 @@ def main() -> int:
                          "default stream, as round-1/2 benches did (A/B of the timing setup)")
     ap.add_argument("--parity-offset", type=int, default=0, help="parity buffer placement (bytes past an allocation start)")
     ap.add_argument("--rebuilt-offset", type=int, default=0, help="rebuilt-packet buffer placement (bytes)")
+    ap.add_argument("--no-other-api", action="store_true",
+                    help="skip the comparison run of the other decode API (PMC passes keyed per API)")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -763,7 +772,8 @@ def main() -> int:
         other = {"packed": "recover", "recover": "in-place"}.get(api, "recover")
         if other == "recover" and rebuilt is None:
             rebuilt = dev_buffer(G * r * P, args.rebuilt_offset)
-        kernels["decode"]["other_api"] = {"api": other, **isolated(lambda: decode_call(other), dec_bytes)}
+        if not args.no_other_api:
+            kernels["decode"]["other_api"] = {"api": other, **isolated(lambda: decode_call(other), dec_bytes)}
     # The box's own HBM copy rate (fec_copy_dev: the encode's 16-B-per-lane pattern, no
     # arithmetic), measured the same way: box-to-box spread is a few percent, so the kernels
     # are also quoted against it.
@@ -779,7 +789,8 @@ def main() -> int:
     roofline = {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["achieved_GBps"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(kernels[dom]["achieved_GBps"] / HBM_PEAK_GBS, 4),
-                "traffic": pmc.get("recover" if dom == "decode" and recover else dom, {}).get("hbm_bytes_per_launch"),
+                # PMC entries are keyed per decode API (recover_packed / recover_slots / decode)
+                "traffic": pmc.get(pmc_key(dom, api) if cfg["decode"] else dom, {}).get("hbm_bytes_per_launch"),
                 "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes"],
                 "traffic_source": pmc_note,
                 "read_frac": round(dom_read / (kernels[dom]["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

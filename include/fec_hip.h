@@ -281,6 +281,9 @@ typedef struct {
   uint64_t batches;    /* launches */
   uint64_t max_batch;  /* groups in the largest launch */
   uint64_t max_calls;  /* calls in the largest launch */
+  uint64_t close_ns;   /* sums over launches: leader waiting for the batch's address writes, */
+  uint64_t launch_ns;  /*   the launch calls, */
+  uint64_t done_ns;    /*   and launch until the leader saw the batch complete */
 } FECCoalesceStats;
 
 /* Process-wide totals over every device and packet size; reset = 1 zeroes them after the read. */

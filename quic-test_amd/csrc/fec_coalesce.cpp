@@ -119,6 +119,13 @@ struct Batch {
 };
 
 std::atomic<uint64_t> g_calls{0}, g_groups{0}, g_batches{0}, g_max_batch{0}, g_max_calls{0};
+std::atomic<uint64_t> g_close_ns{0}, g_launch_ns{0}, g_done_ns{0};
+
+uint64_t now_ns() {
+  return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                   std::chrono::steady_clock::now().time_since_epoch())
+                                   .count());
+}
 
 void atomic_max(std::atomic<uint64_t>& a, uint64_t v) {
   uint64_t cur = a.load(std::memory_order_relaxed);
@@ -215,9 +222,9 @@ class Coalescer {
         spins = 0;
         continue;
       }
-      if (spins < 256) {
+      if (spins < spin_pause) {
         for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
-      } else if (spins < 4096) {
+      } else if (spins < spin_pause + spin_yield) {
         std::this_thread::yield();
       } else {
         lk.lock();
@@ -248,6 +255,9 @@ class Coalescer {
   int open = -1;                    // the batch taking callers, -1 while none is free
   std::atomic<int> inflight{0};     // batches closed by a leader and not done yet
   bool staging_ready = false;
+  // waiting callers' spin budget before they sleep (pause rounds, then yields)
+  uint32_t spin_pause = static_cast<uint32_t>(env_long("QUICFEC_COALESCE_SPIN_PAUSE", 256));
+  uint32_t spin_yield = static_cast<uint32_t>(env_long("QUICFEC_COALESCE_SPIN_YIELD", 3840));
 
   // Opens a free batch for new callers, if there is one.  Caller holds mu.
   void open_free() {
@@ -274,13 +284,17 @@ class Coalescer {
     inflight.fetch_add(1, std::memory_order_acq_rel);
     const uint32_t n = b.used, calls = b.calls;  // closed: no more reservations
     lk.unlock();
+    const uint64_t t0 = now_ns();
     while (b.copying.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
     b.state.store(Batch::kLaunched, std::memory_order_relaxed);
+    const uint64_t t1 = now_ns();
     int rc = encode_addr_batch(ctx, reinterpret_cast<const uint64_t*>(b.addr.dev), n, kPackets, 1, P, b.out.dev, stream);
     std::string err;
+    uint64_t t2 = t1;
     if (rc == FEC_OK) {
       BindDevice bd(device);
       hipError_t e = bd.ok ? hipEventRecord(b.done, stream) : hipErrorInvalidDevice;
+      t2 = now_ns();
       // poll (a blocking wait adds its wake-up to every batch); yield once it takes a while
       for (uint32_t i = 0; e == hipSuccess; ++i) {
         e = hipEventQuery(b.done);
@@ -300,6 +314,10 @@ class Coalescer {
     } else {
       err = fec_hip_last_error();
     }
+    const uint64_t t3 = now_ns();
+    g_close_ns.fetch_add(t1 - t0, std::memory_order_relaxed);
+    g_launch_ns.fetch_add(t2 - t1, std::memory_order_relaxed);
+    g_done_ns.fetch_add(t3 - t2, std::memory_order_relaxed);
     g_batches.fetch_add(1, std::memory_order_relaxed);
     g_calls.fetch_add(calls, std::memory_order_relaxed);
     g_groups.fetch_add(n, std::memory_order_relaxed);
@@ -358,7 +376,13 @@ QFEC_EXPORT int fec_coalesce_stats(FECCoalesceStats* out, int reset) {
   out->batches = g_batches.load();
   out->max_batch = g_max_batch.load();
   out->max_calls = g_max_calls.load();
+  out->close_ns = g_close_ns.load();
+  out->launch_ns = g_launch_ns.load();
+  out->done_ns = g_done_ns.load();
   if (reset) {
+    g_close_ns = 0;
+    g_launch_ns = 0;
+    g_done_ns = 0;
     g_calls = 0;
     g_groups = 0;
     g_batches = 0;

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-launch HBM bytes.
 
-    python scripts/pmc_summary.py <fetch_dir> <write_dir> <config> [out.json]
+    python scripts/pmc_summary.py <fetch_dir> <write_dir> <config> [out.json] [--tag NAME]
+
+--tag NAME: the run timed one decode API only (bench.py --decode-api X --no-other-api), so its
+recover kernel is stored as "recover_NAME" (packed / slots) and merged into an existing out.json
+of the same build, which then holds one entry per API.
 
 Corrections (MI355X_MICROARCH.md §HBM and cdna_hip_programming.md §7):
   * FETCH_SIZE / WRITE_SIZE are in KiB;
@@ -50,8 +54,14 @@ def short(name: str) -> str:
 
 
 def main():
-    fdir, wdir, config = Path(sys.argv[1]), Path(sys.argv[2]), sys.argv[3]
-    out = Path(sys.argv[4]) if len(sys.argv) > 4 else Path(__file__).resolve().parents[1] / "profiles" / f"pmc_{config}.json"
+    argv = sys.argv[1:]
+    tag = None
+    if "--tag" in argv:
+        i = argv.index("--tag")
+        tag = argv[i + 1]
+        del argv[i:i + 2]
+    fdir, wdir, config = Path(argv[0]), Path(argv[1]), argv[2]
+    out = Path(argv[3]) if len(argv) > 3 else Path(__file__).resolve().parents[1] / "profiles" / f"pmc_{config}.json"
     fetch = collect(fdir, "FETCH_SIZE")
     write = collect(wdir, "WRITE_SIZE")
     import hashlib
@@ -60,8 +70,14 @@ def main():
            "correction": "FETCH_SIZE x2 (gfx950 wide-stream read), KiB -> bytes",
            # bench.py uses these bytes only while the loaded library is this build
            "lib_sha256": hashlib.sha256(lib.read_bytes()).hexdigest()}
+    if tag and out.exists():
+        prev = json.loads(out.read_text())
+        if prev.get("lib_sha256") == res["lib_sha256"]:
+            res = {**prev, **res}
     for name in set(fetch) | set(write):
         s = short(name)
+        if tag and s == "recover":
+            s = f"recover_{tag}"
         f = fetch.get(name, [])
         w = write.get(name, [])
         fk = sorted(f)[len(f) // 2] if f else None

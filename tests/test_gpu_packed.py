@@ -186,3 +186,66 @@ def test_chunked_launches(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, api, k, 
         oracle_mod.rs_decode(ref, par, masks, G, k, r, P, nthreads=8)
         assert np.array_equal(dd.cpu().numpy(), ref)
     assert np.array_equal(st.cpu().numpy(), st_exp)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("profile", ["c3_two_erasures", "c5_satellite_iid"])
+def test_full_size_packed_recover(gpu_ctx, oracle_mod, torch_cuda, profile):
+    """The bench's decode API at BASELINE size (1M groups of k=10 r=3, 1200 B): C3 (2 erased
+    shards per group) and C5 (iid loss 0.01 per shard, the scan form via the loss hint).  The
+    whole packed list against the original packets, row starts against a host prefix sum,
+    sampled groups against the oracle's decode (decoder.go:29-34's Recovered list shape)."""
+    torch = torch_cuda
+    k, r, P, G = 10, 3, 1200, 1_000_000
+    data = torch.empty(G * k * P, dtype=torch.uint8, device="cuda")
+    par = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_random_dev(data, data.numel(), SEED + 11)
+    gpu_ctx.encode_dev(data, G, k, r, P, par)
+    rng = np.random.default_rng(SEED + 12)
+    if profile == "c3_two_erasures":
+        pos = np.argsort(rng.random((G, k + r)), axis=1)[:, :2].astype(np.uint64)
+        masks = np.left_shift(np.uint64(1), pos).sum(axis=1, dtype=np.uint64)
+    else:
+        w = np.left_shift(np.uint64(1), np.arange(k + r, dtype=np.uint64))
+        masks = ((rng.random((G, k + r)) < 0.01) * w).sum(axis=1, dtype=np.uint64)
+        gpu_ctx.decode_loss_hint(1.0 - 0.99 ** k)
+    try:
+        orig = data.clone()
+        dm = torch.from_numpy(masks.view(np.int64)).cuda()
+        bits = torch.arange(k, device="cuda", dtype=torch.int64)
+        lost = ((dm.view(G, 1) >> bits.view(1, k)) & 1).bool()
+        data.view(G, k, P)[lost] = 0xEE
+        out = torch.full((G * r * P,), 0x5A, dtype=torch.uint8, device="cuda")
+        rs = torch.zeros(G, dtype=torch.int32, device="cuda")
+        tot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+        st = torch.full((G,), 7, dtype=torch.uint8, device="cuda")
+        gpu_ctx.recover_packed_dev(data, par, dm, G, k, r, P, out, rs, tot, st)
+        gpu_ctx.synchronize()
+        lost_h = ((masks[:, None] >> np.arange(k, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+        plost = ((masks[:, None] >> np.arange(k, k + r, dtype=np.uint64)[None, :]) & np.uint64(1)).sum(axis=1)
+        e = lost_h.sum(axis=1)
+        ok = e <= r - plost
+        rows = np.where(ok, e, 0)
+        start = np.concatenate([[0], np.cumsum(rows)[:-1]]).astype(np.uint32)
+        n = int(rows.sum())
+        assert int(tot.item()) == n
+        assert np.array_equal(rs.cpu().numpy().view(np.uint32), start)
+        assert np.array_equal(st.cpu().numpy(), (~ok).astype(np.uint8))
+        okd = torch.from_numpy(ok).cuda()
+        want = orig.view(G, k, P)[lost & okd.view(G, 1)]         # (g, j ascending) order
+        assert want.shape[0] == n
+        assert torch.equal(out.view(-1, P)[:n], want)
+        assert bool((out.view(-1, P)[n:] == 0x5A).all())
+        # sampled groups through the oracle's own decode
+        cand = np.nonzero(rows > 0)[0]
+        for g in [int(x) for x in rng.choice(cand, size=min(48, len(cand)), replace=False)]:
+            blk = data[g * k * P:(g + 1) * k * P].cpu().numpy().copy()
+            pb = par[g * r * P:(g + 1) * r * P].cpu().numpy()
+            oracle_mod.rs_decode(blk, pb, masks[g:g + 1].copy(), 1, k, r, P)
+            ids = np.nonzero(lost_h[g])[0]
+            got = out.view(-1, P)[int(start[g]):int(start[g]) + len(ids)].cpu().numpy()
+            assert np.array_equal(got, blk.reshape(k, P)[ids]), g
+        # the data stays as received (recover reads it only)
+        assert bool((data.view(G, k, P)[lost] == 0xEE).all())
+    finally:
+        gpu_ctx.decode_loss_hint(-1.0)
