@@ -266,6 +266,10 @@ int fec_batcher_stats(FECBatcher* b, FECBatcherStats* out);
 const char* fec_batcher_last_error(void);
 
 /* ---- legacy-call coalescing (fec_coalesce.cpp) ----
+ * Calls from page-locked slabs (fec_alloc_slab, as the Go wrapper packs them) of 1..8 groups
+ * go to a resident encoder instead: one workgroup per device that stays launched while calls
+ * keep coming and serves a ring of submission slots in page-locked memory, so a call costs no
+ * kernel launch (QUICFEC_RESIDENT=0 turns it off).  The rest:
  * The reference's unchanged call site encodes one group per fec_encode_batch call, each stream
  * on its own context (encoder_hybrid.go:115 via fec_cgo.go:138, client.go:783).  Host-resident
  * legacy calls of at most QUICFEC_COALESCE_MAX_GROUPS groups (default 64) are joined, across
@@ -284,6 +288,8 @@ typedef struct {
   uint64_t close_ns;   /* sums over launches: leader waiting for the batch's address writes, */
   uint64_t launch_ns;  /*   the launch calls, */
   uint64_t done_ns;    /*   and launch until the leader saw the batch complete */
+  uint64_t resident_calls;     /* legacy calls served by the resident encoder instead */
+  uint64_t resident_launches;  /* instances of the resident encoder launched */
 } FECCoalesceStats;
 
 /* Process-wide totals over every device and packet size; reset = 1 zeroes them after the read. */

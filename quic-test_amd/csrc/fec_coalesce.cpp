@@ -27,6 +27,20 @@
 //
 // QUICFEC_COALESCE=0 turns it off; QUICFEC_COALESCE_MAX_GROUPS (default 64) bounds the calls
 // it takes; QUICFEC_COALESCE_INFLIGHT (default 2) the batches in flight per coalescer.
+//
+// Resident server (the default for the Go wrapper's calls: page-locked slab, 1..8 groups, P >=
+// 16).  A launch per batch costs the leader ~6-9 us of HIP API time and ~12 us until it sees
+// the completion (profiles/r03_legacy_v3_tuning.jsonl), so batching alone only matches the
+// per-context path.  Instead one workgroup stays resident on each device and serves a ring of
+// submission slots in page-locked coherent host memory (fec_kernels.hpp ServerSlot,
+// legacy_server): a caller takes a sequence number, writes its packets' device addresses and
+// its repair rows' address into slot seq % kServerSlots, publishes it (release store of
+// ready = seq + 1) and polls the slot's done word; the workgroup takes every published slot in
+// order each time it polls, so concurrent callers share one pass without any host-side batch.
+// No kernel launch per call: the resident instance leaves after QUICFEC_RESIDENT_IDLE_US
+// (default 2000) without work or QUICFEC_RESIDENT_LIFE_US (default 50000) of life, and the next
+// caller that finds it gone (its `exited` word equals the instance's generation) launches the
+// next one from the served-up-to mark (`progress`).  QUICFEC_RESIDENT=0 turns it off.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,6 +59,7 @@
 
 #include "fec_hip.h"
 #include "fec_internal.hpp"
+#include "fec_kernels.hpp"
 
 #define QFEC_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -334,8 +349,182 @@ class Coalescer {
   }
 };
 
+// Page-locked host memory the device reads and writes coherently (polling and flags).
+bool alloc_coherent(Pinned& m, size_t bytes) {
+  void* h = nullptr;
+  if (hipHostMalloc(&h, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  std::memset(h, 0, bytes);
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || d == nullptr) {
+    (void)hipGetLastError();
+    d = h;
+  }
+  m.host = static_cast<uint8_t*>(h);
+  m.dev = static_cast<uint8_t*>(d);
+  return true;
+}
+
+constexpr uint32_t kResidentOutBytes = 16u << 10;  // per slot: repair rows of callers whose buffer is pageable
+
+std::atomic<uint64_t> g_res_calls{0}, g_res_launches{0};
+
+class Resident {
+ public:
+  static Resident* create(int device) {
+    std::unique_ptr<Resident> r(new Resident());
+    r->device = device;
+    BindDevice bd(device);
+    int khz = 0;
+    if (!bd.ok || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0 ||
+        hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    const uint64_t per_us = static_cast<uint64_t>(khz) / 1000u;
+    r->idle_ticks = per_us * static_cast<uint64_t>(std::max(10L, env_long("QUICFEC_RESIDENT_IDLE_US", 2000)));
+    r->life_ticks = per_us * static_cast<uint64_t>(std::max(100L, env_long("QUICFEC_RESIDENT_LIFE_US", 50000)));
+    if (!alloc_coherent(r->ring, sizeof(ServerSlot) * kServerSlots) ||
+        !alloc_coherent(r->done, sizeof(uint64_t) * kServerSlots) || !alloc_coherent(r->ctl, sizeof(ServerControl)) ||
+        !alloc_coherent(r->outs, size_t(kResidentOutBytes) * kServerSlots))
+      return nullptr;
+    r->collected.reset(new std::atomic<uint64_t>[kServerSlots]);
+    for (uint32_t i = 0; i < kServerSlots; ++i) r->collected[i].store(0, std::memory_order_relaxed);
+    return r.release();
+  }
+
+  // Whether a call of G groups of P bytes fits a slot (repair rows staged in the slot unless
+  // the caller's buffer is page-locked).
+  static bool fits(uint32_t G, uint32_t P, bool repair_pinned) {
+    return G >= 1 && G <= kServerMaxGroups && P >= 16 && (repair_pinned || uint64_t(G) * P <= kResidentOutBytes);
+  }
+
+  int encode(const uint8_t* slab_dev, const uint32_t* offsets, uint32_t G, uint32_t P, uint8_t* repair_out,
+             uint8_t* repair_dev) {
+    const uint64_t seq = next_seq.fetch_add(1, std::memory_order_relaxed);
+    const uint32_t si = static_cast<uint32_t>(seq % kServerSlots);
+    // the slot's previous occupant (seq - kServerSlots) has been collected
+    for (uint32_t spins = 0; seq >= kServerSlots && collected[si].load(std::memory_order_acquire) != seq - kServerSlots + 1;
+         ++spins)
+      backoff(spins);
+    ServerSlot* sl = reinterpret_cast<ServerSlot*>(ring.host) + si;
+    sl->groups = G;
+    sl->P = P;
+    uint8_t* out_dev = repair_dev ? repair_dev : outs.dev + size_t(si) * kResidentOutBytes;
+    sl->out = reinterpret_cast<uint64_t>(out_dev);
+    const uint64_t base = reinterpret_cast<uint64_t>(slab_dev);
+    for (uint32_t i = 0; i < G * kServerPackets; ++i) sl->addr[i] = base + offsets[i];
+    __atomic_store_n(&sl->ready, seq + 1, __ATOMIC_RELEASE);
+    g_res_calls.fetch_add(1, std::memory_order_relaxed);
+    int rc = FEC_OK;
+    const uint64_t* dw = reinterpret_cast<const uint64_t*>(done.host) + si;
+    const auto t_fail = std::chrono::steady_clock::now() + std::chrono::seconds(10);
+    for (uint32_t spins = 0;; ++spins) {
+      if (__atomic_load_n(dw, __ATOMIC_ACQUIRE) == seq + 1) break;
+      // no instance serving (never launched, or it left): launch one from its progress mark
+      if ((spins & 15u) == 0 && !instance_alive()) {
+        rc = relaunch();
+        if (rc != FEC_OK) break;
+      }
+      if ((spins & 1023u) == 1023u && std::chrono::steady_clock::now() > t_fail) {
+        set_last_error("fec_encode_batch: the resident encoder did not serve the call within 10 s");
+        rc = FEC_ERR_HIP;
+        break;
+      }
+      backoff(spins);
+    }
+    if (rc != FEC_OK) {
+      // never served: withdraw the slot (no instance may serve it later into the caller's
+      // buffer) -- only safe while none runs, which is the case on every failure path above
+      __atomic_store_n(&sl->ready, 0, __ATOMIC_RELEASE);
+    } else if (!repair_dev) {
+      std::memcpy(repair_out, outs.host + size_t(si) * kResidentOutBytes, size_t(G) * P);
+    }
+    collected[si].store(seq + 1, std::memory_order_release);
+    return rc;
+  }
+
+  // Process exit: ask the running instance to leave and give it a moment (no HIP calls).
+  void shutdown() {
+    __atomic_store_n(&reinterpret_cast<ServerControl*>(ctl.host)->stop, 1, __ATOMIC_RELEASE);
+    const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
+    while (instance_alive() && std::chrono::steady_clock::now() < until) std::this_thread::yield();
+  }
+
+ private:
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint64_t idle_ticks = 0, life_ticks = 0;
+  Pinned ring, done, ctl, outs;
+  std::unique_ptr<std::atomic<uint64_t>[]> collected;  // per slot: seq + 1 of its last collected call
+  std::atomic<uint64_t> next_seq{0};
+  std::mutex mu;
+  std::atomic<uint64_t> gen{0};  // generation of the last launched instance (0 = none yet)
+
+  static void backoff(uint32_t spins) {
+    if (spins < 2048) {
+      for (int i = 0; i < 8; ++i) __builtin_ia32_pause();
+    } else if (spins < 16384) {
+      std::this_thread::yield();
+    } else {
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+
+  bool instance_alive() const {
+    const uint64_t g = gen.load(std::memory_order_acquire);
+    return g != 0 && __atomic_load_n(&reinterpret_cast<const ServerControl*>(ctl.host)->exited, __ATOMIC_ACQUIRE) != g;
+  }
+
+  // Launches the next instance unless another caller just did.
+  int relaunch() {
+    std::lock_guard<std::mutex> lk(mu);
+    if (instance_alive()) return FEC_OK;
+    const ServerControl* c = reinterpret_cast<const ServerControl*>(ctl.host);
+    if (__atomic_load_n(&c->stop, __ATOMIC_ACQUIRE)) {
+      set_last_error("fec_encode_batch: the resident encoder is shutting down");
+      return FEC_ERR_HIP;
+    }
+    const uint64_t start = __atomic_load_n(&c->progress, __ATOMIC_ACQUIRE);
+    const uint64_t g = gen.load(std::memory_order_relaxed) + 1;
+    BindDevice bd(device);
+    const hipError_t e = bd.ok ? launch_legacy_server(reinterpret_cast<const ServerSlot*>(ring.dev),
+                                                      reinterpret_cast<uint64_t*>(done.dev),
+                                                      reinterpret_cast<ServerControl*>(ctl.dev), start, g, idle_ticks,
+                                                      life_ticks, stream)
+                               : hipErrorInvalidDevice;
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      set_last_error((std::string("fec_encode_batch: resident encoder launch failed: ") + hipGetErrorString(e)).c_str());
+      return FEC_ERR_HIP;
+    }
+    gen.store(g, std::memory_order_release);
+    g_res_launches.fetch_add(1, std::memory_order_relaxed);
+    return FEC_OK;
+  }
+};
+
 std::mutex g_reg_mu;
 std::map<std::pair<int, uint32_t>, Coalescer*> g_reg;  // process lifetime (callers may run at exit)
+std::map<int, Resident*> g_resident;                   // per device; NULL when it cannot be set up
+
+void shutdown_residents() {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (auto& kv : g_resident)
+    if (kv.second) kv.second->shutdown();
+}
+
+Resident* resident_for(int device) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_resident.find(device);
+  if (it != g_resident.end()) return it->second;
+  if (g_resident.empty()) std::atexit(shutdown_residents);
+  Resident* r = Resident::create(device);
+  g_resident.emplace(device, r);
+  return r;
+}
 
 Coalescer* coalescer_for(int device, uint32_t P) {
   std::lock_guard<std::mutex> lk(g_reg_mu);
@@ -359,6 +548,15 @@ bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* off
   if (sm == HostMem::kDevice || classify_host_pointer(offsets, nullptr) == HostMem::kDevice ||
       classify_host_pointer(repair_out, nullptr) == HostMem::kDevice)
     return false;  // device-resident callers batch by themselves
+  void* rdev = nullptr;
+  const bool repair_pinned = classify_host_pointer(repair_out, &rdev) == HostMem::kPinned;
+  if (sm == HostMem::kPinned && env_long("QUICFEC_RESIDENT", 1) != 0 && Resident::fits(num_groups, packet_size, repair_pinned)) {
+    if (Resident* r = resident_for(device)) {
+      *rc = r->encode(static_cast<const uint8_t*>(sdev), offsets, num_groups, packet_size, repair_out,
+                      repair_pinned ? static_cast<uint8_t*>(rdev) : nullptr);
+      return true;
+    }
+  }
   Coalescer* c = coalescer_for(device, packet_size);
   if (!c || num_groups > c->capacity() / 2) return false;
   *rc = c->encode(slab, sm == HostMem::kPinned ? static_cast<const uint8_t*>(sdev) : nullptr, offsets, num_groups,
@@ -379,7 +577,11 @@ QFEC_EXPORT int fec_coalesce_stats(FECCoalesceStats* out, int reset) {
   out->close_ns = g_close_ns.load();
   out->launch_ns = g_launch_ns.load();
   out->done_ns = g_done_ns.load();
+  out->resident_calls = g_res_calls.load();
+  out->resident_launches = g_res_launches.load();
   if (reset) {
+    g_res_calls = 0;
+    g_res_launches = 0;
     g_close_ns = 0;
     g_launch_ns = 0;
     g_done_ns = 0;

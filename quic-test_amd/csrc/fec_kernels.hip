@@ -1338,6 +1338,114 @@ __global__ __launch_bounds__(256) void copy_words(const uint4* __restrict__ src,
   if (t < n16) dst[t] = src[t];
 }
 
+// Resident legacy encoder (fec_kernels.hpp ServerSlot): one workgroup of 16 waves.  Wave 0
+// polls the next 64 slots of the ring with one system-scope acquire load per lane and takes
+// the published run from the next expected seq (slots are served in order), with a prefix of
+// the run's work items (one per 16-B column of a group) in LDS; then every thread takes work
+// items (the group's 10 packet addresses from the slot, 10 loads, XOR, one store to the
+// repair row -- the reference's row 0, fec_xor_simd.cpp:411-427), the workgroup fences its
+// stores at system scope and the slots' done words are stored (release).  Every wave leaves
+// together: at the host's stop flag, after idle_ticks without work, after life_ticks, and in
+// any case after kServerMaxPolls polls.
+constexpr uint32_t kServerThreads = 1024;
+constexpr uint32_t kServerMaxPolls = 1u << 22;
+
+__device__ __forceinline__ uint64_t sys_load_acquire(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void sys_store_release(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot* __restrict__ ring,
+                                                                uint64_t* __restrict__ done,
+                                                                ServerControl* __restrict__ ctl, uint64_t start_seq,
+                                                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks) {
+  __shared__ uint64_t s_next;
+  __shared__ uint32_t s_n, s_exit;
+  __shared__ uint32_t s_first[65];  // work items before slot i of the run
+  __shared__ uint32_t s_P[64], s_cpp[64];
+  __shared__ uint64_t s_out[64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  uint64_t t0 = 0, t_last = 0;  // thread 0 only
+  if (tid == 0) {
+    s_next = start_seq;
+    t0 = t_last = static_cast<uint64_t>(wall_clock64());
+  }
+  __syncthreads();
+  for (uint32_t it = 0; it < kServerMaxPolls; ++it) {
+    if (tid < 64) {
+      const uint64_t next = s_next;
+      const uint64_t seq = next + lane;
+      const ServerSlot* sl = ring + seq % kServerSlots;
+      const bool rdy = sys_load_acquire(&sl->ready) == seq + 1;
+      const uint64_t bal = __ballot(rdy);
+      const uint32_t n = ~bal == 0 ? 64u : static_cast<uint32_t>(__builtin_ctzll(~bal));
+      uint32_t work = 0;
+      if (lane < n) {
+        const uint32_t P = sl->P;
+        const uint32_t cpp = (P + 15u) / 16u;
+        s_P[lane] = P;
+        s_cpp[lane] = cpp;
+        s_out[lane] = sl->out;
+        work = sl->groups * cpp;
+      }
+      uint32_t incl = work;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= static_cast<uint32_t>(d)) incl += y;
+      }
+      s_first[lane + 1] = incl;
+      if (lane == 0) {
+        s_first[0] = 0;
+        const uint64_t now = static_cast<uint64_t>(wall_clock64());
+        if (n > 0) t_last = now;
+        const bool stop = sys_load_acquire(&ctl->stop) != 0;
+        s_n = n;
+        s_exit = (stop || now - t0 > life_ticks || (n == 0 && now - t_last > idle_ticks)) ? 1u : 0u;
+      }
+    }
+    __syncthreads();
+    const uint32_t n = s_n;
+    const bool leave = s_exit != 0;
+    if (n > 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the published slots and packets, every wave
+      const uint64_t next = s_next;
+      const uint32_t total = s_first[n];
+      for (uint32_t w = tid; w < total; w += kServerThreads) {
+        uint32_t i = 0;
+        while (s_first[i + 1] <= w) ++i;
+        const uint32_t local = w - s_first[i];
+        const uint32_t cpp = s_cpp[i], P = s_P[i];
+        const uint32_t g = local / cpp, col = local - g * cpp;
+        const uint32_t coff = col * 16u + 16u <= P ? col * 16u : P - 16u;
+        const uint64_t* ad = ring[(next + i) % kServerSlots].addr + g * kServerPackets;
+        u32x4 acc = ld16<0>(reinterpret_cast<const uint8_t*>(ad[0]) + coff);
+#pragma unroll
+        for (uint32_t j = 1; j < kServerPackets; ++j) acc ^= ld16<0>(reinterpret_cast<const uint8_t*>(ad[j]) + coff);
+        st16<0>(reinterpret_cast<uint8_t*>(s_out[i]) + static_cast<uint64_t>(g) * P + coff, acc);
+      }
+      __threadfence_system();  // this thread's repair rows are visible before any done word
+      __syncthreads();
+      if (tid < n) sys_store_release(&done[(next + tid) % kServerSlots], next + tid + 1);
+      if (tid == 0) {
+        s_next = next + n;
+        sys_store_release(&ctl->progress, next + n);
+      }
+    } else if (!leave) {
+      __builtin_amdgcn_s_sleep(8);
+    }
+    __syncthreads();
+    if (leave) break;
+  }
+  if (tid == 0) {
+    sys_store_release(&ctl->progress, s_next);
+    sys_store_release(&ctl->exited, gen);
+  }
+}
+
 constexpr uint32_t kMaxThreadsPerLaunch = 1u << 30;
 // Wave-per-group decode launches: 256-thread workgroups, so at most 2^22 of them keep the
 // grid's work-item count (blocks * 256) inside 32 bits with room to spare.
@@ -1871,6 +1979,13 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t launch_legacy_server(const ServerSlot* ring, uint64_t* done, ServerControl* ctl, uint64_t start_seq,
+                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s) {
+  hipLaunchKernelGGL(legacy_server, dim3(1), dim3(kServerThreads), 0, s, ring, done, ctl, start_seq, gen, idle_ticks,
+                     life_ticks);
+  return hipGetLastError();
 }
 
 hipError_t launch_copy_words(const uint8_t* src, uint8_t* dst, uint64_t nbytes, hipStream_t s) {

@@ -120,6 +120,35 @@ hipError_t launch_rows_prefix(const uint64_t* masks, uint64_t groups, uint32_t k
 bool decode_needs_rec_off(const DecodeLaunch& a);
 // Whether launch_decode(a) runs a form that reads a compact codebook (coefficient bytes).
 bool decode_compact_tables(const DecodeLaunch& a);
+// ---- resident legacy encoder (fec_coalesce.cpp "resident server") ----
+// A ring of submission slots in page-locked, coherent host memory: the host fills slot
+// (seq % kServerSlots) with a legacy call's groups (absolute device addresses of their 10
+// packets, the repair rows' address) and publishes it by storing `ready` = seq + 1; one
+// resident workgroup polls the ring in order, XORs every published slot's groups and stores
+// done[seq % kServerSlots] = seq + 1.  Calls are served without a kernel launch each.
+constexpr uint32_t kServerSlots = 1024;
+constexpr uint32_t kServerMaxGroups = 8;  // groups per slot (legacy calls of 1..8 groups)
+constexpr uint32_t kServerPackets = 10;   // the legacy call's packets per group
+struct alignas(64) ServerSlot {
+  uint64_t ready;           // seq + 1 once the slot is published (host release store)
+  uint32_t groups, P;       // 1..kServerMaxGroups groups of P >= 16 bytes
+  uint64_t out;             // device address of the groups' repair rows, row g at out + g * P
+  uint64_t pad;
+  uint64_t addr[kServerMaxGroups * kServerPackets];  // packet (g, j) at addr[g * 10 + j]
+};
+struct alignas(64) ServerControl {
+  uint64_t stop;            // host -> device: leave at the next poll
+  uint64_t pad0[7];
+  uint64_t progress;        // device -> host: every seq below this has been served
+  uint64_t exited;          // device -> host: generation of the last instance that left
+  uint64_t pad1[6];
+};
+// One resident workgroup serving the ring from start_seq until it has found nothing to do for
+// idle_ticks, or lived life_ticks (wall-clock ticks, hipDeviceAttributeWallClockRate), or the
+// host sets ctl->stop; on leaving it stores progress and then exited = gen.
+hipError_t launch_legacy_server(const ServerSlot* ring, uint64_t* done, ServerControl* ctl, uint64_t start_seq,
+                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s);
+
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);
 // dst <- src, nbytes a multiple of 16, both 16-B aligned (box calibration).

@@ -495,15 +495,19 @@ int legacy(int S, double rate, double seconds) {
   const double cpu = cpu_seconds() - c0;
   fec_coalesce_stats(&cs, 0);
   const char* co = std::getenv("QUICFEC_COALESCE");
+  const char* res = std::getenv("QUICFEC_RESIDENT");
   char cfg[768];
   std::snprintf(cfg, sizeof(cfg),
                 "\"streams\": %d, \"rate_pps\": %.0f, \"r\": 1, \"coalesce\": %d, \"errors\": %ld, \"go_fallback\": %ld, "
                 "\"coalesced_calls\": %llu, \"launches\": %llu, \"mean_batch\": %.2f, \"max_batch\": %llu, "
-                "\"us_per_launch\": {\"close\": %.2f, \"launch\": %.2f, \"done\": %.2f}",
+                "\"us_per_launch\": {\"close\": %.2f, \"launch\": %.2f, \"done\": %.2f}, \"resident\": %d, "
+                "\"resident_calls\": %llu, \"resident_launches\": %llu",
                 S, rate, co && co[0] == '0' ? 0 : 1, errors.load(), fallback.load(), (unsigned long long)cs.calls,
                 (unsigned long long)cs.batches, cs.batches ? double(cs.groups) / cs.batches : 0.0,
                 (unsigned long long)cs.max_batch, cs.batches ? cs.close_ns / 1e3 / cs.batches : 0.0,
-                cs.batches ? cs.launch_ns / 1e3 / cs.batches : 0.0, cs.batches ? cs.done_ns / 1e3 / cs.batches : 0.0);
+                cs.batches ? cs.launch_ns / 1e3 / cs.batches : 0.0, cs.batches ? cs.done_ns / 1e3 / cs.batches : 0.0,
+                res && res[0] == '0' ? 0 : 1, (unsigned long long)cs.resident_calls,
+                (unsigned long long)cs.resident_launches);
   print_lat("legacy", cfg, all, double(groups), wall, cpu, nullptr);
   return errors || fallback ? 1 : 0;
 }

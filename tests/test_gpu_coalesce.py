@@ -44,10 +44,15 @@ def _run_threads(n, fn):
         raise errs[0]
 
 
-@pytest.mark.parametrize("pinned", [True, False], ids=["pinned_slab", "pageable_slab"])
-def test_concurrent_one_group_calls_match_reference(quicfec_mod, oracle_mod, xor_golden, manifest, pinned, monkeypatch):
-    """16 streams, each with its own context (the Go wrapper's FECEncoderCXX), 1 group per call."""
+@pytest.mark.parametrize("pinned,resident", [(True, True), (True, False), (False, True)],
+                         ids=["pinned_slab_resident", "pinned_slab_batches", "pageable_slab"])
+def test_concurrent_one_group_calls_match_reference(quicfec_mod, oracle_mod, xor_golden, manifest, pinned, resident,
+                                                    monkeypatch):
+    """16 streams, each with its own context (the Go wrapper's FECEncoderCXX), 1 group per call:
+    page-locked slabs go to the resident encoder (QUICFEC_RESIDENT=0: shared launches),
+    pageable ones to shared launches."""
     monkeypatch.setenv("QUICFEC_COALESCE", "1")
+    monkeypatch.setenv("QUICFEC_RESIDENT", "1" if resident else "0")
     c = next(c for c in manifest["cases"] if c["name"] == "batch_k10_p1200_g64")
     G, P = c["G"], c["P"]
     slab = oracle_mod.splitmix_bytes(G * 10 * P, c["seed"])
@@ -84,9 +89,15 @@ def test_concurrent_one_group_calls_match_reference(quicfec_mod, oracle_mod, xor
 
     _run_threads(S, stream)
     st = quicfec_mod.coalesce_stats()
-    assert st["calls"] == S * CALLS and st["groups"] == S * CALLS
-    # calls from different contexts shared launches
-    assert st["batches"] < st["calls"] and st["max_calls"] >= 2, st
+    if pinned and resident:
+        # every call served by the resident encoder (the ring of 1024 slots wrapped), a
+        # launch only when no instance was running
+        assert st["resident_calls"] == S * CALLS and st["calls"] == 0, st
+        assert 1 <= st["resident_launches"] < S * CALLS // 8, st
+    else:
+        assert st["calls"] == S * CALLS and st["groups"] == S * CALLS
+        # calls from different contexts shared launches
+        assert st["batches"] < st["calls"] and st["max_calls"] >= 2, st
 
 
 @pytest.mark.parametrize("P", [8, 17, 100, 1200, 1201, 1500])
@@ -126,7 +137,9 @@ def test_concurrent_mixed_calls_match_oracle(quicfec_mod, oracle_mod, P, monkeyp
 
     _run_threads(S, stream)
     st = quicfec_mod.coalesce_stats()
-    assert st["calls"] == S * 24, st
+    assert st["calls"] + st["resident_calls"] == S * 24, st
+    if P >= 16:
+        assert st["resident_calls"] > 0, st          # pinned calls of <= 8 groups
 
 
 @pytest.mark.parametrize("coalesce", ["0", "1"])
@@ -166,3 +179,56 @@ def test_large_and_device_calls_bypass(gpu_ctx, oracle_mod, quicfec_mod, torch_c
     assert gpu_ctx.encode_batch_legacy(slab, offs, 4, P, rep4) == 0
     assert np.array_equal(rep4, exp[:4 * P])
     assert quicfec_mod.coalesce_stats()["calls"] == 1
+
+
+def test_resident_encoder_leaves_when_idle_and_comes_back(quicfec_mod, oracle_mod, monkeypatch):
+    """The resident instance leaves after its idle time (default 2 ms); the next call launches
+    the next one from the served-up-to mark and is served like the first."""
+    import time
+    monkeypatch.setenv("QUICFEC_COALESCE", "1")
+    monkeypatch.setenv("QUICFEC_RESIDENT", "1")
+    lib = quicfec_mod.load_library()
+    P = 1200
+    ctx = quicfec_mod.Context(device=0)
+    sp, rp = lib.fec_alloc_slab(10 * P), lib.fec_alloc_repair_buffer(P)
+    offs = (np.arange(10, dtype=np.uint32) * P).astype(np.uint32)
+    try:
+        quicfec_mod.coalesce_stats(reset=True)
+        for rnd in range(4):
+            grp = oracle_mod.splitmix_bytes(10 * P, 4242 + rnd)
+            ctypes.memmove(sp, grp.ctypes.data, grp.nbytes)
+            assert lib.fec_encode_batch(ctx.handle, sp, offs.ctypes.data, 1, P, rp) == 0
+            exp = oracle_mod.xor_packets([grp[j * P:(j + 1) * P] for j in range(10)], P)
+            assert np.array_equal(_read(rp, P), exp), rnd
+            time.sleep(0.05)                                   # well past the idle time
+        st = quicfec_mod.coalesce_stats()
+        assert st["resident_calls"] == 4 and st["resident_launches"] == 4, st
+    finally:
+        lib.fec_free_slab(sp)
+        lib.fec_free_repair_buffer(rp)
+        ctx.close()
+
+
+def test_resident_repair_to_pageable_buffer(quicfec_mod, oracle_mod, monkeypatch):
+    """Page-locked slab, pageable repair buffer: rows staged in the slot, copied out; 1..8 groups."""
+    monkeypatch.setenv("QUICFEC_COALESCE", "1")
+    monkeypatch.setenv("QUICFEC_RESIDENT", "1")
+    lib = quicfec_mod.load_library()
+    ctx = quicfec_mod.Context(device=0)
+    quicfec_mod.coalesce_stats(reset=True)
+    try:
+        for G, P in ((1, 16), (3, 1201), (8, 1500), (8, 2048), (5, 333)):
+            slab = oracle_mod.splitmix_bytes(G * 10 * P, 77 + G + P)
+            offs = (np.arange(G * 10, dtype=np.uint32) * P).astype(np.uint32)[::-1].copy()   # any order
+            sp = _pinned_copy(lib, slab)
+            rep = np.full(G * P, 0xEE, dtype=np.uint8)
+            try:
+                assert lib.fec_encode_batch(ctx.handle, sp, offs.ctypes.data, G, P, rep.ctypes.data) == 0
+            finally:
+                lib.fec_free_slab(sp)
+            exp = np.concatenate([oracle_mod.xor_packets([slab[o:o + P] for o in offs[g * 10:(g + 1) * 10]], P)
+                                  for g in range(G)])
+            assert np.array_equal(rep, exp), (G, P)
+        assert quicfec_mod.coalesce_stats()["resident_calls"] == 5
+    finally:
+        ctx.close()
