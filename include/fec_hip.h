@@ -290,6 +290,9 @@ typedef struct {
   uint64_t done_ns;    /*   and launch until the leader saw the batch complete */
   uint64_t resident_calls;     /* legacy calls served by the resident encoder instead */
   uint64_t resident_launches;  /* instances of the resident encoder launched */
+  uint64_t resident_pre_ns;    /* sums over resident calls: entry until the slot was published, */
+  uint64_t resident_wait_ns;   /*   published until its done word was seen, */
+  uint64_t resident_post_ns;   /*   and from there to the return */
 } FECCoalesceStats;
 
 /* Process-wide totals over every device and packet size; reset = 1 zeroes them after the read. */

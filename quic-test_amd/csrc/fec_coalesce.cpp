@@ -34,9 +34,10 @@
 // per-context path.  Instead one workgroup stays resident on each device and serves a ring of
 // submission slots in page-locked coherent host memory (fec_kernels.hpp ServerSlot,
 // legacy_server): a caller takes a sequence number, writes its packets' device addresses and
-// its repair rows' address into slot seq % kServerSlots, publishes it (release store of
-// ready = seq + 1) and polls the slot's done word; the workgroup takes every published slot in
-// order each time it polls, so concurrent callers share one pass without any host-side batch.
+// its repair rows' address into slot seq % kServerSlots, every word tagged with the slot's lap,
+// and polls the slot's done word; the workgroup takes every complete slot in order each time it
+// polls (one PCIe round trip reads the next 64 slots' headers and first groups), so concurrent
+// callers share one pass without any host-side batch.
 // No kernel launch per call: the resident instance leaves after QUICFEC_RESIDENT_IDLE_US
 // (default 2000) without work or QUICFEC_RESIDENT_LIFE_US (default 50000) of life, and the next
 // caller that finds it gone (its `exited` word equals the instance's generation) launches the
@@ -369,7 +370,7 @@ bool alloc_coherent(Pinned& m, size_t bytes) {
 
 constexpr uint32_t kResidentOutBytes = 16u << 10;  // per slot: repair rows of callers whose buffer is pageable
 
-std::atomic<uint64_t> g_res_calls{0}, g_res_launches{0};
+std::atomic<uint64_t> g_res_calls{0}, g_res_launches{0}, g_res_pre_ns{0}, g_res_wait_ns{0}, g_res_post_ns{0};
 
 class Resident {
  public:
@@ -390,6 +391,8 @@ class Resident {
         !alloc_coherent(r->done, sizeof(uint64_t) * kServerSlots) || !alloc_coherent(r->ctl, sizeof(ServerControl)) ||
         !alloc_coherent(r->outs, size_t(kResidentOutBytes) * kServerSlots))
       return nullptr;
+    // no word of a slot that was never written may carry lap 0's tag
+    std::memset(r->ring.host, 0xFF, sizeof(ServerSlot) * kServerSlots);
     r->collected.reset(new std::atomic<uint64_t>[kServerSlots]);
     for (uint32_t i = 0; i < kServerSlots; ++i) r->collected[i].store(0, std::memory_order_relaxed);
     return r.release();
@@ -398,28 +401,37 @@ class Resident {
   // Whether a call of G groups of P bytes fits a slot (repair rows staged in the slot unless
   // the caller's buffer is page-locked).
   static bool fits(uint32_t G, uint32_t P, bool repair_pinned) {
-    return G >= 1 && G <= kServerMaxGroups && P >= 16 && (repair_pinned || uint64_t(G) * P <= kResidentOutBytes);
+    return G >= 1 && G <= kServerMaxGroups && P >= 16 && P <= 0xFFFFu &&
+           (repair_pinned || uint64_t(G) * P <= kResidentOutBytes);
   }
 
   int encode(const uint8_t* slab_dev, const uint32_t* offsets, uint32_t G, uint32_t P, uint8_t* repair_out,
-             uint8_t* repair_dev) {
+             uint8_t* repair_dev, uint64_t t_enter) {
+    uint8_t* out_dev = nullptr;
+    const uint64_t base = reinterpret_cast<uint64_t>(slab_dev);
     const uint64_t seq = next_seq.fetch_add(1, std::memory_order_relaxed);
     const uint32_t si = static_cast<uint32_t>(seq % kServerSlots);
-    // the slot's previous occupant (seq - kServerSlots) has been collected
-    for (uint32_t spins = 0; seq >= kServerSlots && collected[si].load(std::memory_order_acquire) != seq - kServerSlots + 1;
-         ++spins)
-      backoff(spins);
-    ServerSlot* sl = reinterpret_cast<ServerSlot*>(ring.host) + si;
-    sl->groups = G;
-    sl->P = P;
-    uint8_t* out_dev = repair_dev ? repair_dev : outs.dev + size_t(si) * kResidentOutBytes;
-    sl->out = reinterpret_cast<uint64_t>(out_dev);
-    const uint64_t base = reinterpret_cast<uint64_t>(slab_dev);
-    for (uint32_t i = 0; i < G * kServerPackets; ++i) sl->addr[i] = base + offsets[i];
-    __atomic_store_n(&sl->ready, seq + 1, __ATOMIC_RELEASE);
-    g_res_calls.fetch_add(1, std::memory_order_relaxed);
-    int rc = FEC_OK;
+    const uint64_t tag = ((seq / kServerSlots) & 0xFFu) << kServerTagShift;
+    // the slot's previous occupant (seq - kServerSlots) has been served and collected
     const uint64_t* dw = reinterpret_cast<const uint64_t*>(done.host) + si;
+    for (uint32_t spins = 0; seq >= kServerSlots && (collected[si].load(std::memory_order_acquire) != seq - kServerSlots + 1 ||
+                                                     __atomic_load_n(dw, __ATOMIC_ACQUIRE) != seq - kServerSlots + 1);
+         ++spins) {
+      if ((spins & 1023u) == 1023u && !instance_alive() && relaunch() != FEC_OK) break;
+      backoff(spins);
+    }
+    ServerSlot* sl = reinterpret_cast<ServerSlot*>(ring.host) + si;
+    out_dev = repair_dev ? repair_dev : outs.dev + size_t(si) * kResidentOutBytes;
+    // groups after the first, then the first group and the header: the device reads the former
+    // only after it has seen every word of the latter with this lap's tag
+    for (uint32_t i = kServerPackets; i < G * kServerPackets; ++i) sl->addr[i] = (base + offsets[i]) | tag;
+    std::atomic_thread_fence(std::memory_order_release);
+    for (uint32_t i = 0; i < kServerPackets; ++i) __atomic_store_n(&sl->addr[i], (base + offsets[i]) | tag, __ATOMIC_RELAXED);
+    __atomic_store_n(&sl->out, reinterpret_cast<uint64_t>(out_dev) | tag, __ATOMIC_RELAXED);
+    __atomic_store_n(&sl->shape, uint64_t(P) | (uint64_t(G) << 16) | tag, __ATOMIC_RELEASE);
+    g_res_calls.fetch_add(1, std::memory_order_relaxed);
+    const uint64_t t_pub = now_ns();
+    int rc = FEC_OK;
     const auto t_fail = std::chrono::steady_clock::now() + std::chrono::seconds(10);
     for (uint32_t spins = 0;; ++spins) {
       if (__atomic_load_n(dw, __ATOMIC_ACQUIRE) == seq + 1) break;
@@ -435,14 +447,19 @@ class Resident {
       }
       backoff(spins);
     }
+    const uint64_t t_done = now_ns();
     if (rc != FEC_OK) {
-      // never served: withdraw the slot (no instance may serve it later into the caller's
-      // buffer) -- only safe while none runs, which is the case on every failure path above
-      __atomic_store_n(&sl->ready, 0, __ATOMIC_RELEASE);
+      // Not served: turn the slot into one with nothing to do (the slots after it are served in
+      // order, so it must still be served), so a later instance does not touch the caller's
+      // buffers.  Only a hung device can have read it already.
+      __atomic_store_n(&sl->shape, uint64_t(P) | tag, __ATOMIC_RELEASE);
     } else if (!repair_dev) {
       std::memcpy(repair_out, outs.host + size_t(si) * kResidentOutBytes, size_t(G) * P);
     }
     collected[si].store(seq + 1, std::memory_order_release);
+    g_res_pre_ns.fetch_add(t_pub - t_enter, std::memory_order_relaxed);
+    g_res_wait_ns.fetch_add(t_done - t_pub, std::memory_order_relaxed);
+    g_res_post_ns.fetch_add(now_ns() - t_done, std::memory_order_relaxed);
     return rc;
   }
 
@@ -516,13 +533,20 @@ void shutdown_residents() {
     if (kv.second) kv.second->shutdown();
 }
 
+constexpr int kResidentDevices = 64;
+std::atomic<Resident*> g_resident_fast[kResidentDevices];  // set once per device
+
 Resident* resident_for(int device) {
+  if (device >= 0 && device < kResidentDevices) {
+    if (Resident* r = g_resident_fast[device].load(std::memory_order_acquire)) return r;
+  }
   std::lock_guard<std::mutex> lk(g_reg_mu);
   auto it = g_resident.find(device);
   if (it != g_resident.end()) return it->second;
   if (g_resident.empty()) std::atexit(shutdown_residents);
   Resident* r = Resident::create(device);
   g_resident.emplace(device, r);
+  if (r && device >= 0 && device < kResidentDevices) g_resident_fast[device].store(r, std::memory_order_release);
   return r;
 }
 
@@ -541,19 +565,21 @@ Coalescer* coalescer_for(int device, uint32_t P) {
 
 bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* offsets, uint32_t num_groups,
                             uint32_t packet_size, uint8_t* repair_out, int* rc) {
+  const uint64_t t_enter = now_ns();
   if (env_long("QUICFEC_COALESCE", 1) == 0) return false;
   if (num_groups > static_cast<uint64_t>(std::max(0L, env_long("QUICFEC_COALESCE_MAX_GROUPS", 64)))) return false;
-  void* sdev = nullptr;
+  void *sdev = nullptr, *rdev = nullptr;
   const HostMem sm = classify_host_pointer(slab, &sdev);
-  if (sm == HostMem::kDevice || classify_host_pointer(offsets, nullptr) == HostMem::kDevice ||
-      classify_host_pointer(repair_out, nullptr) == HostMem::kDevice)
+  const HostMem rm = classify_host_pointer(repair_out, &rdev);
+  if (sm == HostMem::kDevice || rm == HostMem::kDevice || classify_host_pointer(offsets, nullptr) == HostMem::kDevice)
     return false;  // device-resident callers batch by themselves
-  void* rdev = nullptr;
-  const bool repair_pinned = classify_host_pointer(repair_out, &rdev) == HostMem::kPinned;
-  if (sm == HostMem::kPinned && env_long("QUICFEC_RESIDENT", 1) != 0 && Resident::fits(num_groups, packet_size, repair_pinned)) {
+  const bool repair_pinned = rm == HostMem::kPinned;
+  if (sm == HostMem::kPinned && env_long("QUICFEC_RESIDENT", 1) != 0 && Resident::fits(num_groups, packet_size, repair_pinned) &&
+      reinterpret_cast<uint64_t>(sdev) + 0xFFFFFFFFull + packet_size <= kServerAddrMask &&
+      reinterpret_cast<uint64_t>(rdev) <= kServerAddrMask) {
     if (Resident* r = resident_for(device)) {
       *rc = r->encode(static_cast<const uint8_t*>(sdev), offsets, num_groups, packet_size, repair_out,
-                      repair_pinned ? static_cast<uint8_t*>(rdev) : nullptr);
+                      repair_pinned ? static_cast<uint8_t*>(rdev) : nullptr, t_enter);
       return true;
     }
   }
@@ -579,9 +605,15 @@ QFEC_EXPORT int fec_coalesce_stats(FECCoalesceStats* out, int reset) {
   out->done_ns = g_done_ns.load();
   out->resident_calls = g_res_calls.load();
   out->resident_launches = g_res_launches.load();
+  out->resident_pre_ns = g_res_pre_ns.load();
+  out->resident_wait_ns = g_res_wait_ns.load();
+  out->resident_post_ns = g_res_post_ns.load();
   if (reset) {
     g_res_calls = 0;
     g_res_launches = 0;
+    g_res_pre_ns = 0;
+    g_res_wait_ns = 0;
+    g_res_post_ns = 0;
     g_close_ns = 0;
     g_launch_ns = 0;
     g_done_ns = 0;

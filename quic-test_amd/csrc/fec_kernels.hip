@@ -1338,15 +1338,16 @@ __global__ __launch_bounds__(256) void copy_words(const uint4* __restrict__ src,
   if (t < n16) dst[t] = src[t];
 }
 
-// Resident legacy encoder (fec_kernels.hpp ServerSlot): one workgroup of 16 waves.  Wave 0
-// polls the next 64 slots of the ring with one system-scope acquire load per lane and takes
-// the published run from the next expected seq (slots are served in order), with a prefix of
-// the run's work items (one per 16-B column of a group) in LDS; then every thread takes work
-// items (the group's 10 packet addresses from the slot, 10 loads, XOR, one store to the
-// repair row -- the reference's row 0, fec_xor_simd.cpp:411-427), the workgroup fences its
-// stores at system scope and the slots' done words are stored (release).  Every wave leaves
-// together: at the host's stop flag, after idle_ticks without work, after life_ticks, and in
-// any case after kServerMaxPolls polls.
+// Resident legacy encoder (fec_kernels.hpp ServerSlot): one workgroup of 16 waves.  One poll
+// is one round trip over PCIe: wave 0 reads the header words of the next 64 slots (a lane each)
+// while waves 1..10 read the first group's 10 packet addresses of each of them; a slot is
+// complete when every one of those words carries its lap tag, and the run of complete slots
+// from the next expected seq is served (slots in order).  Then every thread takes work items
+// (one 16-B column of one group: its 10 packets loaded, XORed -- the reference's row 0,
+// fec_xor_simd.cpp:411-427 -- and stored to the repair row), the workgroup fences its stores at
+// system scope and the slots' done words are stored (release).  Every wave leaves together: at
+// the host's stop flag, after idle_ticks without work, after life_ticks, and in any case after
+// kServerMaxPolls polls.
 constexpr uint32_t kServerThreads = 1024;
 constexpr uint32_t kServerMaxPolls = 1u << 22;
 
@@ -1358,6 +1359,9 @@ __device__ __forceinline__ void sys_store_release(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A word of host memory as it is now (system-coherent load, no cache).
+__device__ __forceinline__ uint64_t sys_load_word(const uint64_t* p) { return *reinterpret_cast<const volatile uint64_t*>(p); }
+
 __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot* __restrict__ ring,
                                                                 uint64_t* __restrict__ done,
                                                                 ServerControl* __restrict__ ctl, uint64_t start_seq,
@@ -1366,7 +1370,8 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
   __shared__ uint32_t s_n, s_exit;
   __shared__ uint32_t s_first[65];  // work items before slot i of the run
   __shared__ uint32_t s_P[64], s_cpp[64];
-  __shared__ uint64_t s_out[64];
+  __shared__ uint64_t s_out[64], s_shape[64];
+  __shared__ uint64_t s_addr[64][kServerPackets];  // the first group's packet addresses (tagged)
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   uint64_t t0 = 0, t_last = 0;  // thread 0 only
   if (tid == 0) {
@@ -1375,21 +1380,33 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
   }
   __syncthreads();
   for (uint32_t it = 0; it < kServerMaxPolls; ++it) {
+    const uint64_t next = s_next;
+    // the poll: headers (wave 0) and first-group addresses (waves 1..10), all in flight at once
     if (tid < 64) {
-      const uint64_t next = s_next;
+      const ServerSlot* sl = ring + (next + lane) % kServerSlots;
+      s_out[lane] = sys_load_word(&sl->out);
+      s_shape[lane] = sys_load_word(&sl->shape);
+    } else if (tid < 64 + 64 * kServerPackets) {
+      const uint32_t j = tid - 64, i = j / kServerPackets, w = j - i * kServerPackets;
+      s_addr[i][w] = sys_load_word(&ring[(next + i) % kServerSlots].addr[w]);
+    }
+    __syncthreads();
+    if (tid < 64) {
       const uint64_t seq = next + lane;
-      const ServerSlot* sl = ring + seq % kServerSlots;
-      const bool rdy = sys_load_acquire(&sl->ready) == seq + 1;
-      const uint64_t bal = __ballot(rdy);
+      const uint64_t tag = (seq / kServerSlots) & 0xFFu;
+      bool ok = (s_out[lane] >> kServerTagShift) == tag && (s_shape[lane] >> kServerTagShift) == tag;
+#pragma unroll
+      for (uint32_t w = 0; w < kServerPackets; ++w) ok = ok && (s_addr[lane][w] >> kServerTagShift) == tag;
+      const uint64_t bal = __ballot(ok);
       const uint32_t n = ~bal == 0 ? 64u : static_cast<uint32_t>(__builtin_ctzll(~bal));
       uint32_t work = 0;
       if (lane < n) {
-        const uint32_t P = sl->P;
+        const uint64_t sh = s_shape[lane];
+        const uint32_t P = static_cast<uint32_t>(sh & 0xFFFFu), G = static_cast<uint32_t>((sh >> 16) & 0xFFu);
         const uint32_t cpp = (P + 15u) / 16u;
         s_P[lane] = P;
         s_cpp[lane] = cpp;
-        s_out[lane] = sl->out;
-        work = sl->groups * cpp;
+        work = G * cpp;
       }
       uint32_t incl = work;
 #pragma unroll
@@ -1411,8 +1428,8 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
     const uint32_t n = s_n;
     const bool leave = s_exit != 0;
     if (n > 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the published slots and packets, every wave
-      const uint64_t next = s_next;
+      // the packets (and any later groups' addresses) as the host wrote them before the words above
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       const uint32_t total = s_first[n];
       for (uint32_t w = tid; w < total; w += kServerThreads) {
         uint32_t i = 0;
@@ -1421,11 +1438,20 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
         const uint32_t cpp = s_cpp[i], P = s_P[i];
         const uint32_t g = local / cpp, col = local - g * cpp;
         const uint32_t coff = col * 16u + 16u <= P ? col * 16u : P - 16u;
-        const uint64_t* ad = ring[(next + i) % kServerSlots].addr + g * kServerPackets;
-        u32x4 acc = ld16<0>(reinterpret_cast<const uint8_t*>(ad[0]) + coff);
+        uint64_t ad[kServerPackets];
+        if (g == 0) {
 #pragma unroll
-        for (uint32_t j = 1; j < kServerPackets; ++j) acc ^= ld16<0>(reinterpret_cast<const uint8_t*>(ad[j]) + coff);
-        st16<0>(reinterpret_cast<uint8_t*>(s_out[i]) + static_cast<uint64_t>(g) * P + coff, acc);
+          for (uint32_t j = 0; j < kServerPackets; ++j) ad[j] = s_addr[i][j];
+        } else {
+          const uint64_t* src = ring[(next + i) % kServerSlots].addr + g * kServerPackets;
+#pragma unroll
+          for (uint32_t j = 0; j < kServerPackets; ++j) ad[j] = src[j];
+        }
+        u32x4 acc = ld16<0>(reinterpret_cast<const uint8_t*>(ad[0] & kServerAddrMask) + coff);
+#pragma unroll
+        for (uint32_t j = 1; j < kServerPackets; ++j)
+          acc ^= ld16<0>(reinterpret_cast<const uint8_t*>(ad[j] & kServerAddrMask) + coff);
+        st16<0>(reinterpret_cast<uint8_t*>(s_out[i] & kServerAddrMask) + static_cast<uint64_t>(g) * P + coff, acc);
       }
       __threadfence_system();  // this thread's repair rows are visible before any done word
       __syncthreads();

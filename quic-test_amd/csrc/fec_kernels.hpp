@@ -121,20 +121,22 @@ bool decode_needs_rec_off(const DecodeLaunch& a);
 // Whether launch_decode(a) runs a form that reads a compact codebook (coefficient bytes).
 bool decode_compact_tables(const DecodeLaunch& a);
 // ---- resident legacy encoder (fec_coalesce.cpp "resident server") ----
-// A ring of submission slots in page-locked, coherent host memory: the host fills slot
-// (seq % kServerSlots) with a legacy call's groups (absolute device addresses of their 10
-// packets, the repair rows' address) and publishes it by storing `ready` = seq + 1; one
-// resident workgroup polls the ring in order, XORs every published slot's groups and stores
-// done[seq % kServerSlots] = seq + 1.  Calls are served without a kernel launch each.
+// A ring of submission slots in page-locked, coherent host memory.  The host fills slot
+// seq % kServerSlots with a legacy call's groups: every word of a slot carries the slot's lap,
+// (seq / kServerSlots) & 0xFF, in its top byte, so the device recognises a complete slot by
+// the tags alone, whatever order its reads of the host's stores land in (the host writes the
+// groups after the first before the first group and the header, and the device reads those
+// only after it has seen the rest).  One resident workgroup serves the slots in seq order and
+// stores done[seq % kServerSlots] = seq + 1.  Calls are served without a kernel launch each.
 constexpr uint32_t kServerSlots = 1024;
 constexpr uint32_t kServerMaxGroups = 8;  // groups per slot (legacy calls of 1..8 groups)
 constexpr uint32_t kServerPackets = 10;   // the legacy call's packets per group
+constexpr uint64_t kServerTagShift = 56;  // addresses below 2^56 (user virtual addresses)
+constexpr uint64_t kServerAddrMask = (1ull << kServerTagShift) - 1;
 struct alignas(64) ServerSlot {
-  uint64_t ready;           // seq + 1 once the slot is published (host release store)
-  uint32_t groups, P;       // 1..kServerMaxGroups groups of P >= 16 bytes
-  uint64_t out;             // device address of the groups' repair rows, row g at out + g * P
-  uint64_t pad;
-  uint64_t addr[kServerMaxGroups * kServerPackets];  // packet (g, j) at addr[g * 10 + j]
+  uint64_t out;             // tag | device address of the repair rows, row g at out + g * P
+  uint64_t shape;           // tag | P (bits 0..15) | groups (bits 16..23; 0 = nothing to do)
+  uint64_t addr[kServerMaxGroups * kServerPackets];  // tag | device address of packet (g, j) at [g * 10 + j]
 };
 struct alignas(64) ServerControl {
   uint64_t stop;            // host -> device: leave at the next poll

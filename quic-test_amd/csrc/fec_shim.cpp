@@ -23,6 +23,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <utility>
@@ -193,10 +194,49 @@ void parallel_for(uint64_t n, uint64_t min_per_thread, F&& f) {
 
 enum class Mem { kHost, kPinned, kDevice };
 
+// Page-locked buffers this library handed out (fec_alloc_slab / _numa / fec_alloc_repair_buffer).
+// The Go wrapper passes the same two of them to every legacy call (fec_cgo.go:64, :76, :138);
+// finding them here keeps hipPointerGetAttributes -- a runtime lock and a lookup per pointer --
+// off the per-call path.
+struct PinnedRange {
+  uintptr_t hi;   // one past the last byte
+  uintptr_t dev;  // device address of the first byte
+};
+std::shared_mutex g_pin_mu;
+std::map<uintptr_t, PinnedRange> g_pinned;  // by first byte
+
+void pinned_register(void* p, size_t len) {
+  if (!p || len == 0) return;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || d == nullptr) {
+    (void)hipGetLastError();
+    d = p;
+  }
+  std::unique_lock<std::shared_mutex> lk(g_pin_mu);
+  g_pinned[reinterpret_cast<uintptr_t>(p)] = PinnedRange{reinterpret_cast<uintptr_t>(p) + len, reinterpret_cast<uintptr_t>(d)};
+}
+
+void pinned_unregister(void* p) {
+  std::unique_lock<std::shared_mutex> lk(g_pin_mu);
+  g_pinned.erase(reinterpret_cast<uintptr_t>(p));
+}
+
+bool pinned_lookup(const void* p, void** dev) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::shared_lock<std::shared_mutex> lk(g_pin_mu);
+  auto it = g_pinned.upper_bound(a);
+  if (it == g_pinned.begin()) return false;
+  --it;
+  if (a >= it->second.hi) return false;
+  if (dev) *dev = reinterpret_cast<void*>(it->second.dev + (a - it->first));
+  return true;
+}
+
 // `dev` (optional): for page-locked host memory, the address kernels use for `p`.
 Mem classify_ptr(const void* p, void** dev = nullptr) {
   if (dev) *dev = nullptr;
   if (!p) return Mem::kHost;
+  if (pinned_lookup(p, dev)) return Mem::kPinned;
   hipPointerAttribute_t attr;
   std::memset(&attr, 0, sizeof(attr));
   const hipError_t e = hipPointerGetAttributes(&attr, p);
@@ -932,6 +972,7 @@ QFEC_EXPORT void* fec_alloc_slab(size_t size) {
     set_error("fec_alloc_slab(%zu): %s", size, hipGetErrorString(e));
     return nullptr;
   }
+  pinned_register(p, aligned == 0 ? 64 : aligned);
   return p;
 }
 
@@ -975,6 +1016,7 @@ QFEC_EXPORT void* fec_alloc_slab_numa(size_t size, int numa_node) {
   if (hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0)
     registered = hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess;
   (void)hipGetLastError();
+  if (registered) pinned_register(p, len);
   std::lock_guard<std::mutex> lk(g_numa_mu);
   g_numa_slabs[p] = NumaSlab{len, registered};
   return p;
@@ -984,6 +1026,7 @@ QFEC_EXPORT void* fec_alloc_repair_buffer(size_t size) { return fec_alloc_slab(s
 
 QFEC_EXPORT void fec_free_slab(void* ptr) {
   if (!ptr) return;
+  pinned_unregister(ptr);
   {
     std::lock_guard<std::mutex> lk(g_numa_mu);
     auto it = g_numa_slabs.find(ptr);

@@ -496,20 +496,67 @@ int legacy(int S, double rate, double seconds) {
   fec_coalesce_stats(&cs, 0);
   const char* co = std::getenv("QUICFEC_COALESCE");
   const char* res = std::getenv("QUICFEC_RESIDENT");
-  char cfg[768];
+  char cfg[1024];
   std::snprintf(cfg, sizeof(cfg),
                 "\"streams\": %d, \"rate_pps\": %.0f, \"r\": 1, \"coalesce\": %d, \"errors\": %ld, \"go_fallback\": %ld, "
                 "\"coalesced_calls\": %llu, \"launches\": %llu, \"mean_batch\": %.2f, \"max_batch\": %llu, "
                 "\"us_per_launch\": {\"close\": %.2f, \"launch\": %.2f, \"done\": %.2f}, \"resident\": %d, "
-                "\"resident_calls\": %llu, \"resident_launches\": %llu",
+                "\"resident_calls\": %llu, \"resident_launches\": %llu, "
+                "\"resident_us_per_call\": {\"pre\": %.2f, \"wait\": %.2f, \"post\": %.2f}",
                 S, rate, co && co[0] == '0' ? 0 : 1, errors.load(), fallback.load(), (unsigned long long)cs.calls,
                 (unsigned long long)cs.batches, cs.batches ? double(cs.groups) / cs.batches : 0.0,
                 (unsigned long long)cs.max_batch, cs.batches ? cs.close_ns / 1e3 / cs.batches : 0.0,
                 cs.batches ? cs.launch_ns / 1e3 / cs.batches : 0.0, cs.batches ? cs.done_ns / 1e3 / cs.batches : 0.0,
                 res && res[0] == '0' ? 0 : 1, (unsigned long long)cs.resident_calls,
-                (unsigned long long)cs.resident_launches);
+                (unsigned long long)cs.resident_launches, cs.resident_calls ? cs.resident_pre_ns / 1e3 / cs.resident_calls : 0.0,
+                cs.resident_calls ? cs.resident_wait_ns / 1e3 / cs.resident_calls : 0.0,
+                cs.resident_calls ? cs.resident_post_ns / 1e3 / cs.resident_calls : 0.0);
   print_lat("legacy", cfg, all, double(groups), wall, cpu, nullptr);
   return errors || fallback ? 1 : 0;
+}
+
+// fec_encode_batch alone, one group per call on page-locked buffers as FECEncoderCXX holds them
+// (no Go-API mirror around it): the library's own per-call latency on whichever path it takes.
+int legacy_raw(int calls) {
+  FECEncoderCtx* ctx = fec_encoder_new(0.1, 1024);
+  if (!ctx) return 2;
+  auto* slab = static_cast<uint8_t*>(fec_alloc_slab(size_t(kK) * kP));
+  auto* rep = static_cast<uint8_t*>(fec_alloc_repair_buffer(kP));
+  oracle_fill_splitmix(slab, size_t(kK) * kP, 0x5EED10, 0);
+  uint32_t offs[kK];
+  for (int j = 0; j < kK; ++j) offs[j] = uint32_t(j * kP);
+  Bytes xr(kP);
+  const uint8_t* p[kK];
+  for (int j = 0; j < kK; ++j) p[j] = slab + size_t(j) * kP;
+  oracle_xor_avx2(p, kK, kP, xr.data());
+  FECCoalesceStats cs{};
+  fec_coalesce_stats(&cs, 1);
+  std::vector<double> us;
+  long errors = 0;
+  const auto t0 = Clock::now();
+  for (int c = 0; c < calls; ++c) {
+    const auto a = Clock::now();
+    if (fec_encode_batch(ctx, slab, offs, 1, kP, rep) != 0) ++errors;
+    us.push_back(std::chrono::duration<double, std::micro>(Clock::now() - a).count());
+    if (std::memcmp(rep, xr.data(), kP)) ++errors;
+  }
+  const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
+  fec_coalesce_stats(&cs, 0);
+  const char* co = std::getenv("QUICFEC_COALESCE");
+  const char* res = std::getenv("QUICFEC_RESIDENT");
+  char cfg[512];
+  std::snprintf(cfg, sizeof(cfg),
+                "\"streams\": 1, \"coalesce\": %d, \"resident\": %d, \"errors\": %ld, \"resident_calls\": %llu, "
+                "\"resident_us_per_call\": {\"pre\": %.2f, \"wait\": %.2f, \"post\": %.2f}",
+                co && co[0] == '0' ? 0 : 1, res && res[0] == '0' ? 0 : 1, errors, (unsigned long long)cs.resident_calls,
+                cs.resident_calls ? cs.resident_pre_ns / 1e3 / cs.resident_calls : 0.0,
+                cs.resident_calls ? cs.resident_wait_ns / 1e3 / cs.resident_calls : 0.0,
+                cs.resident_calls ? cs.resident_post_ns / 1e3 / cs.resident_calls : 0.0);
+  print_lat("legacy_raw", cfg, us, calls, wall, 0.0, nullptr);
+  fec_free_slab(slab);
+  fec_free_repair_buffer(rep);
+  fec_encoder_free(ctx);
+  return errors ? 1 : 0;
 }
 
 // One core: the reference's computation per group (AVX2 XOR, xor_packets_avx2 restated) and
@@ -564,6 +611,7 @@ int main(int argc, char** argv) {
     return saturate(int(arg(2, 16)), arg(3, 3), int(arg(4, 1)), int(arg(5, 1000)), int(arg(6, 4096)));
   if (mode == "single") return single(int(arg(2, 2000)));
   if (mode == "legacy") return legacy(int(arg(2, 16)), arg(3, 0), arg(4, 3));
+  if (mode == "legacy_raw") return legacy_raw(int(arg(2, 20000)));
   if (mode == "decode")
     return draw(int(arg(2, 16)), arg(3, 3), int(arg(4, 3)), int(arg(5, 1000)), int(arg(6, 4096)), int(arg(7, 1024)));
   if (mode == "raw")

@@ -508,7 +508,8 @@ def xor_packets(packets, packet_size: int, repair, variant: str = "avx2") -> Non
     getattr(lib, f"xor_packets_{variant}")(arr, len(packets), packet_size, _ptr(repair))
 
 
-COALESCE_STATS = ("calls", "groups", "batches", "max_batch", "max_calls", "close_ns", "launch_ns", "done_ns", "resident_calls", "resident_launches")
+COALESCE_STATS = ("calls", "groups", "batches", "max_batch", "max_calls", "close_ns", "launch_ns", "done_ns", "resident_calls", "resident_launches",
+                  "resident_pre_ns", "resident_wait_ns", "resident_post_ns")
 
 
 def coalesce_stats(reset: bool = False) -> dict:

@@ -11,6 +11,7 @@ T="timeout -k 10 60"
 SECS=${SECS:-2}
 run() { "$@" || [ $? -eq 1 ]; }  # a run reporting errors exits 1 after its line; a hang still ends it
 run $T $B cpu
+for e in "QUICFEC_RESIDENT=1" "QUICFEC_RESIDENT=0" "QUICFEC_COALESCE=0"; do env $e $T $B legacy_raw 20000 || [ $? -eq 1 ]; done
 for rep in $(seq 1 "${REPS:-1}"); do
   for s in 1 16 100; do
     for mode in resident batches percontext; do
