@@ -47,6 +47,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -391,6 +392,8 @@ class Resident {
         !alloc_coherent(r->done, sizeof(uint64_t) * kServerSlots) || !alloc_coherent(r->ctl, sizeof(ServerControl)) ||
         !alloc_coherent(r->outs, size_t(kResidentOutBytes) * kServerSlots))
       return nullptr;
+    if (env_long("QUICFEC_RESIDENT_STAMPS", 0) != 0 && !alloc_coherent(r->stamps, 256 * 8 * sizeof(uint64_t))) return nullptr;
+    r->tick_khz = static_cast<uint64_t>(khz);
     // no word of a slot that was never written may carry lap 0's tag
     std::memset(r->ring.host, 0xFF, sizeof(ServerSlot) * kServerSlots);
     r->collected.reset(new std::atomic<uint64_t>[kServerSlots]);
@@ -468,13 +471,34 @@ class Resident {
     __atomic_store_n(&reinterpret_cast<ServerControl*>(ctl.host)->stop, 1, __ATOMIC_RELEASE);
     const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
     while (instance_alive() && std::chrono::steady_clock::now() < until) std::this_thread::yield();
+    if (stamps.host) print_stamps();
+  }
+
+  // QUICFEC_RESIDENT_STAMPS: mean phase times of the last (up to) 256 served batches, to stderr.
+  void print_stamps() const {
+    const uint64_t* st = reinterpret_cast<const uint64_t*>(stamps.host);
+    double sum[7] = {};
+    uint32_t n = 0;
+    for (uint32_t i = 0; i < 256; ++i) {
+      if (st[i * 8 + 7] == 0) continue;
+      for (int k = 0; k < 7; ++k) sum[k] += double(st[i * 8 + k]);
+      ++n;
+    }
+    if (n == 0) return;
+    const double us = 1000.0 / double(tick_khz);
+    std::fprintf(stderr,
+                 "{\"resident_stamps\": {\"batches\": %u, \"us\": {\"poll\": %.2f, \"acquire\": %.2f, \"work\": %.2f, "
+                 "\"release\": %.2f, \"done\": %.2f}, \"mean_slots\": %.2f, \"mean_polls\": %.2f}}\n",
+                 n, sum[0] / n * us, sum[1] / n * us, sum[2] / n * us, sum[3] / n * us, sum[4] / n * us, sum[5] / n,
+                 sum[6] / n);
   }
 
  private:
   int device = 0;
   hipStream_t stream = nullptr;
   uint64_t idle_ticks = 0, life_ticks = 0;
-  Pinned ring, done, ctl, outs;
+  Pinned ring, done, ctl, outs, stamps;
+  uint64_t tick_khz = 100000;
   std::unique_ptr<std::atomic<uint64_t>[]> collected;  // per slot: seq + 1 of its last collected call
   std::atomic<uint64_t> next_seq{0};
   std::mutex mu;
@@ -510,7 +534,8 @@ class Resident {
     const hipError_t e = bd.ok ? launch_legacy_server(reinterpret_cast<const ServerSlot*>(ring.dev),
                                                       reinterpret_cast<uint64_t*>(done.dev),
                                                       reinterpret_cast<ServerControl*>(ctl.dev), start, g, idle_ticks,
-                                                      life_ticks, stream)
+                                                      life_ticks, stamps.host ? reinterpret_cast<uint64_t*>(stamps.dev) : nullptr,
+                                                      stream)
                                : hipErrorInvalidDevice;
     if (e != hipSuccess) {
       (void)hipGetLastError();

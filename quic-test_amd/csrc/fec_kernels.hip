@@ -1339,39 +1339,49 @@ __global__ __launch_bounds__(256) void copy_words(const uint4* __restrict__ src,
 }
 
 // Resident legacy encoder (fec_kernels.hpp ServerSlot): one workgroup of 16 waves.  One poll
-// is one round trip over PCIe: wave 0 reads the header words of the next 64 slots (a lane each)
-// while waves 1..10 read the first group's 10 packet addresses of each of them; a slot is
-// complete when every one of those words carries its lap tag, and the run of complete slots
-// from the next expected seq is served (slots in order).  Then every thread takes work items
-// (one 16-B column of one group: its 10 packets loaded, XORed -- the reference's row 0,
-// fec_xor_simd.cpp:411-427 -- and stored to the repair row), the workgroup fences its stores at
-// system scope and the slots' done words are stored (release).  Every wave leaves together: at
-// the host's stop flag, after idle_ticks without work, after life_ticks, and in any case after
-// kServerMaxPolls polls.
+// is one round trip over PCIe: 128 lanes read the first two 64-B lines of each of the next 16
+// slots (the header words and the first group's 10 packet addresses, 16 B a lane: 32 line reads
+// in all -- reading every word of 64 slots separately took 5 us a poll, 2x a round trip); a
+// slot is complete when every one of those words carries its lap tag, and the run of complete
+// slots from the next expected seq is served (slots in order).  Then every thread takes work
+// items (one 16-B column of one group: its 10 packets loaded, XORed -- the reference's row 0,
+// fec_xor_simd.cpp:411-427 -- and stored to the repair row), the workgroup fences its stores
+// at system scope and the slots' done words are stored (release).  Every wave leaves together:
+// at the host's stop flag, after idle_ticks without work, after life_ticks, and in any case
+// after kServerMaxPolls polls.
 constexpr uint32_t kServerThreads = 1024;
 constexpr uint32_t kServerMaxPolls = 1u << 22;
-
-__device__ __forceinline__ uint64_t sys_load_acquire(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
+constexpr uint32_t kServerPoll = 16;      // slots read per poll
+constexpr uint32_t kServerHeadWords = 16;  // words of a slot read by the poll: out, shape, addr[0..13]
 
 __device__ __forceinline__ void sys_store_release(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// A word of host memory as it is now (system-coherent load, no cache).
-__device__ __forceinline__ uint64_t sys_load_word(const uint64_t* p) { return *reinterpret_cast<const volatile uint64_t*>(p); }
+// System-coherent (uncached) access for the words the host polls: program order with the
+// system-coherent stores before them, and vmcnt(0) in between, is the ordering.
+__device__ __forceinline__ void sys_store_relaxed(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// 16 bytes to host memory at any address, written system-coherent (sc0 sc1: no cache keeps a copy).
+__device__ __forceinline__ void sys_store_16b(uint8_t* p, u32x4 v) { *reinterpret_cast<volatile u32x4u*>(p) = v; }
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// 16 bytes of host memory as they are now (system-coherent load, no cache).
+__device__ __forceinline__ u64x2 sys_load_16(const uint64_t* p) { return *reinterpret_cast<const volatile u64x2*>(p); }
 
 __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot* __restrict__ ring,
                                                                 uint64_t* __restrict__ done,
                                                                 ServerControl* __restrict__ ctl, uint64_t start_seq,
-                                                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks) {
+                                                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+                                                                uint64_t* __restrict__ stamps) {
   __shared__ uint64_t s_next;
-  __shared__ uint32_t s_n, s_exit;
-  __shared__ uint32_t s_first[65];  // work items before slot i of the run
-  __shared__ uint32_t s_P[64], s_cpp[64];
-  __shared__ uint64_t s_out[64], s_shape[64];
-  __shared__ uint64_t s_addr[64][kServerPackets];  // the first group's packet addresses (tagged)
+  __shared__ uint32_t s_n, s_exit, s_stop;
+  __shared__ uint32_t s_first[kServerPoll + 1];  // work items before slot i of the run
+  __shared__ uint32_t s_P[kServerPoll], s_cpp[kServerPoll];
+  __shared__ uint64_t s_head[kServerPoll][kServerHeadWords];  // out, shape, addr[0..13] (tagged)
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   uint64_t t0 = 0, t_last = 0;  // thread 0 only
   if (tid == 0) {
@@ -1379,29 +1389,38 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
     t0 = t_last = static_cast<uint64_t>(wall_clock64());
   }
   __syncthreads();
+  // Diagnostic stamps (stamps != nullptr, QUICFEC_RESIDENT_STAMPS): thread 0's wall clock at the
+  // phases of each served batch, into a ring of 256 records of 8 words in host memory that no
+  // other code reads; never part of a result.
+  uint64_t st_batches = 0, st_polls = 0, st_t[6] = {};
   for (uint32_t it = 0; it < kServerMaxPolls; ++it) {
     const uint64_t next = s_next;
-    // the poll: headers (wave 0) and first-group addresses (waves 1..10), all in flight at once
-    if (tid < 64) {
-      const ServerSlot* sl = ring + (next + lane) % kServerSlots;
-      s_out[lane] = sys_load_word(&sl->out);
-      s_shape[lane] = sys_load_word(&sl->shape);
-    } else if (tid < 64 + 64 * kServerPackets) {
-      const uint32_t j = tid - 64, i = j / kServerPackets, w = j - i * kServerPackets;
-      s_addr[i][w] = sys_load_word(&ring[(next + i) % kServerSlots].addr[w]);
+    if (stamps != nullptr && tid == 0) st_t[0] = static_cast<uint64_t>(wall_clock64());
+    // the poll: the first two lines of each of the next kServerPoll slots, 16 B a lane, and the
+    // host's stop word, all in one round trip
+    if (tid < kServerPoll * kServerHeadWords / 2) {
+      const uint32_t i = tid / (kServerHeadWords / 2), piece = tid % (kServerHeadWords / 2);
+      const u64x2 v = sys_load_16(reinterpret_cast<const uint64_t*>(ring + (next + i) % kServerSlots) + 2 * piece);
+      s_head[i][2 * piece] = v.x;
+      s_head[i][2 * piece + 1] = v.y;
+    } else if (tid == kServerPoll * kServerHeadWords / 2) {
+      s_stop = *reinterpret_cast<const volatile uint64_t*>(&ctl->stop) != 0 ? 1u : 0u;
     }
     __syncthreads();
     if (tid < 64) {
       const uint64_t seq = next + lane;
       const uint64_t tag = (seq / kServerSlots) & 0xFFu;
-      bool ok = (s_out[lane] >> kServerTagShift) == tag && (s_shape[lane] >> kServerTagShift) == tag;
+      bool ok = lane < kServerPoll;
+      if (ok) {
+        // out, shape and the first group's 10 addresses (words 0 .. 11)
 #pragma unroll
-      for (uint32_t w = 0; w < kServerPackets; ++w) ok = ok && (s_addr[lane][w] >> kServerTagShift) == tag;
+        for (uint32_t w = 0; w < 2 + kServerPackets; ++w) ok = ok && (s_head[lane][w] >> kServerTagShift) == tag;
+      }
       const uint64_t bal = __ballot(ok);
       const uint32_t n = ~bal == 0 ? 64u : static_cast<uint32_t>(__builtin_ctzll(~bal));
       uint32_t work = 0;
       if (lane < n) {
-        const uint64_t sh = s_shape[lane];
+        const uint64_t sh = s_head[lane][1];
         const uint32_t P = static_cast<uint32_t>(sh & 0xFFFFu), G = static_cast<uint32_t>((sh >> 16) & 0xFFu);
         const uint32_t cpp = (P + 15u) / 16u;
         s_P[lane] = P;
@@ -1414,12 +1433,12 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
         const uint32_t y = __shfl_up(incl, d, 64);
         if (lane >= static_cast<uint32_t>(d)) incl += y;
       }
-      s_first[lane + 1] = incl;
+      if (lane < kServerPoll) s_first[lane + 1] = incl;
       if (lane == 0) {
         s_first[0] = 0;
         const uint64_t now = static_cast<uint64_t>(wall_clock64());
         if (n > 0) t_last = now;
-        const bool stop = sys_load_acquire(&ctl->stop) != 0;
+        const bool stop = s_stop != 0;
         s_n = n;
         s_exit = (stop || now - t0 > life_ticks || (n == 0 && now - t_last > idle_ticks)) ? 1u : 0u;
       }
@@ -1427,9 +1446,18 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
     __syncthreads();
     const uint32_t n = s_n;
     const bool leave = s_exit != 0;
+    if (stamps != nullptr && tid == 0) {
+      st_t[1] = static_cast<uint64_t>(wall_clock64());
+      ++st_polls;
+    }
     if (n > 0) {
       // the packets (and any later groups' addresses) as the host wrote them before the words above
+      // The caller's packets as the host wrote them before its slot (the L2 may hold an older
+      // copy of the same lines from an earlier call).  Cached loads after this acquire: reading
+      // the packets system-coherent instead (sc0 sc1, no fence) made every 16-B load its own
+      // PCIe read and the work step 2.8x slower (12.6 vs 4.5 us a batch).
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (stamps != nullptr && tid == 0) st_t[2] = static_cast<uint64_t>(wall_clock64());
       const uint32_t total = s_first[n];
       for (uint32_t w = tid; w < total; w += kServerThreads) {
         uint32_t i = 0;
@@ -1441,24 +1469,47 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
         uint64_t ad[kServerPackets];
         if (g == 0) {
 #pragma unroll
-          for (uint32_t j = 0; j < kServerPackets; ++j) ad[j] = s_addr[i][j];
+          for (uint32_t j = 0; j < kServerPackets; ++j) ad[j] = s_head[i][2 + j];
         } else {
+          // written by the host before the slot's first group and header, seen complete above
           const uint64_t* src = ring[(next + i) % kServerSlots].addr + g * kServerPackets;
 #pragma unroll
-          for (uint32_t j = 0; j < kServerPackets; ++j) ad[j] = src[j];
+          for (uint32_t j = 0; j < kServerPackets; ++j) ad[j] = *reinterpret_cast<const volatile uint64_t*>(src + j);
         }
         u32x4 acc = ld16<0>(reinterpret_cast<const uint8_t*>(ad[0] & kServerAddrMask) + coff);
 #pragma unroll
         for (uint32_t j = 1; j < kServerPackets; ++j)
           acc ^= ld16<0>(reinterpret_cast<const uint8_t*>(ad[j] & kServerAddrMask) + coff);
-        st16<0>(reinterpret_cast<uint8_t*>(s_out[i] & kServerAddrMask) + static_cast<uint64_t>(g) * P + coff, acc);
+        uint8_t* dst = reinterpret_cast<uint8_t*>(s_head[i][0] & kServerAddrMask) + static_cast<uint64_t>(g) * P + coff;
+        sys_store_16b(dst, acc);
       }
-      __threadfence_system();  // this thread's repair rows are visible before any done word
+      if (stamps != nullptr && tid == 0) st_t[3] = static_cast<uint64_t>(wall_clock64());
+      // The repair rows were stored system-coherent (no cache to write back): wait until every
+      // one of this thread's stores is acknowledged, then the workgroup's barrier, then the done
+      // words -- no release fence.  Same box, alternating (profiles/r03_resident_store_ab.txt):
+      // one caller 8.0 vs 10.9 us a call, 16 callers 550k vs 330k calls/s against plain stores
+      // and a system release fence (its L2 write-back 1.7-2.9 us a batch).
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      if (stamps != nullptr && tid == 0) st_t[4] = static_cast<uint64_t>(wall_clock64());
       __syncthreads();
-      if (tid < n) sys_store_release(&done[(next + tid) % kServerSlots], next + tid + 1);
+      if (tid < n) sys_store_relaxed(&done[(next + tid) % kServerSlots], next + tid + 1);
       if (tid == 0) {
         s_next = next + n;
-        sys_store_release(&ctl->progress, next + n);
+        sys_store_relaxed(&ctl->progress, next + n);
+      }
+      if (stamps != nullptr && tid == 0) {
+        st_t[5] = static_cast<uint64_t>(wall_clock64());
+        uint64_t* rec = stamps + (st_batches % 256) * 8;
+        rec[0] = st_t[1] - st_t[0];  // the poll that found the run
+        rec[1] = st_t[2] - st_t[1];  // decision + acquire fence
+        rec[2] = st_t[3] - st_t[2];  // thread 0's work items
+        rec[3] = st_t[4] - st_t[3];  // release fence
+        rec[4] = st_t[5] - st_t[4];  // barrier + done stores
+        rec[5] = n;
+        rec[6] = st_polls;           // polls since the previous batch, this one included
+        __threadfence_system();
+        sys_store_release(&rec[7], ++st_batches);
+        st_polls = 0;
       }
     } else if (!leave) {
       __builtin_amdgcn_s_sleep(8);
@@ -2008,9 +2059,9 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
 }
 
 hipError_t launch_legacy_server(const ServerSlot* ring, uint64_t* done, ServerControl* ctl, uint64_t start_seq,
-                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks, hipStream_t s) {
+                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks, uint64_t* stamps, hipStream_t s) {
   hipLaunchKernelGGL(legacy_server, dim3(1), dim3(kServerThreads), 0, s, ring, done, ctl, start_seq, gen, idle_ticks,
-                     life_ticks);
+                     life_ticks, stamps);
   return hipGetLastError();
 }
 
