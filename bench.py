@@ -636,10 +636,12 @@ def main() -> int:
     dec_bytes = dec_read = 0
     api = args.decode_api
     if api == "auto":
-        # packed rows where the shape has a mask-addressed form (C3 recover 2.39 vs 2.42 ms, C5's
-        # sparse loss 0.263 vs 0.267 ms with the two-launch prefix sum,
-        # profiles/r02_packed_ab2.txt), else the (g*r + m)*P slots
-        api = "packed" if packed_supported(k, r, P) else "recover"
+        # The slot rows: the choice that never lost by more than 4% on any box measured, both
+        # APIs interleaved on each (profiles/r03_final/ab_decode_api_box*.jsonl, and the
+        # driver's round-2 record): C3 slots ahead by 0.6% / 8% / 3.9% in step on three boxes;
+        # C5 packed ahead by 4% on one box, slots by 8% on another.  The HBM bytes are the same
+        # either way (PMC per API), so the difference is the box, not the traffic.
+        api = "recover"
     recover = cfg["decode"] and api in ("recover", "packed")
     rebuilt = dev_buffer(G * r * P, args.rebuilt_offset) if recover else None
     row_start = torch.empty(G, dtype=torch.int32, device="cuda") if cfg["decode"] and api == "packed" else None
