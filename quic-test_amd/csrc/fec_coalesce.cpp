@@ -184,6 +184,16 @@ class Coalescer {
 
   uint32_t capacity() const { return cap; }
 
+  ~Coalescer() {  // process exit, no caller left (shutdown_all)
+    BindDevice bd(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& b : batches)
+      if (b->done) (void)hipEventDestroy(b->done);
+    batches.clear();
+    if (stream) (void)hipStreamDestroy(stream);
+    if (ctx) fec_encoder_free(ctx);
+  }
+
   // The legacy call's body; slab_dev is the slab's device address when it is page-locked.
   int encode(const uint8_t* slab, const uint8_t* slab_dev, const uint32_t* offsets, uint32_t G, uint8_t* repair_out) {
     std::unique_lock<std::mutex> lk(mu);
@@ -467,11 +477,19 @@ class Resident {
   }
 
   // Process exit: ask the running instance to leave and give it a moment (no HIP calls).
-  void shutdown() {
+  // Returns whether no instance runs any more (then the memory may be freed).
+  bool shutdown() {
     __atomic_store_n(&reinterpret_cast<ServerControl*>(ctl.host)->stop, 1, __ATOMIC_RELEASE);
     const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
     while (instance_alive() && std::chrono::steady_clock::now() < until) std::this_thread::yield();
     if (stamps.host) print_stamps();
+    if (instance_alive()) return false;
+    BindDevice bd(device);
+    return bd.ok && hipStreamSynchronize(stream) == hipSuccess;  // the last instance has retired
+  }
+
+  ~Resident() {
+    if (stream) (void)hipStreamDestroy(stream);
   }
 
   // QUICFEC_RESIDENT_STAMPS: mean phase times of the last (up to) 256 served batches, to stderr.
@@ -549,26 +567,37 @@ class Resident {
 };
 
 std::mutex g_reg_mu;
-std::map<std::pair<int, uint32_t>, Coalescer*> g_reg;  // process lifetime (callers may run at exit)
-std::map<int, Resident*> g_resident;                   // per device; NULL when it cannot be set up
-
-void shutdown_residents() {
-  std::lock_guard<std::mutex> lk(g_reg_mu);
-  for (auto& kv : g_resident)
-    if (kv.second) kv.second->shutdown();
-}
-
+std::map<std::pair<int, uint32_t>, Coalescer*> g_reg;  // until process exit (shutdown_all)
 constexpr int kResidentDevices = 64;
 std::atomic<Resident*> g_resident_fast[kResidentDevices];  // set once per device
+std::map<int, Resident*> g_resident;                   // per device; NULL when it cannot be set up
+
+std::atomic<bool> g_shut{false};  // process exit: legacy calls run alone from here on
+std::once_flag g_atexit_once;
+
+// Process exit (std::atexit, registered after the HIP runtime is up, so it runs before the
+// runtime's own teardown): stop every resident instance and free what the coalescers hold.
+// A resident instance that does not leave in time keeps its memory (it may still read it).
+void shutdown_all() {
+  g_shut.store(true, std::memory_order_release);
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (int d = 0; d < kResidentDevices; ++d) g_resident_fast[d].store(nullptr, std::memory_order_release);
+  for (auto& kv : g_resident)
+    if (kv.second && kv.second->shutdown()) delete kv.second;
+  g_resident.clear();
+  for (auto& kv : g_reg) delete kv.second;
+  g_reg.clear();
+}
 
 Resident* resident_for(int device) {
   if (device >= 0 && device < kResidentDevices) {
     if (Resident* r = g_resident_fast[device].load(std::memory_order_acquire)) return r;
   }
+  std::call_once(g_atexit_once, [] { std::atexit(shutdown_all); });
   std::lock_guard<std::mutex> lk(g_reg_mu);
+  if (g_shut.load(std::memory_order_acquire)) return nullptr;
   auto it = g_resident.find(device);
   if (it != g_resident.end()) return it->second;
-  if (g_resident.empty()) std::atexit(shutdown_residents);
   Resident* r = Resident::create(device);
   g_resident.emplace(device, r);
   if (r && device >= 0 && device < kResidentDevices) g_resident_fast[device].store(r, std::memory_order_release);
@@ -576,7 +605,9 @@ Resident* resident_for(int device) {
 }
 
 Coalescer* coalescer_for(int device, uint32_t P) {
+  std::call_once(g_atexit_once, [] { std::atexit(shutdown_all); });
   std::lock_guard<std::mutex> lk(g_reg_mu);
+  if (g_shut.load(std::memory_order_acquire)) return nullptr;
   const auto key = std::make_pair(device, P);
   auto it = g_reg.find(key);
   if (it != g_reg.end()) return it->second;
@@ -591,7 +622,7 @@ Coalescer* coalescer_for(int device, uint32_t P) {
 bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* offsets, uint32_t num_groups,
                             uint32_t packet_size, uint8_t* repair_out, int* rc) {
   const uint64_t t_enter = now_ns();
-  if (env_long("QUICFEC_COALESCE", 1) == 0) return false;
+  if (env_long("QUICFEC_COALESCE", 1) == 0 || g_shut.load(std::memory_order_acquire)) return false;
   if (num_groups > static_cast<uint64_t>(std::max(0L, env_long("QUICFEC_COALESCE_MAX_GROUPS", 64)))) return false;
   void *sdev = nullptr, *rdev = nullptr;
   const HostMem sm = classify_host_pointer(slab, &sdev);

@@ -6,7 +6,9 @@
 # The shim and batcher are compiled with -Xarch_host -fsanitize=address (device code is not
 # instrumented: GPU sanitizers are not available on this pool), the mirror and its test with
 # clang++ -fsanitize=address, against the product's kernel object.  Leak checking is off (the
-# HIP runtime keeps allocations until exit).
+# HIP runtime keeps allocations until exit).  The quarantine is large enough never to recycle
+# during the run: ASan's device-memory allocator CHECK-fails when a device chunk parked in the
+# quarantine is recycled after the HIP runtime has unloaded at exit (sanitizer_allocator_device.h).
 set -euo pipefail
 cd "$(dirname "$0")/.."
 SANK=${SAN:-address}
@@ -18,20 +20,28 @@ case "${1:-run}" in
     SANF="-Xarch_host -fsanitize=$SANK -Xarch_host -fno-omit-frame-pointer"
     $H -x hip -c -o $A/fec_shim.o quic-test_amd/csrc/fec_shim.cpp $SANF
     $H -x hip -c -o $A/fec_batcher.o quic-test_amd/csrc/fec_batcher.cpp $SANF
+    $H -x hip -c -o $A/fec_coalesce.o quic-test_amd/csrc/fec_coalesce.cpp $SANF
     RT=$([ "$SANK" = thread ] && echo "" || echo -shared-libasan)
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -fsanitize=$SANK $RT -o $A/libfec_hip.so \
-      quic-test_amd/lib/fec_kernels.o $A/fec_shim.o $A/fec_batcher.o
+      quic-test_amd/lib/fec_kernels.o $A/fec_shim.o $A/fec_batcher.o $A/fec_coalesce.o
     C="/opt/rocm/llvm/bin/clang++ -O1 -g -std=c++17 -fsanitize=$SANK $RT -fno-omit-frame-pointer -Iinclude -Iquic-test_amd/host"
     $C -fPIC -shared -o $A/libquicfec_host.so quic-test_amd/host/fec.cpp -L$A -lfec_hip -Wl,-rpath,'$ORIGIN'
     $C -o $A/host_mirror_test tests/csrc/host_mirror_test.cpp -L$A -lquicfec_host -lfec_hip oracle/liboracle.so \
       -Wl,-rpath,'$ORIGIN' -Wl,-rpath,'$ORIGIN/../../oracle' -lpthread
+    $C -o $A/ctx_isolation_test tests/csrc/ctx_isolation_test.cpp -L$A -lfec_hip -Wl,-rpath,'$ORIGIN' -lpthread
+    # the unchanged call site from 16 streams through the resident encoder and shared launches
+    $C -o $A/batcher_latency quic-test_amd/csrc/tools/batcher_latency.cpp -Iquic-test_amd/csrc -L$A -lquicfec_host -lfec_hip \
+      oracle/liboracle.so -Wl,-rpath,'$ORIGIN' -Wl,-rpath,'$ORIGIN/../../oracle' -lpthread
     [ "$SANK" = thread ] || cp /opt/rocm/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so $A/
     printf 'called_from_lib:libamdhip64.so\ncalled_from_lib:libhsa-runtime64.so\nrace:libamdhip64.so\nrace:libhsa-runtime64.so\n' > $A/tsan.supp
     ;;
   run)
     export LD_LIBRARY_PATH=$A
-    export ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0:verify_asan_link_order=0:halt_on_error=1
+    export ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0:verify_asan_link_order=0:halt_on_error=1:quarantine_size_mb=16384
     export TSAN_OPTIONS="suppressions=$A/tsan.supp:report_signal_unsafe=0:second_deadlock_stack=1:history_size=4"
     timeout -k 10 600 $A/host_mirror_test
+    timeout -k 10 300 $A/ctx_isolation_test
+    QUICFEC_RESIDENT=1 timeout -k 10 120 $A/batcher_latency legacy 16 0 2
+    QUICFEC_RESIDENT=0 timeout -k 10 120 $A/batcher_latency legacy 16 0 2
     ;;
 esac

@@ -232,3 +232,37 @@ def test_resident_repair_to_pageable_buffer(quicfec_mod, oracle_mod, monkeypatch
         assert quicfec_mod.coalesce_stats()["resident_calls"] == 5
     finally:
         ctx.close()
+
+
+def test_process_exits_promptly_with_resident_instance(tmp_path):
+    """A process that used the resident encoder exits at once: its exit handler stores the stop
+    word and the instance leaves (no kernel outlives its process's last call by more than the
+    poll it is in)."""
+    import subprocess
+    import sys
+    import time
+    from pathlib import Path
+    repo = Path(__file__).resolve().parent.parent
+    code = f"""
+import ctypes, sys, numpy as np
+sys.path.insert(0, {str(repo / 'quic-test_amd')!r})
+import quicfec
+lib = quicfec.load_library()
+ctx = quicfec.Context(device=0)
+P = 1200
+sp, rp = lib.fec_alloc_slab(10 * P), lib.fec_alloc_repair_buffer(P)
+ctypes.memset(sp, 7, 10 * P)
+offs = (np.arange(10, dtype=np.uint32) * P).astype(np.uint32)
+for _ in range(100):
+    assert lib.fec_encode_batch(ctx.handle, sp, offs.ctypes.data, 1, P, rp) == 0
+st = quicfec.coalesce_stats()
+assert st["resident_calls"] == 100, st
+print("CALLS_DONE", flush=True)
+"""
+    env = {**__import__("os").environ, "QUICFEC_COALESCE": "1", "QUICFEC_RESIDENT": "1",
+           "QUICFEC_RESIDENT_IDLE_US": "10000000", "QUICFEC_RESIDENT_LIFE_US": "10000000"}
+    t0 = time.monotonic()
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert out.returncode == 0 and "CALLS_DONE" in out.stdout, out.stdout + out.stderr
+    # with a 10-s idle time the instance would still run at exit: only the stop word ends it
+    assert time.monotonic() - t0 < 60
