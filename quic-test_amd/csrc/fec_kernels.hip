@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "bitslice.hpp"
 #include "coef_tables.hpp"
 #include "fec_kernels.hpp"
 
@@ -292,6 +293,51 @@ __global__ __launch_bounds__(512) void encode_v16(const uint8_t* __restrict__ da
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     st16<POL>(parity + (g * r_total + row0 + static_cast<uint32_t>(i)) * static_cast<uint64_t>(P) + coff, acc[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Encode, bit-sliced (bitslice.hpp): the code's coefficients compiled in, no tables.
+// A lane owns one 16-byte column of two groups: group gl and group gl + tile of its
+// workgroup's 2 * tile groups.  The 32 bytes a lane transposes need not be neighbours —
+// every byte of packet j is multiplied by the same coefficient in every group — so each load
+// instruction of a wave reads 64 consecutive columns exactly as encode_v16 does (a 32-byte
+// chunk of one packet per lane measured 10% slower at k=10 r=3: two runs per instruction and
+// a partial line in every packet).  A second group past the end repeats the first and is not
+// stored.  All R rows, device-contiguous packets.
+// ---------------------------------------------------------------------------------
+template <int K, int R, int W, int POL>
+__global__ __launch_bounds__(512) void encode_bits(const uint8_t* __restrict__ data,
+                                                   uint8_t* __restrict__ parity, uint64_t g_first,
+                                                   uint32_t cpp, uint32_t P, uint32_t tile,
+                                                   uint64_t groups, uint32_t never) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];
+  if (never) occupancy_lds[threadIdx.x] = 0;
+  const uint32_t lane = threadIdx.x;
+  uint32_t gl = lane / cpp;
+  const uint32_t c = lane - gl * cpp;
+  if (gl >= tile) return;
+  gl += xcd_tile(blockIdx.x, gridDim.x) * (2 * tile);
+  if (gl >= groups) return;
+  const bool second = gl + tile < groups;
+  const uint64_t g = g_first + gl, g2 = second ? g + tile : g;
+  const uint32_t o = col_off16(c, P);
+  const uint8_t* base = data + g * K * static_cast<uint64_t>(P) + o;
+  const uint8_t* base2 = data + g2 * K * static_cast<uint64_t>(P) + o;
+  auto load = [&](int j, uint32_t(&x)[8]) {
+    const u32x4 a = ld16<POL>(base + static_cast<uint64_t>(j) * P), b = ld16<POL>(base2 + static_cast<uint64_t>(j) * P);
+    x[0] = a.x, x[1] = a.y, x[2] = a.z, x[3] = a.w;
+    x[4] = b.x, x[5] = b.y, x[6] = b.z, x[7] = b.w;
+  };
+  uint32_t out[R][8];
+  bs::encode_stream<K, R, W>(load, out);
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+    st16<POL>(parity + (g * R + i) * static_cast<uint64_t>(P) + o, u32x4{out[i][0], out[i][1], out[i][2], out[i][3]});
+  if (second) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      st16<POL>(parity + (g2 * R + i) * static_cast<uint64_t>(P) + o, u32x4{out[i][4], out[i][5], out[i][6], out[i][7]});
   }
 }
 
@@ -1623,6 +1669,35 @@ hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
   return hipSuccess;
 }
 
+template <int K, int R, int W, int POL = kNtStore>
+hipError_t run_encode_bits(const EncodeLaunch& a, hipStream_t s) {
+  const uint32_t cpp = (a.P + 15u) / 16u;
+  const int tile_env = env_waves("QUICFEC_ENCODE_TILE", 0);
+  const uint32_t tile = tile_env > 0 && uint32_t(tile_env) * cpp <= 512 ? uint32_t(tile_env) : pick_tile(cpp, a.k, a.P);
+  if (tile == 0) return hipErrorInvalidValue;  // callers route P > 8,192 elsewhere
+  const uint32_t bs = (tile * cpp + 63) / 64 * 64;
+  const uint64_t gchunk = max_wave_blocks() * 2 * tile;
+  for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
+    const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
+    const uint32_t blocks = static_cast<uint32_t>((gn + 2 * tile - 1) / (2 * tile));
+    const int waves = a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_ENCODE_WAVES", 0);
+    const uint32_t smem = occupancy_cap_lds(waves, bs / 64);
+    hipLaunchKernelGGL((encode_bits<K, R, W, POL>), dim3(blocks), dim3(bs), smem, s, a.data, a.parity, g0, cpp, a.P,
+                       tile, gn, 0u);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// Bit-sliced encode for a compile-time shape: QUICFEC_ENCODE_BITS=0 never, 1 for every
+// instantiated shape, default (-1) where it is faster than the tables (r >= 4: the table
+// form is VALU-bound there).
+bool use_encode_bits(uint32_t r) {
+  const int mode = env_waves("QUICFEC_ENCODE_BITS", -1);
+  return mode == 1 || (mode < 0 && r >= 4);
+}
+
 template <int OFF>
 hipError_t run_encode_generic(const EncodeLaunch& a, hipStream_t s) {
   if (a.P < kVecMinP) {
@@ -1674,6 +1749,18 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
       // +1.0% at k=10 r=3 (2.65 vs 2.68 ms), same box, alternating runs
       // (profiles/r02_ab_encode_pair.txt).  QUICFEC_ENCODE_PAIR=0 restores the single form.
       static const bool pair = env_waves("QUICFEC_ENCODE_PAIR", 1) == 1;
+      // Bit-sliced form (bitslice.hpp) while a workgroup holds a whole group's 32-byte chunks
+      if (a.P <= 8192 && use_encode_bits(a.r)) {
+        // packets in flight per lane (bitslice.hpp encode_stream); QUICFEC_ENCODE_BITS_WINDOW
+        const int w = env_waves("QUICFEC_ENCODE_BITS_WINDOW", 4);
+        if (a.k == 20 && a.r == 5)
+          return w >= 20 ? run_encode_bits<20, 5, 20>(a, s) : w >= 8 ? run_encode_bits<20, 5, 8>(a, s)
+                 : w >= 6 ? run_encode_bits<20, 5, 6>(a, s) : w >= 4 ? run_encode_bits<20, 5, 4>(a, s)
+                          : run_encode_bits<20, 5, 2>(a, s);
+        if (a.k == 10 && a.r == 3)
+          return w >= 10 ? run_encode_bits<10, 3, 10>(a, s) : w >= 6 ? run_encode_bits<10, 3, 6>(a, s)
+                 : w >= 4 ? run_encode_bits<10, 3, 4>(a, s) : run_encode_bits<10, 3, 2>(a, s);
+      }
       if (a.k == 10 && a.r == 3)
         return pair ? run_encode_v16<10, 3, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<10, 3, 0, true>(a, 0, s);
       if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 0, true>(a, 0, s);

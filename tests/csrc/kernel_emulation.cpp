@@ -11,6 +11,7 @@
 #include <random>
 #include <vector>
 
+#include "bitslice.hpp"
 #include "coef_tables.hpp"
 #include "gf256.hpp"
 
@@ -54,6 +55,51 @@ static void st32(uint8_t* p, uint32_t v) { std::memcpy(p, &v, 4); }
 static int fail(const char* what, int a, int b, int c) {
   std::printf("MISMATCH %s (%d,%d,%d)\n", what, a, b, c);
   return 1;
+}
+
+// bitslice.hpp against gf256.hpp and the oracle: matrix, transpose, and groups of 1,208-byte
+// packets encoded the way encode_bits maps lanes.
+template <int K, int R>
+static int bitslice_check(std::mt19937_64& rng) {
+  std::vector<uint8_t> M;
+  qfec::parity_matrix(K, R, M);
+  constexpr qfec::bs::CodeMatrix<K, R> CM{};
+  for (int i = 0; i < R; ++i)
+    for (int j = 0; j < K; ++j)
+      if (CM.m[i][j] != M[i * K + j]) return fail("bitslice matrix", K, R, i * K + j);
+  uint32_t t[8], t0[8];
+  for (auto& v : t) v = static_cast<uint32_t>(rng());
+  std::memcpy(t0, t, sizeof t);
+  qfec::bs::transpose8(t);
+  for (int b = 0; b < 8; ++b)
+    for (int q = 0; q < 4; ++q)
+      for (int d = 0; d < 8; ++d)
+        if (((t[b] >> (8 * q + d)) & 1u) != ((t0[d] >> (8 * q + b)) & 1u)) return fail("transpose8", b, q, d);
+  qfec::bs::transpose8(t);
+  if (std::memcmp(t, t0, sizeof t) != 0) return fail("transpose8 involution", K, R, 0);
+  // encode_bits' lane mapping: one 16-byte column (the last shifted back to end at P) of
+  // groups g and g + tile; a second group past the end repeats the first and is not stored.
+  const uint32_t P = 1208, cpp = (P + 15) / 16, tile = 3;
+  const uint64_t G = 5;
+  std::vector<uint8_t> data(G * K * P), par(G * R * P), ref(G * R * P);
+  oracle_fill_splitmix(data.data(), data.size(), rng(), 0);
+  for (uint64_t g = 0; g < tile; ++g)
+    for (uint32_t c = 0; c < cpp; ++c) {
+      const uint32_t o = c * 16 + 16 <= P ? c * 16 : P - 16;
+      const bool second = g + tile < G;
+      const uint64_t gg[2] = {g, second ? g + tile : g};
+      uint32_t x[K][8], out[R][8];
+      for (int j = 0; j < K; ++j)
+        for (int h = 0; h < 2; ++h)
+          for (int w = 0; w < 4; ++w) x[j][4 * h + w] = ld32(&data[(gg[h] * K + j) * P + o + 4 * w]);
+      qfec::bs::encode_chunk<K, R>(x, out);
+      for (int i = 0; i < R; ++i)
+        for (int h = 0; h < (second ? 2 : 1); ++h)
+          for (int w = 0; w < 4; ++w) st32(&par[(gg[h] * R + i) * P + o + 4 * w], out[i][4 * h + w]);
+    }
+  oracle_rs_encode(data.data(), G, K, R, P, ref.data(), 1);
+  if (par != ref) return fail("bitslice encode", K, R, int(P));
+  return 0;
 }
 
 int main() {
@@ -107,6 +153,12 @@ int main() {
       const uint64_t v = t == 1u ? a : t == 2u ? (a * b) >> 1 : (a * b * c) / 6u;
       if (v != qfec::binom().c[n][t]) return fail("choose_small", int(n), int(t), 0);
     }
+  // encode_bits (bitslice.hpp): the compiled-in matrix is gf256.hpp's, the transpose is an
+  // involution, and 32-byte chunks of the bit-sliced encode equal the oracle's parity.
+  if (bitslice_check<20, 5>(rng) || bitslice_check<10, 3>(rng) || bitslice_check<10, 2>(rng) ||
+      bitslice_check<4, 4>(rng))
+    return 1;
+  cases += 4;
   const uint32_t shapes[][3] = {{4, 2, 256}, {10, 3, 1200}, {10, 1, 64}, {20, 5, 96}, {7, 4, 32}, {3, 8, 16}, {1, 1, 8}, {16, 16, 16}, {32, 8, 8}};
   for (const auto& sh : shapes) {
     const uint32_t k = sh[0], r = sh[1], P = sh[2];
