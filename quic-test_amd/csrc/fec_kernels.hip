@@ -301,10 +301,11 @@ __global__ __launch_bounds__(512) void encode_v16(const uint8_t* __restrict__ da
 // A lane owns one 16-byte column of two groups: group gl and group gl + tile of its
 // workgroup's 2 * tile groups.  The 32 bytes a lane transposes need not be neighbours —
 // every byte of packet j is multiplied by the same coefficient in every group — so each load
-// instruction of a wave reads 64 consecutive columns exactly as encode_v16 does (a 32-byte
-// chunk of one packet per lane measured 10% slower at k=10 r=3: two runs per instruction and
-// a partial line in every packet).  A second group past the end repeats the first and is not
-// stored.  All R rows, device-contiguous packets.
+// instruction of a wave reads 64 consecutive columns exactly as encode_v16 does.  A second
+// group past the end repeats the first and is not stored.  All R rows, device-contiguous
+// packets.  Measured alternatives (profiles/r03_ab_bits_*.jsonl): a 32-byte chunk of one packet
+// per lane (two column runs per instruction) 10% slower at k=10 r=3; adjacent groups, or wave
+// pairs over one run of columns, the same as this form; non-temporal loads no better.
 // ---------------------------------------------------------------------------------
 template <int K, int R, int W, int POL>
 __global__ __launch_bounds__(512) void encode_bits(const uint8_t* __restrict__ data,
@@ -1680,6 +1681,7 @@ hipError_t run_encode_bits(const EncodeLaunch& a, hipStream_t s) {
   for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
     const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
     const uint32_t blocks = static_cast<uint32_t>((gn + 2 * tile - 1) / (2 * tile));
+    // uncapped: k=20 r=5 at 12 / 18 / 24 waves per CU within 0.2% (3 waves per SIMD by VGPRs)
     const int waves = a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_ENCODE_WAVES", 0);
     const uint32_t smem = occupancy_cap_lds(waves, bs / 64);
     hipLaunchKernelGGL((encode_bits<K, R, W, POL>), dim3(blocks), dim3(bs), smem, s, a.data, a.parity, g0, cpp, a.P,
@@ -1749,17 +1751,14 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
       // +1.0% at k=10 r=3 (2.65 vs 2.68 ms), same box, alternating runs
       // (profiles/r02_ab_encode_pair.txt).  QUICFEC_ENCODE_PAIR=0 restores the single form.
       static const bool pair = env_waves("QUICFEC_ENCODE_PAIR", 1) == 1;
-      // Bit-sliced form (bitslice.hpp) while a workgroup holds a whole group's 32-byte chunks
+      // Bit-sliced form (bitslice.hpp) while a workgroup holds whole groups.  k=20 r=5 (VALU-
+      // bound with the tables): 5.24-5.41 vs 5.37-5.54 ms over six boxes; k=10 r=3 (HBM-bound
+      // with the tables) 2.74-2.76 vs 2.63-2.66 ms, so opt-in there (QUICFEC_ENCODE_BITS=1).
+      // QUICFEC_ENCODE_BITS_WINDOW: packets in flight per lane (4; 2: 5.70 ms, 8: 5.28, 20: 5.91-6.03).
       if (a.P <= 8192 && use_encode_bits(a.r)) {
-        // packets in flight per lane (bitslice.hpp encode_stream); QUICFEC_ENCODE_BITS_WINDOW
         const int w = env_waves("QUICFEC_ENCODE_BITS_WINDOW", 4);
-        if (a.k == 20 && a.r == 5)
-          return w >= 20 ? run_encode_bits<20, 5, 20>(a, s) : w >= 8 ? run_encode_bits<20, 5, 8>(a, s)
-                 : w >= 6 ? run_encode_bits<20, 5, 6>(a, s) : w >= 4 ? run_encode_bits<20, 5, 4>(a, s)
-                          : run_encode_bits<20, 5, 2>(a, s);
-        if (a.k == 10 && a.r == 3)
-          return w >= 10 ? run_encode_bits<10, 3, 10>(a, s) : w >= 6 ? run_encode_bits<10, 3, 6>(a, s)
-                 : w >= 4 ? run_encode_bits<10, 3, 4>(a, s) : run_encode_bits<10, 3, 2>(a, s);
+        if (a.k == 20 && a.r == 5) return w >= 8 ? run_encode_bits<20, 5, 8>(a, s) : run_encode_bits<20, 5, 4>(a, s);
+        if (a.k == 10 && a.r == 3) return run_encode_bits<10, 3, 4>(a, s);
       }
       if (a.k == 10 && a.r == 3)
         return pair ? run_encode_v16<10, 3, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<10, 3, 0, true>(a, 0, s);

@@ -39,12 +39,15 @@ def test_bits_equals_oracle_and_tables(gpu_ctx, oracle_mod, torch_cuda, monkeypa
     assert np.array_equal(tabs, exp.reshape(-1))
 
 
+@pytest.mark.parametrize("window", ["4", "8"])
 @pytest.mark.parametrize("tile", ["0", "1", "3"])
-def test_bits_tiles_and_chunks(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, tile):
-    """Groups per workgroup (QUICFEC_ENCODE_TILE) and launches split into chunks of
-    QUICFEC_MAX_WAVE_BLOCKS workgroups: every group's rows land at their global place."""
+def test_bits_tiles_and_chunks(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, tile, window):
+    """Groups per workgroup (QUICFEC_ENCODE_TILE), packets in flight per lane
+    (QUICFEC_ENCODE_BITS_WINDOW) and launches split into chunks of QUICFEC_MAX_WAVE_BLOCKS
+    workgroups: every group's rows land at their global place."""
     k, r, P, G = 20, 5, 1200, 1_001
     monkeypatch.setenv("QUICFEC_ENCODE_BITS", "1")
+    monkeypatch.setenv("QUICFEC_ENCODE_BITS_WINDOW", window)
     if tile != "0":
         monkeypatch.setenv("QUICFEC_ENCODE_TILE", tile)
     monkeypatch.setenv("QUICFEC_MAX_WAVE_BLOCKS", "37")
