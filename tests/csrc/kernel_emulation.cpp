@@ -7,6 +7,7 @@
 // codebook-layout bugs before a GPU run.  Prints "OK <cases>" or the first mismatch.
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <random>
 #include <vector>
@@ -156,9 +157,9 @@ int main() {
   // encode_bits (bitslice.hpp): the compiled-in matrix is gf256.hpp's, the transpose is an
   // involution, and 32-byte chunks of the bit-sliced encode equal the oracle's parity.
   if (bitslice_check<20, 5>(rng) || bitslice_check<10, 3>(rng) || bitslice_check<10, 2>(rng) ||
-      bitslice_check<4, 4>(rng))
+      bitslice_check<4, 4>(rng) || bitslice_check<7, 4>(rng) || bitslice_check<9, 6>(rng))
     return 1;
-  cases += 4;
+  cases += 6;
   const uint32_t shapes[][3] = {{4, 2, 256}, {10, 3, 1200}, {10, 1, 64}, {20, 5, 96}, {7, 4, 32}, {3, 8, 16}, {1, 1, 8}, {16, 16, 16}, {32, 8, 8}};
   for (const auto& sh : shapes) {
     const uint32_t k = sh[0], r = sh[1], P = sh[2];
