@@ -856,6 +856,9 @@ def main() -> int:
         }
         if e2e is not None:
             out["e2e_pinned"] = e2e
+        if os.environ.get("QUICFEC_BENCH_ADDRS") == "1":  # placement diagnostics (A/B runs)
+            out["buffers"] = {n: hex(t.data_ptr()) for n, t in (("data", data), ("parity", parity), ("rebuilt", rebuilt))
+                              if t is not None}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -158,6 +158,13 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
   return b < (per << 3) ? (b & 7u) * per + (b >> 3) : b;
 }
 
+// Tile of a decode workgroup by the launch's `swz`: bit 0 the XCD-aware order (xcd_tile),
+// bit 1 the groups from last to first.
+__device__ __forceinline__ uint32_t decode_block(uint32_t swz) {
+  const uint32_t b = (swz & 2u) ? gridDim.x - 1u - blockIdx.x : blockIdx.x;
+  return (swz & 1u) ? xcd_tile(b, gridDim.x) : b;
+}
+
 // Byte offset of 16-byte column `col` inside a packet of P >= 16 bytes: the last column
 // is shifted back to end at P (see the header).
 __device__ __forceinline__ uint32_t col_off16(uint32_t col, uint32_t P) {
@@ -886,7 +893,7 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
                 "scan: mask-addressed inline forms, <= 64 groups per wave or whole 256-group rows per block");
   extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];  // see encode_v16
   if (never) occupancy_lds[threadIdx.x] = 0;
-  const uint64_t wv = static_cast<uint64_t>(swz ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * 4u +
+  const uint64_t wv = static_cast<uint64_t>(decode_block(swz)) * 4u +
                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   const uint32_t lane = threadIdx.x & 63u;
   if constexpr (SCAN > 64) {
@@ -899,7 +906,7 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
     __shared__ uint64_t seg_mask[SCAN];
     __shared__ uint16_t seg_idx[SCAN];
     __shared__ uint32_t seg_cnt[J * 4];
-    const uint64_t g0 = static_cast<uint64_t>(swz ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * SCAN;
+    const uint64_t g0 = static_cast<uint64_t>(decode_block(swz)) * SCAN;
     if (g0 >= groups) return;
     const uint32_t wave = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
     constexpr uint64_t kmask = (1ull << K) - 1;
@@ -1112,7 +1119,7 @@ __global__ __launch_bounds__(256) void decode_wave(uint8_t* __restrict__ data,
   // holding the wave's coefficient rows (see kLdsTabs and decode_fused).
   extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];
   if (never) occupancy_lds[threadIdx.x] = 0;
-  const uint64_t gw = static_cast<uint64_t>(swz ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * 4u +
+  const uint64_t gw = static_cast<uint64_t>(decode_block(swz)) * 4u +
                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   if (gw >= groups) return;
   const uint32_t lane = threadIdx.x & 63u;
@@ -1592,17 +1599,19 @@ inline uint32_t blocks_for(uint64_t n) { return static_cast<uint32_t>((n + 255) 
 // ---------------------------------------------------------------------------------
 namespace {
 
-// XCD-aware group order for a decode kernel: at k=10 r=3 measured +10% for decode_fused and
-// -1%..+5% for decode_wave over two boxes (tools/probe_decode.hip; tunable per kernel).
-uint32_t decode_swizzle(const DecodeLaunch& a, int tuned) {
-  return static_cast<uint32_t>(a.xcd_swizzle >= 0 ? a.xcd_swizzle : tuned);
-}
-
 // Tuning override of an occupancy cap from the environment (-1 = none), else `def`.
 int env_waves(const char* name, int def) {
   const char* v = std::getenv(name);
   return v && *v ? std::atoi(v) : def;
 }
+
+// XCD-aware group order for a decode kernel: at k=10 r=3 measured +10% for decode_fused and
+// -1%..+5% for decode_wave over two boxes (tools/probe_decode.hip; tunable per kernel).
+uint32_t decode_swizzle(const DecodeLaunch& a, int tuned) {
+  // QUICFEC_DECODE_SWIZZLE: 0 / 1 overrides the tuned default (A/B across boxes)
+  return static_cast<uint32_t>(a.xcd_swizzle >= 0 ? a.xcd_swizzle : env_waves("QUICFEC_DECODE_SWIZZLE", tuned));
+}
+
 
 // Groups per workgroup for the tiled mapping: the fewest idle lanes (workgroup = whole
 // waves), preferring tiles whose byte size is a multiple of 128 (tile starts stay
