@@ -26,6 +26,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--trials", type=int, default=4)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--block-orders", action="store_true")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -42,6 +43,7 @@ def main() -> int:
     ctx.encode_dev(data, G, k, r, P, parity, stream=sp)
     masks = torch.from_numpy(bench.erasure_masks(G, k + r, 2, 0x5EED0003).view(np.int64)).to("cuda")
     ctx.decode_prepare(k, r)
+    row_start = torch.empty(G, dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
 
     def timed(d, p, rb):
@@ -73,11 +75,14 @@ def main() -> int:
         rb = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
         rbs.append(rb)
         out("rebuilt", timed(data, parity, rb), data=data, parity=parity, rebuilt=rb)
-        # the decode's block order (QUICFEC_DECODE_SWIZZLE is read at every launch)
-        for swz in ("0", "2", "3"):
-            os.environ["QUICFEC_DECODE_SWIZZLE"] = swz
-            out(f"rebuilt_swz{swz}", timed(data, parity, rb), rebuilt=rb)
-        os.environ.pop("QUICFEC_DECODE_SWIZZLE", None)
+        # the packed rows (no gaps between groups' rows) into the same buffer
+        out("packed", timed_fn(lambda: ctx.recover_packed_dev(data, parity, masks, G, k, r, P, rb, row_start,
+                                                              None, None, stream=sp)), rebuilt=rb)
+        if args.block_orders:
+            for swz in ("0", "2", "3"):   # QUICFEC_DECODE_SWIZZLE is read at every launch
+                os.environ["QUICFEC_DECODE_SWIZZLE"] = swz
+                out(f"rebuilt_swz{swz}", timed(data, parity, rb), rebuilt=rb)
+            os.environ.pop("QUICFEC_DECODE_SWIZZLE", None)
         # the same buffer under a pure write (fill) and a copy from parity (read one, write one)
         out("fill_rebuilt", timed_fn(lambda: ctx.fill_random_dev(rb, rb.numel(), 7, stream=sp)), rebuilt=rb)
         out("copy_parity_to_rebuilt", timed_fn(lambda: ctx.copy_dev(parity, rb, rb.numel(), stream=sp)), rebuilt=rb)
