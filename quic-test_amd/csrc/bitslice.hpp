@@ -7,10 +7,10 @@
 // parity row is those XORs summed over the group's packets.  The parity matrix of the code
 // (gf256.hpp's parity_matrix: Cauchy, normalised so row 0 and column 0 are all ones) is
 // fixed by (k, r), so for a compile-time (K, R) every XOR is decided by the compiler: no
-// table lookups, no selector preparation.  Per data dword at k=20 r=5 that is ~13 VALU
-// operations (the 3-stage bit transpose 6, the plane XORs ~7) against ~27 for the
-// v_perm_b32 tables (fec_kernels.hip encode_v16, 97% VALU issue on MI355X,
-// profiles/r03_sq/sq_c4.json) — the bytes produced are identical.
+// table lookups, no selector preparation.  Per data dword at k=20 r=5 that is ~15 VALU
+// operations (the 3-stage bit transpose 6, plane-subset XORs and row planes ~8, the row-0 XOR
+// and the transposes back) against ~26 for the v_perm_b32 tables (fec_kernels.hip encode_v16,
+// 97% VALU issue on MI355X, profiles/r03_sq/sq_c4.json) — the bytes produced are identical.
 //
 // Used by fec_kernels.hip (encode_bits) and checked on the CPU against the oracle
 // (tests/csrc/kernel_emulation.cpp): the header is plain C++17 so the same code runs on both.
