@@ -86,6 +86,26 @@ def main() -> int:
         # the same buffer under a pure write (fill) and a copy from parity (read one, write one)
         out("fill_rebuilt", timed_fn(lambda: ctx.fill_random_dev(rb, rb.numel(), 7, stream=sp)), rebuilt=rb)
         out("copy_parity_to_rebuilt", timed_fn(lambda: ctx.copy_dev(parity, rb, rb.numel(), stream=sp)), rebuilt=rb)
+    # rebuilt buffers straight from the HIP runtime torch loaded: plain hipMalloc and
+    # hipExtMallocWithFlags(hipDeviceMallocContiguous = 0x4), physically contiguous
+    import ctypes
+    hip_path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
+    hip = ctypes.CDLL(hip_path)
+    raw = []
+    for kind, flags in (("hipMalloc", None), ("contiguous", 0x4), ("hipMalloc", None), ("contiguous", 0x4)):
+        pp = ctypes.c_void_p()
+        nb = ctypes.c_size_t(G * r * P)
+        rc = hip.hipMalloc(ctypes.byref(pp), nb) if flags is None else \
+            hip.hipExtMallocWithFlags(ctypes.byref(pp), nb, ctypes.c_uint(flags))
+        if rc != 0:
+            print(json.dumps({"kind": kind, "error": rc}), flush=True)
+            continue
+        raw.append(pp.value)
+        out(f"raw_{kind}", timed(data, parity, pp.value), rebuilt=torch.empty(0))
+        print(json.dumps({"kind": f"raw_{kind}_addr", "rebuilt": hex(pp.value)}), flush=True)
+    torch.cuda.synchronize()
+    for pv in raw:
+        hip.hipFree(ctypes.c_void_p(pv))
     for t in range(2):
         d2 = data.clone()
         out("data_copy", timed(d2, parity, rbs[0]), data=d2, parity=parity, rebuilt=rbs[0])
