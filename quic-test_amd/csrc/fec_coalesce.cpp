@@ -383,6 +383,35 @@ constexpr uint32_t kResidentOutBytes = 16u << 10;  // per slot: repair rows of c
 
 std::atomic<uint64_t> g_res_calls{0}, g_res_launches{0}, g_res_pre_ns{0}, g_res_wait_ns{0}, g_res_post_ns{0};
 
+// The stream the resident instance runs on.  A persistent kernel occupies its hardware queue:
+// every later kernel on a stream that shares that queue waits until the instance leaves (up to
+// the life bound).  On a plain non-blocking stream, the runtime's queue pool put other streams
+// of the process behind it: their kernels' p99 launch-to-completion went from ~50 us to 33 ms
+// while legacy calls were being served, the context's own stream's p50 to 48 ms
+// (scripts/probe_resident_interference.py, profiles/r03_probe_resident_interference.txt).
+// Streams of another priority come from another queue pool, so the instance runs on a
+// non-blocking stream of the highest priority ("high", the default: other streams' p99 52 us,
+// and the instance's relaunch is dispatched ahead of bulk work); a normal-priority stream of
+// the caller never shares its queue.  QUICFEC_RESIDENT_STREAM: "plain" (the old form), "low"
+// (lowest priority), "cumask" (a CU-masked stream, always a queue of its own, but blocking:
+// it orders against the legacy null stream).
+bool create_server_stream(int device, hipStream_t* s) {
+  const char* v = std::getenv("QUICFEC_RESIDENT_STREAM");
+  const std::string mode = v && *v ? v : "high";
+  if (mode == "cumask") {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return false;
+    std::vector<uint32_t> mask((cus + 31) / 32, 0xFFFFFFFFu);
+    return hipExtStreamCreateWithCUMask(s, static_cast<uint32_t>(mask.size()), mask.data()) == hipSuccess;
+  }
+  if (mode == "high" || mode == "low") {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return false;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, mode == "high" ? hi : lo) == hipSuccess;
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess;
+}
+
 class Resident {
  public:
   static Resident* create(int device) {
@@ -391,7 +420,7 @@ class Resident {
     BindDevice bd(device);
     int khz = 0;
     if (!bd.ok || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0 ||
-        hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) {
+        !create_server_stream(device, &r->stream)) {
       (void)hipGetLastError();
       return nullptr;
     }

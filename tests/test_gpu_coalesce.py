@@ -266,3 +266,57 @@ print("CALLS_DONE", flush=True)
     assert out.returncode == 0 and "CALLS_DONE" in out.stdout, out.stdout + out.stderr
     # with a 10-s idle time the instance would still run at exit: only the stop word ends it
     assert time.monotonic() - t0 < 60
+
+
+def test_resident_does_not_hold_up_other_streams(quicfec_mod, torch_cuda, monkeypatch):
+    """While the resident encoder serves legacy calls (a persistent kernel on its own
+    high-priority stream), kernels the same process launches on its other streams run at once:
+    on a plain stream the runtime's queue pool put some of them behind the resident instance
+    for up to its life bound (p99 33 ms, profiles/r03_probe_resident_interference.txt)."""
+    import time
+    monkeypatch.setenv("QUICFEC_COALESCE", "1")
+    monkeypatch.setenv("QUICFEC_RESIDENT", "1")
+    torch = torch_cuda
+    lib = quicfec_mod.load_library()
+    bg = quicfec_mod.Context(device=0)
+    ctx = quicfec_mod.Context(device=0)
+    G, k, r, P = 500, 10, 3, 1200
+    data = torch.randint(0, 256, (G * k * P,), dtype=torch.uint8, device="cuda")
+    par = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
+    streams = [torch.cuda.Stream() for _ in range(8)]
+    for s in streams:  # warm: module load, first launches
+        ctx.encode_dev(data, G, k, r, P, par, stream=s.cuda_stream)
+        s.synchronize()
+    slab = lib.fec_alloc_slab(10 * P)
+    rep = lib.fec_alloc_repair_buffer(P)
+    offs = (np.arange(10, dtype=np.uint32) * P).astype(np.uint32)
+    stop = threading.Event()
+    calls = [0]
+
+    def background():
+        while not stop.is_set():
+            assert lib.fec_encode_batch(bg.handle, slab, offs.ctypes.data, 1, P, rep) == 0
+            calls[0] += 1
+
+    th = threading.Thread(target=background)
+    th.start()
+    try:
+        time.sleep(0.05)
+        lat = []
+        for i in range(96):
+            s = streams[i % len(streams)]
+            t0 = time.perf_counter()
+            ctx.encode_dev(data, G, k, r, P, par, stream=s.cuda_stream)
+            s.synchronize()
+            lat.append(time.perf_counter() - t0)
+            time.sleep(0.001)
+    finally:
+        stop.set()
+        th.join()
+        lib.fec_free_slab(slab)
+        lib.fec_free_repair_buffer(rep)
+        bg.close()
+        ctx.close()
+    assert calls[0] > 100, calls[0]  # the resident path was busy the whole time
+    slow = [x for x in lat if x > 0.02]
+    assert len(slow) <= 1, f"{len(slow)} of {len(lat)} launches took > 20 ms: {sorted(lat)[-5:]}"
