@@ -648,6 +648,11 @@ Coalescer* coalescer_for(int device, uint32_t P) {
 
 }  // namespace
 
+void coalesce_prepare(int device) {
+  if (env_long("QUICFEC_COALESCE", 1) == 0 || env_long("QUICFEC_RESIDENT", 1) == 0) return;
+  (void)resident_for(device);
+}
+
 bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* offsets, uint32_t num_groups,
                             uint32_t packet_size, uint8_t* repair_out, int* rc) {
   const uint64_t t_enter = now_ns();

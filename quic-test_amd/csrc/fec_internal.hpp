@@ -31,4 +31,8 @@ void set_last_error(const char* msg);
 bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* offsets, uint32_t num_groups,
                             uint32_t packet_size, uint8_t* repair_out, int* rc);
 
+// Sets up the resident encoder's page-locked ring for `device` ahead of the first legacy call
+// (no kernel launch; that happens on the first call).
+void coalesce_prepare(int device);
+
 }  // namespace qfec

@@ -369,6 +369,27 @@ struct FECEncoderCtx {
 
 namespace {
 
+// The first kernel launched on a device loads the library's code object there (all kernels of
+// fec_kernels.hip at once), and the resident encoder's first call allocates its page-locked
+// ring: together ~26 ms that otherwise land on the first fec_encode_batch of the process — the
+// first repair packet of the first QUIC stream (batcher_latency legacy_raw: max delay 25.8-27.5
+// ms without, 11.5-12.2 ms with the code object loaded here).  Done once per device, at the
+// first context; failures are left to the calls that follow (they report them).
+void warm_device_once(int device, hipStream_t s) {
+  constexpr int kMaxWarm = 64;
+  static std::once_flag once[kMaxWarm];
+  if (device < 0 || device >= kMaxWarm || std::getenv("QUICFEC_NO_WARMUP") != nullptr) return;
+  std::call_once(once[device], [&] {
+    uint8_t* p = nullptr;
+    if (hipMalloc(&p, 256) == hipSuccess) {
+      if (qfec::launch_fill_splitmix(p, 256, 0, 0, s) == hipSuccess) (void)hipStreamSynchronize(s);
+      (void)hipFree(p);
+    }
+    (void)hipGetLastError();
+    qfec::coalesce_prepare(device);
+  });
+}
+
 FECEncoderCtx* make_ctx(double redundancy, uint32_t max_groups, int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
@@ -400,6 +421,7 @@ FECEncoderCtx* make_ctx(double redundancy, uint32_t max_groups, int device) {
     delete ctx;
     return nullptr;
   }
+  warm_device_once(device, ctx->stream);
   return ctx;
 }
 
