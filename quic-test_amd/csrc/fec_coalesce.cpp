@@ -633,9 +633,17 @@ Resident* resident_for(int device) {
   return r;
 }
 
+// Set while this thread holds g_reg_mu in coalescer_for: Coalescer::create makes a context,
+// whose first-context warm-up must not take g_reg_mu again (coalesce_prepare skips then).
+thread_local bool t_holds_reg = false;
+
 Coalescer* coalescer_for(int device, uint32_t P) {
   std::call_once(g_atexit_once, [] { std::atexit(shutdown_all); });
   std::lock_guard<std::mutex> lk(g_reg_mu);
+  struct Flag {
+    Flag() { t_holds_reg = true; }
+    ~Flag() { t_holds_reg = false; }
+  } flag;
   if (g_shut.load(std::memory_order_acquire)) return nullptr;
   const auto key = std::make_pair(device, P);
   auto it = g_reg.find(key);
@@ -649,7 +657,7 @@ Coalescer* coalescer_for(int device, uint32_t P) {
 }  // namespace
 
 void coalesce_prepare(int device) {
-  if (env_long("QUICFEC_COALESCE", 1) == 0 || env_long("QUICFEC_RESIDENT", 1) == 0) return;
+  if (t_holds_reg || env_long("QUICFEC_COALESCE", 1) == 0 || env_long("QUICFEC_RESIDENT", 1) == 0) return;
   (void)resident_for(device);
 }
 
