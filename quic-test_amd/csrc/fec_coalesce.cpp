@@ -509,6 +509,10 @@ class Resident {
   // Returns whether no instance runs any more (then the memory may be freed).
   bool shutdown() {
     __atomic_store_n(&reinterpret_cast<ServerControl*>(ctl.host)->stop, 1, __ATOMIC_RELEASE);
+    // Never launched (set up ahead of a first call that did not come, coalesce_prepare): no HIP
+    // call at exit -- under rocprofv3 the tool has finalised by now and a runtime call there
+    // aborted the process; the memory goes with the process.
+    if (gen.load(std::memory_order_acquire) == 0) return false;
     const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
     while (instance_alive() && std::chrono::steady_clock::now() < until) std::this_thread::yield();
     if (stamps.host) print_stamps();
