@@ -320,3 +320,41 @@ def test_resident_does_not_hold_up_other_streams(quicfec_mod, torch_cuda, monkey
     assert calls[0] > 100, calls[0]  # the resident path was busy the whole time
     slow = [x for x in lat if x > 0.02]
     assert len(slow) <= 1, f"{len(slow)} of {len(lat)} launches took > 20 ms: {sorted(lat)[-5:]}"
+
+
+def test_first_legacy_call_of_a_process_is_not_a_spike(tmp_path):
+    """The first context on a device loads the kernels and sets up the resident ring, so the
+    first fec_encode_batch of a fresh process (the first repair packet of the first stream)
+    does not pay ~26 ms for them (profiles/r03_first_call_warmup.jsonl)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parent.parent
+    code = r'''
+import ctypes, sys, time
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import quicfec
+lib = quicfec.load_library()
+ctx = lib.fec_encoder_new(0.1, 64)
+assert ctx
+P = 1200
+slab = lib.fec_alloc_slab(10 * P)
+rep = lib.fec_alloc_repair_buffer(P)
+offs = (np.arange(10, dtype=np.uint32) * P).astype(np.uint32)
+t0 = time.perf_counter()
+rc = lib.fec_encode_batch(ctx, slab, offs.ctypes.data, 1, P, rep)
+dt = time.perf_counter() - t0
+assert rc == 0, rc
+print(f"{dt * 1e6:.1f}")
+lib.fec_free_slab(slab)
+lib.fec_free_repair_buffer(rep)
+lib.fec_encoder_free(ctx)
+'''
+    env = {k: v for k, v in os.environ.items() if not k.startswith("QUICFEC_")}
+    out = subprocess.run([sys.executable, "-c", code, str(repo / "quic-test_amd")], capture_output=True, text=True,
+                         timeout=120, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    first_us = float(out.stdout.strip().splitlines()[-1])
+    assert first_us < 5000, f"first legacy call took {first_us:.0f} us"
