@@ -172,27 +172,6 @@ def spawn_ranks(n: int, argv: list[str], check_devices: bool = True) -> int:
     return rc if rc >= 0 else 1
 
 
-def launch_selftest(args) -> int:
-    """CPU-only check of the launch path (tests/test_distributed.py): every rank joins a
-    gloo group, reduces like the bench does, and rank 0 prints one JSON line."""
-    import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    if world > 1:
-        dist.init_process_group(backend="gloo", init_method="env://")
-    G = 1000
-    g0, g1 = shard_range(G * world, rank, world)
-    mx = reduce_max(0.25 * (rank + 1))
-    total = reduce_sum(float(g1 - g0))
-    barrier()
-    if rank == 0:
-        print(json.dumps({"selftest": True, "n_gpus": world, "gpus_arg": args.gpus, "max_elapsed": mx,
-                          "total_groups": total}), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
-    return 0
-
-
 # ----------------------------------------------------------------------------- helpers
 def shard_range(total_groups: int, rank: int, world: int) -> tuple[int, int]:
     """Contiguous [g0, g1) slice of the global group stream owned by `rank`."""
@@ -529,24 +508,50 @@ def lib_sha256() -> str:
     return hashlib.sha256(Path(quicfec.LIB_PATH).read_bytes()).hexdigest()
 
 
-def load_pmc_traffic(config: str):
+def workload_key(cfg: dict, G: int) -> dict:
+    """What a PMC file's bytes were measured on: the code shape, groups per GPU and loss model.
+    roofline.traffic is taken from a profiles/pmc_<config>.json only when its recorded workload
+    equals this one field for field (a --shape / --groups / --loss override gets null)."""
+    return {"k": int(cfg["k"]), "r": int(cfg["r"]), "P": int(cfg["P"]), "groups": int(G),
+            "erasures": int(cfg["erasures"]) if cfg.get("erasures") else None,
+            "loss": float(cfg["loss"]) if cfg.get("loss") else None}
+
+
+def workload_of_line(line: dict) -> dict:
+    """workload_key() of the run that printed this bench JSON line (scripts/pmc_summary.py)."""
+    c = line["config"]
+    return {"k": int(c["k"]), "r": int(c["r"]), "P": int(c["packet_bytes"]), "groups": int(c["groups_per_gpu"]),
+            "erasures": int(c["erasures_per_group"]) if c.get("erasures_per_group") else None,
+            "loss": float(c["iid_loss"]) if c.get("iid_loss") else None}
+
+
+def load_pmc_traffic(config: str, workload: dict, path=None, sha: str | None = None):
     """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/pmc_<config>.json,
     scripts/gpu_pmc.sh), used only when they were measured on this very library build (the
-    file's lib_sha256 equals the loaded .so's).  Returns (pmc dict or None, note)."""
-    p = REPO / "profiles" / f"pmc_{config}.json"
+    file's lib_sha256 equals the loaded .so's) AND on this exact workload (the file's `workload`,
+    recorded by scripts/pmc_summary.py from the profiled bench line, equals `workload`).
+    Returns (pmc dict or None, note naming the source or the mismatch)."""
+    p = Path(path) if path is not None else REPO / "profiles" / f"pmc_{config}.json"
+    name = f"profiles/{p.name}"
     if not p.exists():
-        return None, f"no profiles/pmc_{config}.json"
+        return None, f"no {name}"
     try:
         pmc = json.loads(p.read_text())
     except (OSError, ValueError):
-        return None, f"unreadable profiles/pmc_{config}.json"
-    if pmc.get("lib_sha256") != lib_sha256():
-        return None, f"profiles/pmc_{config}.json was measured on another build of libfec_hip.so"
-    return pmc, f"profiles/pmc_{config}.json (rocprofv3 PMC on this build, lib_sha256 {pmc['lib_sha256'][:16]})"
+        return None, f"unreadable {name}"
+    if pmc.get("lib_sha256") != (sha if sha is not None else lib_sha256()):
+        return None, f"{name} was measured on another build of libfec_hip.so"
+    wl = pmc.get("workload")
+    if not isinstance(wl, dict):
+        return None, f"{name} records no workload: not attributable to this run"
+    diff = [f"{f}={wl.get(f)!r} there vs {workload[f]!r} here" for f in workload if wl.get(f) != workload[f]]
+    if diff:
+        return None, f"{name} was measured on another workload ({'; '.join(diff)})"
+    return pmc, f"{name} (rocprofv3 PMC on this build, lib_sha256 {pmc['lib_sha256'][:16]}, same workload)"
 
 
 # ----------------------------------------------------------------------------- main
-def main() -> int:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -564,8 +569,8 @@ def main() -> int:
     ap.add_argument("--decode-api", default="auto", choices=("auto", "packed", "recover", "in-place"),
                     help="packed: fec_recover_batch_rs_dev_packed (all groups' rebuilt packets back to back, as "
                          "the reference decoder returns its Recovered list); recover: fec_recover_batch_rs_dev "
-                         "((g*r + m)*P slots); in-place: fec_decode_batch_rs_dev; auto: packed where the shape has "
-                         "a mask-addressed form, else recover")
+                         "((g*r + m)*P slots); in-place: fec_decode_batch_rs_dev; auto: packed for sparse loss "
+                         "(a loss profile), else recover")
     ap.add_argument("--null-stream", action="store_true",
                     help="launch through stream handle 0 (the context's own stream) with events on torch's "
                          "default stream, as round-1/2 benches did (A/B of the timing setup)")
@@ -573,19 +578,343 @@ def main() -> int:
     ap.add_argument("--rebuilt-offset", type=int, default=0, help="rebuilt-packet buffer placement (bytes)")
     ap.add_argument("--no-other-api", action="store_true",
                     help="skip the comparison run of the other decode API (PMC passes keyed per API)")
+    ap.add_argument("--legs", default="auto", choices=("auto", "on", "off"),
+                    help="after the headline, measure the other multi-GPU BASELINE configs in the same ranks: "
+                         "C4 (k=20 r=5 encode) and C5 (satellite loss, device-resident and host-resident with "
+                         "H2D/D2H); auto = on when N > 1")
+    ap.add_argument("--leg-groups", type=int, default=0, help="groups per GPU of the legs (default: each config's)")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+# The other multi-GPU BASELINE lines, measured after the headline when N > 1 (--legs): C4
+# (configs[3], 8M groups over 8 GPUs = 1M per GPU, encode) and C5 (configs[4], satellite loss,
+# "timed with H2D/D2H copies": device-resident step plus the host-resident legs).
+LEGS = (("c4", "c4", False), ("c5_e2e", "c5", True))
+
+
+def legs_enabled(args, world: int) -> bool:
+    return args.legs == "on" or (args.legs == "auto" and world > 1)
+
+
+def leg_section(res: dict) -> dict:
+    """A leg's entry in rank 0's JSON line: the same quantities as the headline (payload of all
+    ranks / the slowest rank's time, per-kernel timings, roofline) for that config."""
+    keep = ("workload", "value", "unit", "ranks", "groups_per_gpu", "steps", "warmup", "ms_per_step", "verified",
+            "decode_api", "kernels", "roofline", "e2e_pinned")
+    return {k: res[k] for k in keep if k in res}
+
+
+def run_legs(measure_leg) -> dict:
+    """measure_leg(config) -> result dict, on every rank in the same order (its collectives
+    line up); returns {section: leg_section(...)}."""
+    return {section: leg_section(measure_leg(config, e2e)) for section, config, e2e in LEGS}
+
+
+def launch_selftest(args) -> int:
+    """CPU-only check of the launch path (tests/test_distributed.py): every rank joins a
+    gloo group, reduces like the bench does (headline and legs), and rank 0 prints one JSON
+    line with the same sections as the real bench."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="gloo", init_method="env://")
+    G = 1000
+    g0, g1 = shard_range(G * world, rank, world)
+    mx = reduce_max(0.25 * (rank + 1))
+    total = reduce_sum(float(g1 - g0))
+
+    def fake_leg(config: str, e2e: bool) -> dict:
+        cfg = CONFIGS[config]
+        barrier()
+        t = reduce_max(0.01 * (rank + 1))
+        ranks = int(reduce_sum(1.0))
+        res = {"workload": cfg["workload"], "value": ranks * G * cfg["k"] * cfg["P"] / t / 2**30, "unit": "GiB/s",
+               "ranks": ranks, "groups_per_gpu": G, "ms_per_step": t * 1e3, "verified": True}
+        if e2e:
+            res["e2e_pinned"] = {"ranks": ranks}
+        return res
+
+    legs = run_legs(fake_leg) if legs_enabled(args, world) else None
+    barrier()
+    if rank == 0:
+        line = {"selftest": True, "n_gpus": world, "gpus_arg": args.gpus, "max_elapsed": mx, "total_groups": total}
+        if legs:
+            line.update(legs)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+class Bench:
+    """One rank's measurement state: context, stream, the rank's place in the job."""
+
+    def __init__(self, args, rank: int, world: int, local: int):
+        import torch
+        import quicfec
+        self.args, self.rank, self.world = args, rank, world
+        self.ctx = quicfec.Context(device=local)
+        # One stream for everything: the library's launches, torch's ops and the timing events.
+        # torch's default stream has handle 0, which the C-ABI reads as "the context's own
+        # stream" (a blocking stream); launching there while recording events on the default
+        # stream made every event an implicit cross-stream synchronisation inside the timed steps
+        # (~15-60 us per kernel, profiles/r02_stream_ab.txt).  --null-stream keeps that old setup.
+        if args.null_stream:
+            self.stream = torch.cuda.current_stream()
+        else:
+            self.stream = torch.cuda.Stream()
+            torch.cuda.set_stream(self.stream)
+        self.sp = self.stream.cuda_stream
+        self.copy = None  # the box's copy rate (measured once per process)
+
+    def measure(self, config: str, cfg: dict, G: int, steps: int, warmup: int, api: str, verify: bool,
+                other_api: bool, e2e: bool) -> dict:
+        """One workload on this rank: verify, W untimed + K timed steps between barriers, per-kernel
+        timings, roofline.  Every rank calls it with the same arguments (collectives line up)."""
+        import numpy as np
+        import torch
+        args, rank, world, ctx, stream, sp = self.args, self.rank, self.world, self.ctx, self.stream, self.sp
+        k, r, P = cfg["k"], cfg["r"], cfg["P"]
+        g0, _ = shard_range(G * world, rank, world)
+
+        def dev_buffer(nbytes: int, offset: int):
+            """nbytes of HBM starting `offset` bytes into a fresh allocation (buffer placement A/B)."""
+            if offset <= 0:
+                return torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+            return torch.empty(nbytes + offset, dtype=torch.uint8, device="cuda")[offset:]
+
+        data = torch.empty(G * k * P, dtype=torch.uint8, device="cuda")
+        parity = dev_buffer(G * r * P, args.parity_offset)
+        # this rank's slice of one global synthetic stream
+        ctx.fill_random_dev(data, data.numel(), SEED + 2, byte_offset=g0 * k * P, stream=sp)
+        dec_bytes = dec_read = 0
+        if api == "auto":
+            # Sparse loss (a loss profile: C5 ~10% of groups lose data): the packed rows, whose
+            # one-launch form (recover_runs: rows leave each workgroup as one run) beats the slot
+            # rows by 7-15% (profiles/r04_probe_runs_*.txt).  Dense loss (C3): the slot rows,
+            # which never lost by more than 4% on any box measured against packed rows
+            # (profiles/r03_final/ab_decode_api_box*.jsonl; same HBM bytes by PMC, DESIGN §5).
+            api = "packed" if cfg.get("loss") and packed_supported(k, r, P) else "recover"
+        recover = cfg["decode"] and api in ("recover", "packed")
+        rebuilt = dev_buffer(G * r * P, args.rebuilt_offset) if recover else None
+        row_start = torch.empty(G, dtype=torch.int32, device="cuda") if cfg["decode"] and api == "packed" else None
+        masks = None
+
+        def decode_call(api: str, status=None):
+            if api == "packed":
+                ctx.recover_packed_dev(data, parity, masks, G, k, r, P, rebuilt, row_start, None, status, stream=sp)
+            elif api == "recover":
+                ctx.recover_dev(data, parity, masks, G, k, r, P, rebuilt, status, stream=sp)
+            else:
+                ctx.decode_dev(data, parity, masks, G, k, r, P, status, stream=sp)
+
+        if cfg["decode"]:
+            masks_h = make_masks(cfg, G, SEED + 3 + rank)
+            dec_bytes = decode_algorithmic_bytes(masks_h, k, r, P)
+            dec_read = decode_algorithmic_bytes(masks_h, k, r, P, reads_only=True)
+            masks = torch.from_numpy(masks_h.view(np.int64)).to("cuda")
+            ctx.decode_prepare(k, r)
+            # the receiver knows its loss profile: share of groups that lose a data shard (a
+            # dense caller says so too: the library's scan form is for sparse loss only)
+            ctx.decode_loss_hint(1.0 - (1.0 - cfg["loss"]) ** k if cfg.get("loss") else -1.0)
+        torch.cuda.synchronize()
+
+        verified = None
+        if verify:
+            # correctness of this exact configuration before timing: encode, poison the erased
+            # data shards, rebuild, compare with the untouched copy; sampled groups vs oracle
+            # parity are covered by tests/test_gpu_parity.py.
+            orig = data.clone()
+            ctx.encode_dev(data, G, k, r, P, parity, stream=sp)
+            if cfg["decode"]:
+                bits = torch.arange(k, device="cuda", dtype=torch.int64)
+                lost = ((masks.view(G, 1) >> bits.view(1, k)) & 1).bool()
+                data.view(G, k, P)[lost] = 0xEE
+                st = torch.zeros(G, dtype=torch.uint8, device="cuda")
+                decode_call(api, st)
+                torch.cuda.synchronize()
+                bad_exp = unrecoverable_count(masks_h, k, r)
+                n_bad = int(st.sum().item())
+                ok_rows = st == 0
+                if api == "packed":
+                    # rows back to back in (g, j ascending) order: boolean indexing's order
+                    want = orig.view(G, k, P)[lost & ok_rows.view(G, 1)]
+                    got = rebuilt.view(-1, P)[:want.shape[0]]
+                    verified = bool(torch.equal(got, want)) and n_bad == bad_exp
+                    data.copy_(orig)
+                elif recover:
+                    # slot m of group g = its m-th lost data shard: the same (g, j ascending) order
+                    # as boolean indexing of the lost shards
+                    e_g = lost.sum(dim=1, keepdim=True)
+                    slots = torch.arange(r, device="cuda").view(1, r) < e_g
+                    got = rebuilt.view(G, r, P)[slots & ok_rows.view(G, 1)]
+                    want = orig.view(G, k, P)[lost & ok_rows.view(G, 1)]
+                    verified = bool(torch.equal(got, want)) and n_bad == bad_exp
+                    data.copy_(orig)
+                elif n_bad == 0:
+                    verified = bool(torch.equal(data, orig)) and bad_exp == 0
+                else:
+                    verified = bool(torch.equal(data.view(G, -1)[ok_rows], orig.view(G, -1)[ok_rows])) and n_bad == bad_exp
+            else:
+                # encode-only config: the library's decoder (separate kernels, table arithmetic)
+                # rebuilds r erased shards of every group, data and parity mixed, from the parity
+                # just written -- a size-independent round trip of every parity row (the encode
+                # against the oracle on sampled groups is in tests/)
+                vm_h = erasure_masks(G, k + r, r, SEED + 7 + rank)
+                vm = torch.from_numpy(vm_h.view(np.int64)).to("cuda")
+                ctx.decode_prepare(k, r)
+                bits = torch.arange(k, device="cuda", dtype=torch.int64)
+                lost = ((vm.view(G, 1) >> bits.view(1, k)) & 1).bool()
+                data.view(G, k, P)[lost] = 0xEE
+                st = torch.zeros(G, dtype=torch.uint8, device="cuda")
+                rb = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
+                ctx.recover_dev(data, parity, vm, G, k, r, P, rb, st, stream=sp)
+                torch.cuda.synchronize()
+                e_g = lost.sum(dim=1, keepdim=True)
+                slots = torch.arange(r, device="cuda").view(1, r) < e_g
+                verified = bool(torch.equal(rb.view(G, r, P)[slots], orig.view(G, k, P)[lost])) and int(st.sum().item()) == 0
+                data.copy_(orig)
+                del rb, vm, lost, slots, st
+            del orig
+            torch.cuda.empty_cache()
+
+        def step(ev=None):
+            if ev is not None:
+                ev[0].record(stream)
+            ctx.encode_dev(data, G, k, r, P, parity, stream=sp)
+            if ev is not None:
+                ev[1].record(stream)
+            if cfg["decode"]:
+                decode_call(api)
+                if ev is not None:
+                    ev[2].record(stream)
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(events[i])
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / steps
+        dec_ms = (sum(e[1].elapsed_time(e[2]) for e in events) / steps) if cfg["decode"] else 0.0
+
+        elapsed_max = reduce_max(elapsed)
+        if verified is not None:  # every rank must have rebuilt its shard exactly
+            verified = reduce_max(0.0 if verified else 1.0) == 0.0
+        total_groups = reduce_sum(float(G))
+        ranks = int(reduce_sum(1.0))
+        payload = total_groups * k * P * steps
+        value = payload / elapsed_max / 2**30
+        ms_per_step = elapsed_max / steps * 1e3
+
+        enc_bytes = (k + r) * P * G
+        enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
+        kernels = {"encode": {"ms": round(enc_ms, 4), "algorithmic_bytes": enc_bytes,
+                              "achieved_GBps": round(enc_gbs, 1),
+                              "payload_GiBps": round(k * P * G / (enc_ms * 1e-3) / 2**30, 2)}}
+        if cfg["decode"]:
+            dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
+            kernels["decode"] = {"ms": round(dec_ms, 4), "algorithmic_bytes": dec_bytes,
+                                 "achieved_GBps": round(dec_gbs, 1),
+                                 "payload_GiBps": round(k * P * G / (dec_ms * 1e-3) / 2**30, 2)}
+        # Each kernel alone, back to back (decode is idempotent on rebuilt data): its own time,
+        # without the write-back of the other kernel's output still draining from the caches
+        # when it starts (which the in-step times above include).
+        reps = max(5, steps // 4)
+
+        def isolated(fn, nbytes):
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+            evs[0].record(stream)
+            for i in range(reps):
+                fn()
+                evs[i + 1].record(stream)
+            torch.cuda.synchronize()
+            ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(reps))[reps // 2]
+            return {"ms_median": round(ms, 4), "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1)}
+
+        kernels["encode"]["isolated"] = isolated(lambda: ctx.encode_dev(data, G, k, r, P, parity, stream=sp), enc_bytes)
+        if cfg["decode"]:
+            kernels["decode"]["api"] = api
+            kernels["decode"]["isolated"] = isolated(lambda: decode_call(api), dec_bytes)
+            # the other decode API on the same buffers, for comparison (not in `value`)
+            other = {"packed": "recover", "recover": "in-place"}.get(api, "recover")
+            if other_api:
+                if other == "recover" and rebuilt is None:
+                    rebuilt = dev_buffer(G * r * P, args.rebuilt_offset)
+                kernels["decode"]["other_api"] = {"api": other, **isolated(lambda: decode_call(other), dec_bytes)}
+        # The box's own HBM copy rate (fec_copy_dev: the encode's 16-B-per-lane pattern, no
+        # arithmetic), measured the same way once per process: box-to-box spread is a few
+        # percent, so the kernels are also quoted against it.
+        if self.copy is None:
+            half = (data.numel() // 2) // 16 * 16
+            scratch = torch.empty(half, dtype=torch.uint8, device="cuda")
+            self.copy = isolated(lambda: ctx.copy_dev(data, scratch, half, stream=sp), 2 * half)
+            del scratch
+            torch.cuda.empty_cache()
+        copy = self.copy
+        dom = max(kernels, key=lambda n: kernels[n]["ms"])
+        dom_read = k * P * G if dom == "encode" else dec_read
+        wl = workload_key(cfg, G)
+        pmc, pmc_note = load_pmc_traffic(config, wl)
+        pmc = pmc or {}
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["achieved_GBps"],
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(kernels[dom]["achieved_GBps"] / HBM_PEAK_GBS, 4),
+                    # PMC entries are keyed per decode API (recover_packed / recover_slots / decode)
+                    "traffic": pmc.get(pmc_key(dom, api) if cfg["decode"] else dom, {}).get("hbm_bytes_per_launch"),
+                    "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes"],
+                    "traffic_source": pmc_note,
+                    "read_frac": round(dom_read / (kernels[dom]["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "read_frac_of_box_copy": round(dom_read / (kernels[dom]["ms"] * 1e-3) / 1e9 / copy["achieved_GBps"], 4),
+                    # north_star's "70% of the HBM-read roofline": reads at 0.70 x 8 TB/s while this
+                    # kernel also writes its bytes needs this much total traffic -- above the box's
+                    # copy ceiling (box_copy_GBps), so that literal target is out of reach (DESIGN §5)
+                    "read_target_total_GBps": round(0.70 * HBM_PEAK_GBS * kernels[dom]["algorithmic_bytes"] / dom_read, 1),
+                    "box_copy_GBps": copy["achieved_GBps"],
+                    "frac_of_box_copy": round(kernels[dom]["achieved_GBps"] / copy["achieved_GBps"], 4),
+                    "timing": ("torch.cuda.Event on torch's default stream, kernels on the context's stream"
+                               if args.null_stream else
+                               "torch.cuda.Event on the launch stream (one torch stream for launches, ops and "
+                               "events), averaged over the timed steps")}
+        res = {"workload": cfg["workload"], "value": round(value, 3), "unit": "GiB/s", "ranks": ranks,
+               "groups_per_gpu": G, "steps": steps, "warmup": warmup, "ms_per_step": round(ms_per_step, 4),
+               "verified": verified, "decode_api": api if cfg["decode"] else None,
+               "kernels": kernels, "roofline": roofline, "workload_key": wl}
+        if e2e:
+            res["e2e_pinned"] = e2e_pinned(ctx, data, parity, masks if cfg["decode"] else None, G, cfg)
+        if os.environ.get("QUICFEC_BENCH_ADDRS") == "1":  # placement diagnostics (A/B runs)
+            res["buffers"] = {n: hex(t.data_ptr()) for n, t in (("data", data), ("parity", parity), ("rebuilt", rebuilt))
+                              if t is not None}
+        del data, parity, rebuilt, row_start, masks
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        return res
+
+
+DECODE_API_TEXT = {"packed": "fec_recover_batch_rs_dev_packed (rebuilt packets of all groups back to back with "
+                             "per-group row starts, decoder.go Recovered list)",
+                   "recover": "fec_recover_batch_rs_dev (rebuilt packets at (g*r + m)*P slots)",
+                   "in-place": "fec_decode_batch_rs_dev (in place)"}
+
+
+def main() -> int:
+    args = parse_args()
     mode, n = launch_plan(args.gpus, os.environ)
     if mode == "spawn":
         return spawn_ranks(n, sys.argv[1:])
     if args.launch_selftest:
         return launch_selftest(args)
 
-    import numpy as np
     import torch
     import torch.distributed as dist
-    import quicfec
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -604,265 +933,57 @@ def main() -> int:
         cfg["k"], cfg["r"], cfg["P"] = (int(x) for x in args.shape.split(","))
         cfg["erasures"] = min(cfg["erasures"], cfg["r"])
         cfg["workload"] += f" (shape override k={cfg['k']} r={cfg['r']} P={cfg['P']})"
-    k, r, P = cfg["k"], cfg["r"], cfg["P"]
     G = args.groups or cfg["groups"]
     if args.groups:
         cfg["workload"] += f" (groups override: {G}/GPU)"
-    g0, _ = shard_range(G * world, rank, world)
 
-    ctx = quicfec.Context(device=local)
-    # One stream for everything: the library's launches, torch's ops and the timing events.
-    # torch's default stream has handle 0, which the C-ABI reads as "the context's own
-    # stream" (a blocking stream); launching there while recording events on the default
-    # stream made every event an implicit cross-stream synchronisation inside the timed steps
-    # (~15-60 us per kernel, profiles/r02_stream_ab.txt).  --null-stream keeps that old setup.
-    if args.null_stream:
-        stream = torch.cuda.current_stream()
-    else:
-        stream = torch.cuda.Stream()
-        torch.cuda.set_stream(stream)
-    sp = stream.cuda_stream
+    bench = Bench(args, rank, world, local)
+    head = bench.measure(args.config, cfg, G, args.steps, args.warmup, args.decode_api, not args.no_verify,
+                         not args.no_other_api, args.e2e)
 
-    def dev_buffer(nbytes: int, offset: int):
-        """nbytes of HBM starting `offset` bytes into a fresh allocation (buffer placement A/B)."""
-        if offset <= 0:
-            return torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-        return torch.empty(nbytes + offset, dtype=torch.uint8, device="cuda")[offset:]
-
-    data = torch.empty(G * k * P, dtype=torch.uint8, device="cuda")
-    parity = dev_buffer(G * r * P, args.parity_offset)
-    # this rank's slice of one global synthetic stream
-    ctx.fill_random_dev(data, data.numel(), SEED + 2, byte_offset=g0 * k * P, stream=sp)
-    dec_bytes = dec_read = 0
-    api = args.decode_api
-    if api == "auto":
-        # The slot rows: the choice that never lost by more than 4% on any box measured, both
-        # APIs interleaved on each (profiles/r03_final/ab_decode_api_box*.jsonl, and the
-        # driver's round-2 record): C3 slots ahead by 0.6% / 8% / 3.9% in step on three boxes;
-        # C5 packed ahead by 4% on one box, slots by 8% on another.  The HBM bytes are the same
-        # either way (PMC per API, DESIGN §5), so the difference is the box, not the traffic.
-        api = "recover"
-    recover = cfg["decode"] and api in ("recover", "packed")
-    rebuilt = dev_buffer(G * r * P, args.rebuilt_offset) if recover else None
-    row_start = torch.empty(G, dtype=torch.int32, device="cuda") if cfg["decode"] and api == "packed" else None
-
-    def decode_call(api: str, status=None):
-        if api == "packed":
-            ctx.recover_packed_dev(data, parity, masks, G, k, r, P, rebuilt, row_start, None, status, stream=sp)
-        elif api == "recover":
-            ctx.recover_dev(data, parity, masks, G, k, r, P, rebuilt, status, stream=sp)
-        else:
-            ctx.decode_dev(data, parity, masks, G, k, r, P, status, stream=sp)
-
-    if cfg["decode"]:
-        masks_h = make_masks(cfg, G, SEED + 3 + rank)
-        dec_bytes = decode_algorithmic_bytes(masks_h, k, r, P)
-        dec_read = decode_algorithmic_bytes(masks_h, k, r, P, reads_only=True)
-        masks = torch.from_numpy(masks_h.view(np.int64)).to("cuda")
-        ctx.decode_prepare(k, r)
-        if cfg.get("loss"):
-            # the receiver knows its loss profile: share of groups that lose a data shard
-            ctx.decode_loss_hint(1.0 - (1.0 - cfg["loss"]) ** k)
-    torch.cuda.synchronize()
-
-    verified = None
-    if not args.no_verify:
-        # correctness of this exact configuration before timing: encode, poison the erased
-        # data shards, rebuild, compare with the untouched copy; sampled groups vs oracle
-        # parity are covered by tests/test_gpu_parity.py.
-        orig = data.clone()
-        ctx.encode_dev(data, G, k, r, P, parity, stream=sp)
-        if cfg["decode"]:
-            bits = torch.arange(k, device="cuda", dtype=torch.int64)
-            lost = ((masks.view(G, 1) >> bits.view(1, k)) & 1).bool()
-            data.view(G, k, P)[lost] = 0xEE
-            st = torch.zeros(G, dtype=torch.uint8, device="cuda")
-            decode_call(api, st)
-            torch.cuda.synchronize()
-            bad_exp = unrecoverable_count(masks_h, k, r)
-            n_bad = int(st.sum().item())
-            ok_rows = st == 0
-            if api == "packed":
-                # rows back to back in (g, j ascending) order: boolean indexing's order
-                want = orig.view(G, k, P)[lost & ok_rows.view(G, 1)]
-                got = rebuilt.view(-1, P)[:want.shape[0]]
-                verified = bool(torch.equal(got, want)) and n_bad == bad_exp
-                data.copy_(orig)
-            elif recover:
-                # slot m of group g = its m-th lost data shard: the same (g, j ascending) order
-                # as boolean indexing of the lost shards
-                e_g = lost.sum(dim=1, keepdim=True)
-                slots = torch.arange(r, device="cuda").view(1, r) < e_g
-                got = rebuilt.view(G, r, P)[slots & ok_rows.view(G, 1)]
-                want = orig.view(G, k, P)[lost & ok_rows.view(G, 1)]
-                verified = bool(torch.equal(got, want)) and n_bad == bad_exp
-                data.copy_(orig)
-            elif n_bad == 0:
-                verified = bool(torch.equal(data, orig)) and bad_exp == 0
-            else:
-                verified = bool(torch.equal(data.view(G, -1)[ok_rows], orig.view(G, -1)[ok_rows])) and n_bad == bad_exp
-        else:
-            # encode-only config: the library's decoder (separate kernels, table arithmetic)
-            # rebuilds r erased shards of every group, data and parity mixed, from the parity
-            # just written -- a size-independent round trip of every parity row (the encode
-            # against the oracle on sampled groups is in tests/)
-            vm_h = erasure_masks(G, k + r, r, SEED + 7 + rank)
-            vm = torch.from_numpy(vm_h.view(np.int64)).to("cuda")
-            ctx.decode_prepare(k, r)
-            bits = torch.arange(k, device="cuda", dtype=torch.int64)
-            lost = ((vm.view(G, 1) >> bits.view(1, k)) & 1).bool()
-            data.view(G, k, P)[lost] = 0xEE
-            st = torch.zeros(G, dtype=torch.uint8, device="cuda")
-            rb = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
-            ctx.recover_dev(data, parity, vm, G, k, r, P, rb, st, stream=sp)
-            torch.cuda.synchronize()
-            e_g = lost.sum(dim=1, keepdim=True)
-            slots = torch.arange(r, device="cuda").view(1, r) < e_g
-            verified = bool(torch.equal(rb.view(G, r, P)[slots], orig.view(G, k, P)[lost])) and int(st.sum().item()) == 0
-            data.copy_(orig)
-            del rb, vm, lost, slots, st
-        del orig
-        torch.cuda.empty_cache()
-
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        ctx.encode_dev(data, G, k, r, P, parity, stream=sp)
-        if ev is not None:
-            ev[1].record(stream)
-        if cfg["decode"]:
-            decode_call(api)
-            if ev is not None:
-                ev[2].record(stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(events[i])
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
-    dec_ms = (sum(e[1].elapsed_time(e[2]) for e in events) / args.steps) if cfg["decode"] else 0.0
-
-    elapsed_max = reduce_max(elapsed)
-    if verified is not None:  # every rank must have rebuilt its shard exactly
-        verified = reduce_max(0.0 if verified else 1.0) == 0.0
-    total_groups = reduce_sum(float(G))
-    payload = total_groups * k * P * args.steps
-    value = payload / elapsed_max / 2**30
-    ms_per_step = elapsed_max / args.steps * 1e3
-
-    enc_bytes = (k + r) * P * G
-    enc_gbs = enc_bytes / (enc_ms * 1e-3) / 1e9
-    kernels = {"encode": {"ms": round(enc_ms, 4), "algorithmic_bytes": enc_bytes,
-                          "achieved_GBps": round(enc_gbs, 1),
-                          "payload_GiBps": round(k * P * G / (enc_ms * 1e-3) / 2**30, 2)}}
-    if cfg["decode"]:
-        dec_gbs = dec_bytes / (dec_ms * 1e-3) / 1e9
-        kernels["decode"] = {"ms": round(dec_ms, 4), "algorithmic_bytes": dec_bytes,
-                             "achieved_GBps": round(dec_gbs, 1),
-                             "payload_GiBps": round(k * P * G / (dec_ms * 1e-3) / 2**30, 2)}
-    # Each kernel alone, back to back (decode is idempotent on rebuilt data): its own time,
-    # without the write-back of the other kernel's output still draining from the caches
-    # when it starts (which the in-step times above include).
-    reps = max(5, args.steps // 4)
-
-    def isolated(fn, nbytes):
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
-        evs[0].record(stream)
-        for i in range(reps):
-            fn()
-            evs[i + 1].record(stream)
-        torch.cuda.synchronize()
-        ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(reps))[reps // 2]
-        return {"ms_median": round(ms, 4), "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1)}
-
-    kernels["encode"]["isolated"] = isolated(lambda: ctx.encode_dev(data, G, k, r, P, parity, stream=sp), enc_bytes)
-    if cfg["decode"]:
-        kernels["decode"]["api"] = api
-        kernels["decode"]["isolated"] = isolated(lambda: decode_call(api), dec_bytes)
-        # the other decode API on the same buffers, for comparison (not in `value`)
-        other = {"packed": "recover", "recover": "in-place"}.get(api, "recover")
-        if other == "recover" and rebuilt is None:
-            rebuilt = dev_buffer(G * r * P, args.rebuilt_offset)
-        if not args.no_other_api:
-            kernels["decode"]["other_api"] = {"api": other, **isolated(lambda: decode_call(other), dec_bytes)}
-    # The box's own HBM copy rate (fec_copy_dev: the encode's 16-B-per-lane pattern, no
-    # arithmetic), measured the same way: box-to-box spread is a few percent, so the kernels
-    # are also quoted against it.
-    half = (data.numel() // 2) // 16 * 16
-    scratch = torch.empty(half, dtype=torch.uint8, device="cuda")
-    copy = isolated(lambda: ctx.copy_dev(data, scratch, half, stream=sp), 2 * half)
-    del scratch
-    torch.cuda.empty_cache()
-    dom = max(kernels, key=lambda n: kernels[n]["ms"])
-    dom_read = k * P * G if dom == "encode" else dec_read
-    pmc, pmc_note = load_pmc_traffic(args.config)
-    pmc = pmc or {}
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["achieved_GBps"],
-                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(kernels[dom]["achieved_GBps"] / HBM_PEAK_GBS, 4),
-                # PMC entries are keyed per decode API (recover_packed / recover_slots / decode)
-                "traffic": pmc.get(pmc_key(dom, api) if cfg["decode"] else dom, {}).get("hbm_bytes_per_launch"),
-                "algorithmic_bytes_per_launch": kernels[dom]["algorithmic_bytes"],
-                "traffic_source": pmc_note,
-                "read_frac": round(dom_read / (kernels[dom]["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "read_frac_of_box_copy": round(dom_read / (kernels[dom]["ms"] * 1e-3) / 1e9 / copy["achieved_GBps"], 4),
-                # north_star's "70% of the HBM-read roofline": reads at 0.70 x 8 TB/s while this
-                # kernel also writes its bytes needs this much total traffic -- above the box's
-                # copy ceiling (box_copy_GBps), so that literal target is out of reach (DESIGN §5)
-                "read_target_total_GBps": round(0.70 * HBM_PEAK_GBS * kernels[dom]["algorithmic_bytes"] / dom_read, 1),
-                "box_copy_GBps": copy["achieved_GBps"],
-                "frac_of_box_copy": round(kernels[dom]["achieved_GBps"] / copy["achieved_GBps"], 4),
-                "timing": ("torch.cuda.Event on torch's default stream, kernels on the context's stream"
-                           if args.null_stream else
-                           "torch.cuda.Event on the launch stream (one torch stream for launches, ops and "
-                           "events), averaged over the timed steps")}
-
-    e2e = None
-    if args.e2e:
-        e2e = e2e_pinned(ctx, data, parity, masks if cfg["decode"] else None, G, cfg)
+    legs = None
+    if legs_enabled(args, world):
+        def measure_leg(config: str, e2e: bool) -> dict:
+            lc = dict(CONFIGS[config])
+            lg = args.leg_groups or lc["groups"]
+            if args.leg_groups:
+                lc["workload"] += f" (groups override: {lg}/GPU)"
+            return bench.measure(config, lc, lg, min(args.steps, 20), min(args.warmup, 2), "auto",
+                                 not args.no_verify, False, e2e)
+        legs = run_legs(measure_leg)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)
 
     if rank == 0:
+        k, r, P = cfg["k"], cfg["r"], cfg["P"]
         out = {
             "metric": "FEC encode+decode GiB/s (device-resident), k=10 r=3 1200B pkts, 1/2/4/8 GPU",
-            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "value": head["value"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (counter-based splitmix64 bytes generated in HBM; seeded erasure masks)",
             "config": {"workload": cfg["workload"], "k": k, "r": r, "packet_bytes": P,
                        "groups_per_gpu": G, "erasures_per_group": cfg["erasures"] or None,
                        "iid_loss": cfg.get("loss"),
-                       "decode_api": ({"packed": "fec_recover_batch_rs_dev_packed (rebuilt packets of all groups back "
-                                                 "to back with per-group row starts, decoder.go Recovered list)",
-                                       "recover": "fec_recover_batch_rs_dev (rebuilt packets at (g*r + m)*P slots)",
-                                       "in-place": "fec_decode_batch_rs_dev (in place)"}[api]
-                                      if cfg["decode"] else None),
+                       "decode_api": DECODE_API_TEXT[head["decode_api"]] if cfg["decode"] else None,
                        "parallelism": f"group-sharded x{world} (no collective)"},
-            "verified": verified,
-            "kernels": kernels,
-            "roofline": roofline,
+            "verified": head["verified"],
+            "kernels": head["kernels"],
+            "roofline": head["roofline"],
             "cpu_baseline": cpu,
         }
-        if e2e is not None:
-            out["e2e_pinned"] = e2e
-        if os.environ.get("QUICFEC_BENCH_ADDRS") == "1":  # placement diagnostics (A/B runs)
-            out["buffers"] = {n: hex(t.data_ptr()) for n, t in (("data", data), ("parity", parity), ("rebuilt", rebuilt))
-                              if t is not None}
+        if "e2e_pinned" in head:
+            out["e2e_pinned"] = head["e2e_pinned"]
+        if "buffers" in head:
+            out["buffers"] = head["buffers"]
+        if legs:
+            out.update(legs)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    ctx.close()
+    bench.ctx.close()
     return 0
 
 

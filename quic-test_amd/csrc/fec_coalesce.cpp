@@ -72,6 +72,7 @@ constexpr uint32_t kPackets = 10;  // packets per group of the legacy call (fec_
 constexpr uint32_t kMaxBatchGroups = 1024;
 constexpr uint64_t kStageBudget = 16ull << 20;  // page-locked staging bytes per batch
 constexpr size_t kMaxCoalescers = 16;           // (device, packet size) pairs
+constexpr uint32_t kCoalesceMaxP = 16u << 10;   // larger packets: no shared launches (staging bound)
 
 long env_long(const char* name, long def) {
   const char* v = std::getenv(name);
@@ -427,10 +428,15 @@ class Resident {
     const uint64_t per_us = static_cast<uint64_t>(khz) / 1000u;
     r->idle_ticks = per_us * static_cast<uint64_t>(std::max(10L, env_long("QUICFEC_RESIDENT_IDLE_US", 2000)));
     r->life_ticks = per_us * static_cast<uint64_t>(std::max(100L, env_long("QUICFEC_RESIDENT_LIFE_US", 50000)));
+    // The per-slot staging of pageable repair buffers (16 MB) comes with the first call that
+    // needs it (ensure_outs): the first context of every process sets a Resident up
+    // (coalesce_prepare), most never make such a call.
     if (!alloc_coherent(r->ring, sizeof(ServerSlot) * kServerSlots) ||
-        !alloc_coherent(r->done, sizeof(uint64_t) * kServerSlots) || !alloc_coherent(r->ctl, sizeof(ServerControl)) ||
-        !alloc_coherent(r->outs, size_t(kResidentOutBytes) * kServerSlots))
+        !alloc_coherent(r->done, sizeof(uint64_t) * kServerSlots) || !alloc_coherent(r->ctl, sizeof(ServerControl)))
       return nullptr;
+    r->deadline = std::chrono::milliseconds(std::max(1L, env_long("QUICFEC_RESIDENT_DEADLINE_MS", 10000)));
+    // tests: an instance that never serves (relaunch records a launch without launching)
+    r->no_launch = env_long("QUICFEC_RESIDENT_TEST_NOLAUNCH", 0) != 0;
     if (env_long("QUICFEC_RESIDENT_STAMPS", 0) != 0 && !alloc_coherent(r->stamps, 256 * 8 * sizeof(uint64_t))) return nullptr;
     r->tick_khz = static_cast<uint64_t>(khz);
     // no word of a slot that was never written may carry lap 0's tag
@@ -447,21 +453,42 @@ class Resident {
            (repair_pinned || uint64_t(G) * P <= kResidentOutBytes);
   }
 
+  // False once a call timed out or a relaunch failed (poison): later legacy calls take the
+  // coalescer / per-context paths, and no instance is launched again.
+  bool usable() const { return !broken.load(std::memory_order_acquire); }
+
+  // The call's result, or kNotTaken when the Resident is (or just became) unusable before the
+  // call published its slot: nothing of the caller's was handed to the device, and the caller
+  // runs the call on another path.
+  static constexpr int kNotTaken = 1;
+
   int encode(const uint8_t* slab_dev, const uint32_t* offsets, uint32_t G, uint32_t P, uint8_t* repair_out,
              uint8_t* repair_dev, uint64_t t_enter) {
     uint8_t* out_dev = nullptr;
+    if (!repair_dev && !ensure_outs()) return kNotTaken;
     const uint64_t base = reinterpret_cast<uint64_t>(slab_dev);
     const uint64_t seq = next_seq.fetch_add(1, std::memory_order_relaxed);
     const uint32_t si = static_cast<uint32_t>(seq % kServerSlots);
     const uint64_t tag = ((seq / kServerSlots) & 0xFFu) << kServerTagShift;
-    // the slot's previous occupant (seq - kServerSlots) has been served and collected
+    // the slot's previous occupant (seq - kServerSlots) has been served and collected; if that
+    // does not happen within the deadline, or no instance can be launched to serve it, the
+    // Resident is poisoned and this call is not taken (its slot stays untouched: overwriting it
+    // would change the lap tag of a call the device has not served yet)
     const uint64_t* dw = reinterpret_cast<const uint64_t*>(done.host) + si;
+    const auto t_reuse = std::chrono::steady_clock::now() + deadline;
     for (uint32_t spins = 0; seq >= kServerSlots && (collected[si].load(std::memory_order_acquire) != seq - kServerSlots + 1 ||
                                                      __atomic_load_n(dw, __ATOMIC_ACQUIRE) != seq - kServerSlots + 1);
          ++spins) {
-      if ((spins & 1023u) == 1023u && !instance_alive() && relaunch() != FEC_OK) break;
+      if (!usable()) return kNotTaken;
+      if ((spins & 1023u) == 1023u) {
+        if ((!instance_alive() && relaunch() != FEC_OK) || std::chrono::steady_clock::now() > t_reuse) {
+          poison();
+          return kNotTaken;
+        }
+      }
       backoff(spins);
     }
+    if (!usable()) return kNotTaken;
     ServerSlot* sl = reinterpret_cast<ServerSlot*>(ring.host) + si;
     out_dev = repair_dev ? repair_dev : outs.dev + size_t(si) * kResidentOutBytes;
     // groups after the first, then the first group and the header: the device reads the former
@@ -474,7 +501,7 @@ class Resident {
     g_res_calls.fetch_add(1, std::memory_order_relaxed);
     const uint64_t t_pub = now_ns();
     int rc = FEC_OK;
-    const auto t_fail = std::chrono::steady_clock::now() + std::chrono::seconds(10);
+    const auto t_fail = std::chrono::steady_clock::now() + deadline;
     for (uint32_t spins = 0;; ++spins) {
       if (__atomic_load_n(dw, __ATOMIC_ACQUIRE) == seq + 1) break;
       // no instance serving (never launched, or it left): launch one from its progress mark
@@ -483,7 +510,8 @@ class Resident {
         if (rc != FEC_OK) break;
       }
       if ((spins & 1023u) == 1023u && std::chrono::steady_clock::now() > t_fail) {
-        set_last_error("fec_encode_batch: the resident encoder did not serve the call within 10 s");
+        set_last_error("fec_encode_batch: the resident encoder did not serve the call within the deadline "
+                       "(QUICFEC_RESIDENT_DEADLINE_MS); legacy calls now take the coalescer path");
         rc = FEC_ERR_HIP;
         break;
       }
@@ -491,10 +519,20 @@ class Resident {
     }
     const uint64_t t_done = now_ns();
     if (rc != FEC_OK) {
-      // Not served: turn the slot into one with nothing to do (the slots after it are served in
-      // order, so it must still be served), so a later instance does not touch the caller's
-      // buffers.  Only a hung device can have read it already.
+      // Not served.  Turn the slot into one with nothing to do (the slots after it are served in
+      // order), poison the Resident (never relaunched), and ask a running instance to leave.  An
+      // instance that read the slot before the rewrite may still write the caller's repair rows
+      // and read its slab: wait, bounded, until it has served this seq or left.  Past that bound
+      // the device is hung, and the caller's buffers handed to this call must not be reused
+      // (include/fec_xor_simd.h, fec_encode_batch).
       __atomic_store_n(&sl->shape, uint64_t(P) | tag, __ATOMIC_RELEASE);
+      poison();
+      const auto t_drain = std::chrono::steady_clock::now() + deadline;
+      const ServerControl* c = reinterpret_cast<const ServerControl*>(ctl.host);
+      for (uint32_t spins = 0; instance_alive() && __atomic_load_n(&c->progress, __ATOMIC_ACQUIRE) <= seq &&
+                               __atomic_load_n(dw, __ATOMIC_ACQUIRE) != seq + 1 && std::chrono::steady_clock::now() < t_drain;
+           ++spins)
+        backoff(spins);
     } else if (!repair_dev) {
       std::memcpy(repair_out, outs.host + size_t(si) * kResidentOutBytes, size_t(G) * P);
     }
@@ -505,23 +543,19 @@ class Resident {
     return rc;
   }
 
-  // Process exit: ask the running instance to leave and give it a moment (no HIP calls).
-  // Returns whether no instance runs any more (then the memory may be freed).
-  bool shutdown() {
+  // Process exit: ask the running instance to leave and wait, bounded, until its host-visible
+  // `exited` word says it has.  No HIP call: under rocprofv3 the tool has finalised by the time
+  // atexit handlers run, and a runtime call there aborted the process (f13ed47); the stream,
+  // the page-locked ring and the device memory go with the process.  Never deleted.
+  void shutdown() {
     __atomic_store_n(&reinterpret_cast<ServerControl*>(ctl.host)->stop, 1, __ATOMIC_RELEASE);
-    // Never launched (set up ahead of a first call that did not come, coalesce_prepare): no HIP
-    // call at exit -- under rocprofv3 the tool has finalised by now and a runtime call there
-    // aborted the process; the memory goes with the process.
-    if (gen.load(std::memory_order_acquire) == 0) return false;
+    if (gen.load(std::memory_order_acquire) == 0) return;
     const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
     while (instance_alive() && std::chrono::steady_clock::now() < until) std::this_thread::yield();
     if (stamps.host) print_stamps();
-    if (instance_alive()) return false;
-    BindDevice bd(device);
-    return bd.ok && hipStreamSynchronize(stream) == hipSuccess;  // the last instance has retired
   }
 
-  ~Resident() {
+  ~Resident() {  // only a Resident whose create() failed; never at exit (shutdown)
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -554,6 +588,23 @@ class Resident {
   std::atomic<uint64_t> next_seq{0};
   std::mutex mu;
   std::atomic<uint64_t> gen{0};  // generation of the last launched instance (0 = none yet)
+  std::atomic<bool> broken{false};
+  std::chrono::milliseconds deadline{10000};  // QUICFEC_RESIDENT_DEADLINE_MS
+  bool no_launch = false;                     // QUICFEC_RESIDENT_TEST_NOLAUNCH
+  std::atomic<bool> outs_ready{false};
+
+  void poison() {
+    broken.store(true, std::memory_order_release);
+    __atomic_store_n(&reinterpret_cast<ServerControl*>(ctl.host)->stop, 1, __ATOMIC_RELEASE);
+  }
+
+  bool ensure_outs() {
+    if (outs_ready.load(std::memory_order_acquire)) return true;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!outs.host && !alloc_coherent(outs, size_t(kResidentOutBytes) * kServerSlots)) return false;
+    outs_ready.store(true, std::memory_order_release);
+    return true;
+  }
 
   static void backoff(uint32_t spins) {
     if (spins < 2048) {
@@ -575,12 +626,16 @@ class Resident {
     std::lock_guard<std::mutex> lk(mu);
     if (instance_alive()) return FEC_OK;
     const ServerControl* c = reinterpret_cast<const ServerControl*>(ctl.host);
-    if (__atomic_load_n(&c->stop, __ATOMIC_ACQUIRE)) {
-      set_last_error("fec_encode_batch: the resident encoder is shutting down");
+    if (__atomic_load_n(&c->stop, __ATOMIC_ACQUIRE) || !usable()) {
+      set_last_error("fec_encode_batch: the resident encoder is shutting down or out of service");
       return FEC_ERR_HIP;
     }
     const uint64_t start = __atomic_load_n(&c->progress, __ATOMIC_ACQUIRE);
     const uint64_t g = gen.load(std::memory_order_relaxed) + 1;
+    if (no_launch) {  // tests: an instance that is "alive" and never serves
+      gen.store(g, std::memory_order_release);
+      return FEC_OK;
+    }
     BindDevice bd(device);
     const hipError_t e = bd.ok ? launch_legacy_server(reinterpret_cast<const ServerSlot*>(ring.dev),
                                                       reinterpret_cast<uint64_t*>(done.dev),
@@ -608,18 +663,17 @@ std::map<int, Resident*> g_resident;                   // per device; NULL when 
 std::atomic<bool> g_shut{false};  // process exit: legacy calls run alone from here on
 std::once_flag g_atexit_once;
 
-// Process exit (std::atexit, registered after the HIP runtime is up, so it runs before the
-// runtime's own teardown): stop every resident instance and free what the coalescers hold.
-// A resident instance that does not leave in time keeps its memory (it may still read it).
+// Process exit (std::atexit): stop every resident instance (a store to host memory and a
+// bounded wait on its host-visible `exited` word).  No HIP call from here on: under a tool that
+// tears the runtime down before atexit handlers run (rocprofv3), one aborted the process
+// (f13ed47).  Residents, coalescers, their streams, events and page-locked buffers are left to
+// process teardown (tests/csrc/exit_path_test.cpp counts the HIP calls made after exit begins).
 void shutdown_all() {
   g_shut.store(true, std::memory_order_release);
   std::lock_guard<std::mutex> lk(g_reg_mu);
   for (int d = 0; d < kResidentDevices; ++d) g_resident_fast[d].store(nullptr, std::memory_order_release);
   for (auto& kv : g_resident)
-    if (kv.second && kv.second->shutdown()) delete kv.second;
-  g_resident.clear();
-  for (auto& kv : g_reg) delete kv.second;
-  g_reg.clear();
+    if (kv.second) kv.second->shutdown();
 }
 
 Resident* resident_for(int device) {
@@ -679,12 +733,19 @@ bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* off
   if (sm == HostMem::kPinned && env_long("QUICFEC_RESIDENT", 1) != 0 && Resident::fits(num_groups, packet_size, repair_pinned) &&
       reinterpret_cast<uint64_t>(sdev) + 0xFFFFFFFFull + packet_size <= kServerAddrMask &&
       reinterpret_cast<uint64_t>(rdev) <= kServerAddrMask) {
-    if (Resident* r = resident_for(device)) {
-      *rc = r->encode(static_cast<const uint8_t*>(sdev), offsets, num_groups, packet_size, repair_out,
-                      repair_pinned ? static_cast<uint8_t*>(rdev) : nullptr, t_enter);
-      return true;
+    Resident* r = resident_for(device);
+    if (r && r->usable()) {
+      const int res = r->encode(static_cast<const uint8_t*>(sdev), offsets, num_groups, packet_size, repair_out,
+                                repair_pinned ? static_cast<uint8_t*>(rdev) : nullptr, t_enter);
+      if (res != Resident::kNotTaken) {
+        *rc = res;
+        return true;
+      }
     }
   }
+  // Pageable packets are staged per batch at cap * 10 * P bytes (cap >= 8): past this size the
+  // legacy call runs alone on its context (QUIC datagrams are <= 1500 B).
+  if (packet_size > kCoalesceMaxP) return false;
   Coalescer* c = coalescer_for(device, packet_size);
   if (!c || num_groups > c->capacity() / 2) return false;
   *rc = c->encode(slab, sm == HostMem::kPinned ? static_cast<const uint8_t*>(sdev) : nullptr, offsets, num_groups,

@@ -986,6 +986,304 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
 
 }
 
+// ---------------------------------------------------------------------------------
+// Packed recover in one launch: recover_runs (fec_recover_batch_rs_dev_packed; DESIGN.md §5,
+// round 4).  The reference decoder hands rebuilt packets back as separate buffers
+// (decoder.go:29-34 `Recovered`); the packed list puts all of a batch's rebuilt packets back
+// to back, group g's from row row_start[g] (exclusive prefix sum of the rows every group
+// rebuilds: its lost data shards when recoverable, else 0).
+//
+// A workgroup owns kRunGroups consecutive groups (one erasure mask per thread), so all of
+// their rebuilt rows form ONE contiguous run of the packed list:
+//  1. every thread classifies its group (status byte; rows), the block scans the rows and
+//     lists the groups to rebuild in LDS, in group order;
+//  2. wave 0 finds the run's first row by decoupled look-back over the blocks before it
+//     (blocks take their tile from an atomic ticket, so every block one waits on has
+//     started and publishes its own row count before it waits on anything) and publishes
+//     its inclusive prefix; row_start[g] is written for every group.  No prefix launches;
+//  3. the 4 waves rebuild the listed groups (mask-addressed, exactly decode_fused's INLINE
+//     arithmetic) into an LDS image of the run; rows past the image's capacity (dense loss)
+//     are stored straight to HBM;
+//  4. the block copies the image out with 16-B stores by consecutive threads, so the run
+//     leaves as whole 128-B lines except at its two ends -- instead of every 1.2-KB row being
+//     stored by its own wave with partial lines at both ends.
+// Look-back words: epoch (bits 34..63) | flag (bits 32..33: kRunAgg, kRunIncl) | rows.  The
+// epoch is the launch's, so words left by earlier launches never match (no reset launch).
+// ---------------------------------------------------------------------------------
+constexpr uint32_t kRunGroups = 256;
+constexpr uint64_t kRunAgg = 1ull << 32;
+constexpr uint64_t kRunIncl = 2ull << 32;
+constexpr uint32_t kRunEpochShift = 34;
+
+// One group's rebuilt rows into acc (rows 0..e-1), returns e.  Same survivor choice, record
+// and arithmetic as fused_group's DIRECT + INLINE path (survivors: the surviving data shards
+// ascending, then the e lowest surviving parity rows; record from the colex ranks).
+template <int K, int R, int NM, int NT, int POL>
+__device__ __forceinline__ uint32_t runs_rebuild(uint64_t g, uint64_t m, uint32_t lane,
+                                                 const uint8_t* __restrict__ data,
+                                                 const uint8_t* __restrict__ parity,
+                                                 const uint8_t* __restrict__ codebook, const RankMeta& rm,
+                                                 uint32_t P, const uint32_t (&toff)[NT > 0 ? NT : 1],
+                                                 uint32_t (&acc)[R][4 * NM + NT]) {
+  constexpr int NW = 4 * NM + NT;
+  constexpr uint64_t kmask = (1ull << K) - 1;
+  constexpr uint64_t rmask = (1ull << R) - 1;
+  const uint64_t lost = m & kmask;
+  const uint32_t e = static_cast<uint32_t>(__popcll(lost));
+  const uint64_t pm = (m >> K) & rmask;
+  uint64_t rank_e = 0, rank_r = 0, rsel = 0;
+  {
+    uint64_t dm = lost;
+    for (uint32_t t = 0; dm; ++t) {
+      rank_e += choose_small(static_cast<uint32_t>(__builtin_ctzll(dm)), t + 1u);
+      dm &= dm - 1;
+    }
+    uint64_t sp = ~pm & rmask;
+    for (uint32_t t = 0; t < e; ++t) {
+      const uint32_t bit = static_cast<uint32_t>(__builtin_ctzll(sp));
+      rank_r += choose_small(bit, t + 1u);
+      rsel |= 1ull << bit;
+      sp &= sp - 1;
+    }
+  }
+  const bool xor_only = e == 1 && (pm & 1u) == 0;
+  const Tab* tabs = reinterpret_cast<const Tab*>(codebook + rm.base[e] + (rank_e * rm.count_r[e] + rank_r) * rm.stride[e] + 128);
+  uint64_t surv = (~lost & kmask) | (rsel << K);
+  const uint8_t* dg = data + g * K * static_cast<uint64_t>(P);
+  const uint8_t* pg = parity + g * R * static_cast<uint64_t>(P);
+  uint32_t x[K][NW];
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    const uint32_t sid = static_cast<uint32_t>(__builtin_ctzll(surv));
+    surv &= surv - 1;
+    const uint8_t* src = sid < K ? dg + sid * static_cast<uint64_t>(P) : pg + (sid - K) * static_cast<uint64_t>(P);
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      const u32x4 t = ld16<POL>(src + i * 1024u + lane * 16u);
+      x[s][4 * i] = t.x;
+      x[s][4 * i + 1] = t.y;
+      x[s][4 * i + 2] = t.z;
+      x[s][4 * i + 3] = t.w;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if constexpr ((POL & kNtLoad) != 0) x[s][4 * NM + t] = __builtin_nontemporal_load(reinterpret_cast<const u32u*>(src + toff[t]));
+      else x[s][4 * NM + t] = *reinterpret_cast<const u32u*>(src + toff[t]);
+    }
+  }
+#pragma unroll
+  for (int mm = 0; mm < R; ++mm)
+#pragma unroll
+    for (int q = 0; q < NW; ++q) acc[mm][q] = 0;
+  if (xor_only) {  // single data loss rebuilt from parity row 0: the reference XOR
+#pragma unroll
+    for (int s = 0; s < K; ++s)
+#pragma unroll
+      for (int q = 0; q < NW; ++q) acc[0][q] ^= x[s][q];
+    return 1;
+  }
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    uint32_t s0[NW], s1[NW], s2[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      s0[q] = x[s][q] & 0x07070707u;
+      s1[q] = (x[s][q] >> 3) & 0x07070707u;
+      s2[q] = (x[s][q] >> 6) & 0x03030303u;
+    }
+#pragma unroll
+    for (int mm = 0; mm < R; ++mm) {
+      if (static_cast<uint32_t>(mm) < e) {
+        const Tab& t = tabs[mm * K + s];
+        if (t.coef == 1u) {
+#pragma unroll
+          for (int q = 0; q < NW; ++q) acc[mm][q] ^= x[s][q];
+        } else if (t.coef != 0u) {
+#pragma unroll
+          for (int q = 0; q < NW; ++q) acc[mm][q] ^= gmul(s0[q], s1[q], s2[q], t);
+        }
+      }
+    }
+  }
+  return e;
+}
+
+// stage_bytes: dynamic LDS of the run image (0: every row straight to HBM).  The image is used
+// only when P % 16 == 0 and `out` is 16-B aligned (the launcher passes 0 otherwise), so row
+// starts in the image and in HBM are 16-B aligned alike.
+// base_in (nullable): rows before this launch (chunked launches: the previous chunk's total).
+// POL: kNtLoad for the survivor loads, kNtStore for the row stores.  WAVES: waves per workgroup;
+// TG: groups per workgroup (<= 64 * WAVES: the first TG threads classify one group each).
+// flags bit 0 (probes only): no row stores at all.
+template <int K, int R, int NM, int NT, int POL, int WAVES, int TG = 64 * WAVES>
+__global__ __launch_bounds__(64 * WAVES) void recover_runs(const uint8_t* __restrict__ data,
+                                                    const uint8_t* __restrict__ parity,
+                                                    const uint64_t* __restrict__ masks, uint64_t groups,
+                                                    uint32_t P, const uint8_t* __restrict__ codebook, RankMeta rm,
+                                                    uint8_t* __restrict__ out, uint32_t* __restrict__ row_start,
+                                                    uint8_t* __restrict__ status, uint64_t* __restrict__ lb,
+                                                    uint32_t* __restrict__ ticket, uint32_t epoch,
+                                                    uint32_t stage_bytes, const uint64_t* __restrict__ base_in,
+                                                    uint64_t* __restrict__ total_out, uint64_t* __restrict__ total_user,
+                                                    uint32_t flags) {
+  static_assert(R <= 3, "mask-addressed shapes: r <= 3");
+  static_assert(TG <= 64 * WAVES && TG % 64 == 0, "one classifying thread per group, whole waves");
+  constexpr uint32_t kTile = TG;
+  constexpr uint32_t kScanWaves = TG / 64;
+  constexpr int NW = 4 * NM + NT;
+  constexpr uint64_t kmask = (1ull << K) - 1;
+  constexpr uint64_t rmask = (1ull << R) - 1;
+  extern __shared__ __attribute__((aligned(16))) uint8_t run_image[];
+  __shared__ uint64_t s_mask[kTile];
+  __shared__ uint32_t s_item[kTile];  // (local group << 16) | first row in the run
+  __shared__ uint32_t s_wrows[kScanWaves], s_wwork[kScanWaves];
+  __shared__ uint32_t s_tile, s_first;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(tid >> 6));
+  if (tid == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every ticket of this launch is taken: the counter starts from 0 for the next launch
+    // (which the stream orders after this one)
+    if (t == gridDim.x - 1u) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tile = t;
+  }
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint64_t g = static_cast<uint64_t>(tile) * kTile + tid;
+  uint64_t m = 0;
+  uint32_t rows = 0;
+  if (tid < kTile && g < groups) {
+    m = masks[g];
+    const uint32_t ne = static_cast<uint32_t>(__popcll(m & kmask));
+    const bool bad = ne > R - static_cast<uint32_t>(__popcll((m >> K) & rmask));
+    if (status != nullptr) status[g] = bad ? 1 : 0;
+    rows = ne > 0 && !bad ? ne : 0u;
+  }
+  uint32_t incl = rows;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+  const uint64_t need = __ballot(rows != 0u);
+  if (wave < kScanWaves) {
+    if (lane == 63u) s_wrows[wave] = incl;
+    if (lane == 0u) s_wwork[wave] = static_cast<uint32_t>(__popcll(need));
+  }
+  __syncthreads();
+  uint32_t wrow = 0, witem = 0, A = 0, nwork = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kScanWaves; ++w) {
+    if (w < wave) {
+      wrow += s_wrows[w];
+      witem += s_wwork[w];
+    }
+    A += s_wrows[w];
+    nwork += s_wwork[w];
+  }
+  const uint32_t lrow = wrow + incl - rows;  // the group's first row inside the run
+  if (rows != 0u) {
+    const uint32_t i = witem + static_cast<uint32_t>(__popcll(need & ((1ull << lane) - 1)));
+    s_mask[i] = m;
+    s_item[i] = (tid << 16) | lrow;
+  }
+  if (wave == 0) {
+    // decoupled look-back
+    const uint64_t tag = static_cast<uint64_t>(epoch) << kRunEpochShift;
+    const uint32_t base = base_in != nullptr ? static_cast<uint32_t>(*base_in) : 0u;
+    uint32_t excl = 0;
+    if (tile == 0) {
+      excl = base;
+      if (lane == 0) __hip_atomic_store(&lb[0], tag | kRunIncl | (base + A), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(&lb[tile], tag | kRunAgg | A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t pos = static_cast<int64_t>(tile) - 1;
+      for (;;) {
+        const int64_t idx = pos - static_cast<int64_t>(lane);
+        uint64_t s = tag | kRunIncl | base;  // "before tile 0": the rows before this launch
+        if (idx >= 0) {
+          for (;;) {
+            s = __hip_atomic_load(&lb[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((s >> kRunEpochShift) == epoch && (s & (kRunAgg | kRunIncl)) != 0) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        const uint64_t inc = __ballot((s & kRunIncl) != 0);
+        const uint32_t stop = inc ? static_cast<uint32_t>(__builtin_ctzll(inc)) : 64u;
+        uint32_t v = lane <= stop ? static_cast<uint32_t>(s) : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        excl += v;
+        if (inc) break;
+        pos -= 64;
+      }
+      if (lane == 0) __hip_atomic_store(&lb[tile], tag | kRunIncl | (excl + A), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      s_first = excl;
+      if (tile == gridDim.x - 1u) {
+        if (total_out != nullptr) *total_out = static_cast<uint64_t>(excl) + A;
+        if (total_user != nullptr) *total_user = static_cast<uint64_t>(excl) + A;
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t first = s_first;
+  if (tid < kTile && g < groups) row_start[g] = first + lrow;
+  const uint32_t cap_rows = stage_bytes / P;
+  uint8_t* run = out + static_cast<uint64_t>(first) * P;
+  uint32_t toff[NT > 0 ? NT : 1];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    toff[t] = NM * 1024u + t * 256u + lane * 4u;
+    if (toff[t] + 4u > P) toff[t] = P - 4u;
+  }
+  for (uint32_t i = wave; i < nwork; i += WAVES) {
+    const uint64_t mi = s_mask[i];
+    const uint64_t mw = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(mi >> 32))) << 32) |
+                        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(mi));
+    const uint32_t item = __builtin_amdgcn_readfirstlane(s_item[i]);
+    const uint64_t gi = static_cast<uint64_t>(tile) * kTile + (item >> 16);
+    const uint32_t r0 = item & 0xFFFFu;
+    uint32_t acc[R][NW];
+    const uint32_t e = runs_rebuild<K, R, NM, NT, POL>(gi, mw, lane, data, parity, codebook, rm, P, toff, acc);
+    if (flags & 1u) continue;  // probe: reads and arithmetic only
+#pragma unroll
+    for (int mm = 0; mm < R; ++mm) {
+      if (static_cast<uint32_t>(mm) < e) {
+        const uint32_t row = r0 + mm;
+        if (row < cap_rows) {  // into the run image (16-B aligned rows: see stage_bytes)
+          uint8_t* dst = run_image + row * P;
+#pragma unroll
+          for (int q = 0; q < NM; ++q)
+            *reinterpret_cast<u32x4*>(dst + q * 1024u + lane * 16u) =
+                u32x4{acc[mm][4 * q], acc[mm][4 * q + 1], acc[mm][4 * q + 2], acc[mm][4 * q + 3]};
+#pragma unroll
+          for (int t = 0; t < NT; ++t) *reinterpret_cast<uint32_t*>(dst + toff[t]) = acc[mm][4 * NM + t];
+        } else {
+          uint8_t* dst = run + static_cast<uint64_t>(row) * P;
+#pragma unroll
+          for (int q = 0; q < NM; ++q)
+            st16<POL>(dst + q * 1024u + lane * 16u,
+                           u32x4{acc[mm][4 * q], acc[mm][4 * q + 1], acc[mm][4 * q + 2], acc[mm][4 * q + 3]});
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            if constexpr ((POL & kNtStore) != 0) __builtin_nontemporal_store(acc[mm][4 * NM + t], reinterpret_cast<u32u*>(dst + toff[t]));
+            else *reinterpret_cast<u32u*>(dst + toff[t]) = acc[mm][4 * NM + t];
+          }
+        }
+      }
+    }
+  }
+  const uint32_t staged = (flags & 1u) ? 0u : (A < cap_rows ? A : cap_rows);
+  if (staged == 0u) return;
+  __syncthreads();
+  // the image leaves in 16-B pieces by consecutive threads: whole lines but at the run's ends
+  const uint32_t n16 = staged * P / 16u;
+  for (uint32_t c = tid; c < n16; c += 64u * WAVES)
+    st16<POL>(run + c * 16u, *reinterpret_cast<const u32x4*>(run_image + c * 16u));
+}
+
 // Packed recover rows: row_start[g] = exclusive prefix sum over groups of the number of rows a
 // group rebuilds (its lost data shards when recoverable, else 0).  Block sums of kRowsPerBlock
 // groups first; then every block of rows_write adds up the sums of the blocks before it itself
@@ -1419,6 +1717,14 @@ __device__ __forceinline__ void sys_store_relaxed(uint64_t* p, uint64_t v) {
 }
 
 // 16 bytes to host memory at any address, written system-coherent (sc0 sc1: no cache keeps a copy).
+// ISA assumption, not the HIP memory model's guarantee: on gfx94x / gfx95x a volatile global
+// store is emitted with sc0 sc1 (write-through to memory), so legacy_server's vmcnt(0) after its
+// repair-row stores means the rows are in host memory before it stores the done words (no
+// release fence; profiles/r03_resident_store_ab.txt).  The library is built for gfx950 only
+// (Makefile ARCH); a build for another target stops here instead of silently relying on it.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "legacy_server assumes gfx94x/gfx95x volatile stores are sc0 sc1 write-through (sys_store_16b)"
+#endif
 __device__ __forceinline__ void sys_store_16b(uint8_t* p, u32x4 v) { *reinterpret_cast<volatile u32x4u*>(p) = v; }
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
@@ -2028,6 +2334,95 @@ hipError_t launch_rows_prefix(const uint64_t* masks, uint64_t groups, uint32_t k
                        nullptr);
   }
   return hipGetLastError();
+}
+
+namespace {
+
+uint64_t runs_blocks_per_launch(uint64_t groups) {
+  const uint64_t nb = (groups + kRunGroups - 1) / kRunGroups;
+  const uint64_t mb = max_wave_blocks();
+  return nb < mb ? nb : mb;
+}
+
+template <int K, int R, int NM, int NT>
+hipError_t run_recover_runs(const RunsLaunch& a, uint32_t stage, hipStream_t s) {
+  RankMeta rm{};
+  for (int e = 1; e <= 3; ++e) {
+    rm.base[e] = a.meta.base[e];
+    rm.stride[e] = a.meta.stride[e];
+    rm.count_r[e] = a.meta.count_r[e];
+  }
+  uint8_t* ws = static_cast<uint8_t*>(a.workspace);
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(ws);
+  const uint64_t per = runs_blocks_per_launch(a.groups) * kRunGroups;
+  const uint32_t launches = runs_launches(a.groups);
+  uint64_t* totals = reinterpret_cast<uint64_t*>(ws + 64);
+  uint64_t* lb = reinterpret_cast<uint64_t*>(ws + 64 + 8 * static_cast<uint64_t>(launches));
+  for (uint32_t c = 0; c < launches; ++c) {
+    const uint64_t g0 = c * per;
+    const uint64_t gn = a.groups - g0 < per ? a.groups - g0 : per;
+    const uint32_t nb = static_cast<uint32_t>((gn + kRunGroups - 1) / kRunGroups);
+    hipLaunchKernelGGL((recover_runs<K, R, NM, NT, kNtLoad | kNtStore, 4>), dim3(nb), dim3(256), stage, s, a.data + g0 * K * static_cast<uint64_t>(a.P),
+                       a.parity + g0 * R * static_cast<uint64_t>(a.P), a.masks + g0, gn, a.P, a.codebook, rm, a.out,
+                       a.row_start + g0, a.status ? a.status + g0 : nullptr, lb, ticket, a.epoch + c, stage,
+                       c > 0 ? totals + (c - 1) : nullptr, totals + c, c + 1 == launches ? a.total : nullptr, 0u);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// (k, r, P) shapes with a compiled recover_runs: the mask-addressed decode's (try_decode_fused
+// QFEC_FUSED_DS / _D lists), 256 < P <= 2048 or P <= 256 with one 4-B piece.
+hipError_t try_recover_runs(const RunsLaunch& a, uint32_t stage, hipStream_t s, bool dry) {
+  const uint32_t nm = a.P / 1024u, nt = (a.P % 1024u + 255u) / 256u;
+#define QFEC_RUNS(KK, RR, NMM, NTT) \
+  if (a.k == KK && a.r == RR && nm == NMM && nt == NTT) return dry ? hipSuccess : run_recover_runs<KK, RR, NMM, NTT>(a, stage, s);
+#define QFEC_RUNS_P(KK, RR)                                                                                    \
+  QFEC_RUNS(KK, RR, 0, 1) QFEC_RUNS(KK, RR, 0, 2) QFEC_RUNS(KK, RR, 0, 3) QFEC_RUNS(KK, RR, 0, 4)            \
+  QFEC_RUNS(KK, RR, 1, 0) QFEC_RUNS(KK, RR, 1, 1) QFEC_RUNS(KK, RR, 1, 2) QFEC_RUNS(KK, RR, 1, 3) QFEC_RUNS(KK, RR, 1, 4)
+  QFEC_RUNS_P(10, 3)
+  QFEC_RUNS_P(10, 1)
+  QFEC_RUNS_P(10, 2)
+  QFEC_RUNS_P(4, 2)
+#undef QFEC_RUNS_P
+#undef QFEC_RUNS
+  return hipErrorNotSupported;
+}
+
+}  // namespace
+
+uint32_t runs_launches(uint64_t groups) {
+  if (groups == 0) return 0;
+  const uint64_t per = runs_blocks_per_launch(groups) * kRunGroups;
+  return static_cast<uint32_t>((groups + per - 1) / per);
+}
+
+uint64_t runs_workspace_bytes(uint64_t groups) {
+  return 64 + 8 * static_cast<uint64_t>(runs_launches(groups)) + 8 * runs_blocks_per_launch(groups);
+}
+
+bool runs_supported(uint32_t k, uint32_t r, uint32_t P) {
+  RunsLaunch a{};
+  a.k = k;
+  a.r = r;
+  a.P = P;
+  return P >= kVecMinP && try_recover_runs(a, 0, nullptr, true) == hipSuccess;
+}
+
+uint32_t runs_stage_bytes(const RunsLaunch& a) {
+  // the run image needs 16-B aligned row starts in LDS and in HBM
+  if (a.P % 16u != 0 || reinterpret_cast<uintptr_t>(a.out) % 16u != 0) return 0;
+  const int v = a.stage_bytes >= 0 ? a.stage_bytes : env_waves("QUICFEC_RUNS_STAGE", kRunsStageBytes);
+  if (v <= 0) return 0;
+  const uint32_t cap = 64u * 1024u;  // dynamic LDS per workgroup (160 KiB per CU)
+  return static_cast<uint32_t>(v) < cap ? static_cast<uint32_t>(v) : cap;
+}
+
+hipError_t launch_recover_runs(const RunsLaunch& a, hipStream_t s) {
+  if (a.groups == 0) return hipSuccess;
+  if (a.workspace == nullptr || a.row_start == nullptr || a.out == nullptr || a.masks == nullptr) return hipErrorInvalidValue;
+  return try_recover_runs(a, runs_stage_bytes(a), s, false);
 }
 
 hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {

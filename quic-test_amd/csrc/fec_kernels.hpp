@@ -115,6 +115,37 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s);
 uint64_t rows_prefix_workspace_bytes(uint64_t groups);
 hipError_t launch_rows_prefix(const uint64_t* masks, uint64_t groups, uint32_t k, uint32_t r, uint32_t* row_start,
                               uint32_t* block_sums, uint64_t* total, hipStream_t s);
+// Packed recover in one launch (recover_runs, fec_kernels.hip): every workgroup owns 256
+// consecutive groups, finds its run's first row by decoupled look-back (no prefix launches)
+// and writes its rebuilt rows as one contiguous run, staged through an LDS image of up to
+// stage bytes.  Mask-addressed shapes only (runs_supported).
+struct RunsLaunch {
+  const uint8_t* data;
+  const uint8_t* parity;
+  const uint64_t* masks;
+  uint64_t groups;
+  uint32_t k, r, P;
+  const uint8_t* codebook;   // dense CoefEntry codebook (the mask-addressed decode's)
+  LevelMeta meta;
+  uint8_t* out;              // packed rows
+  uint32_t* row_start;       // one u32 per group (written)
+  uint64_t* total;           // nullable: all rows
+  uint8_t* status;           // nullable
+  // runs_workspace_bytes(groups) of device memory, zeroed when first allocated, kept by the
+  // caller stream: ticket counter, chunk totals, look-back words
+  void* workspace;
+  // look-back epoch of the first launch; a call takes runs_launches(groups) epochs, never
+  // reused while the workspace lives (the caller counts; < 2^30, then re-zero the workspace)
+  uint32_t epoch;
+  int stage_bytes = -1;      // LDS run image: -1 tuned default (QUICFEC_RUNS_STAGE), 0 none
+};
+// LDS run image per workgroup (tools/probe_runs.hip).
+constexpr int kRunsStageBytes = 40 * 1024;
+bool runs_supported(uint32_t k, uint32_t r, uint32_t P);
+uint32_t runs_launches(uint64_t groups);
+uint64_t runs_workspace_bytes(uint64_t groups);
+uint32_t runs_stage_bytes(const RunsLaunch& a);
+hipError_t launch_recover_runs(const RunsLaunch& a, hipStream_t s);
 // Whether launch_decode(a) uses the rec_off workspace (every form but the mask-addressed
 // one, which classifies inline).  The caller then provides a workspace private to the call.
 bool decode_needs_rec_off(const DecodeLaunch& a);

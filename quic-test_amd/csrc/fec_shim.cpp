@@ -306,6 +306,10 @@ struct StreamWorkspace {
   hipStream_t s = nullptr;
   DevBuf buf;
   uint64_t last_use = 0;
+  // one-launch packed recover (recover_runs): ticket, chunk totals and look-back words, zeroed
+  // when allocated; `epoch` = the last look-back epoch a launch on this stream used
+  DevBuf runs;
+  uint32_t epoch = 0;
 };
 
 struct FECEncoderCtx {
@@ -522,7 +526,49 @@ int encode_dev_locked(FECEncoderCtx* ctx, const uint8_t* d_data, const void* d_o
 // ctx->mu.
 constexpr size_t kMaxStreamWorkspaces = 16;
 
+hipError_t find_stream_ws(FECEncoderCtx* ctx, hipStream_t s, StreamWorkspace** out);
+
 hipError_t stream_workspace(FECEncoderCtx* ctx, hipStream_t s, size_t bytes, void** out) {
+  StreamWorkspace* w = nullptr;
+  const hipError_t fe = find_stream_ws(ctx, s, &w);
+  if (fe != hipSuccess) return fe;
+  if (bytes > w->buf.cap) {
+    if (w->buf.ptr) {
+      const hipError_t e = hipStreamSynchronize(s);  // queued calls may still read the old one
+      if (e != hipSuccess) return e;
+    }
+    const hipError_t e = w->buf.ensure(bytes);
+    if (e != hipSuccess) return e;
+  }
+  *out = w->buf.ptr;
+  return hipSuccess;
+}
+
+// The recover_runs workspace of caller stream s and the first look-back epoch of a call of G
+// groups.  Epochs are never reused while the buffer lives (words of earlier launches on this
+// stream cannot match); the buffer is zeroed when allocated and when the epochs wrap.
+hipError_t runs_workspace(FECEncoderCtx* ctx, hipStream_t s, uint64_t G, void** out, uint32_t* epoch) {
+  StreamWorkspace* w = nullptr;
+  hipError_t e = find_stream_ws(ctx, s, &w);
+  if (e != hipSuccess) return e;
+  const uint64_t bytes = qfec::runs_workspace_bytes(G);
+  const uint32_t n = qfec::runs_launches(G);
+  if (bytes > w->runs.cap) {
+    if (w->runs.ptr && (e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    if ((e = w->runs.ensure(bytes)) != hipSuccess) return e;
+    w->epoch = 0;
+    if ((e = hipMemsetAsync(w->runs.ptr, 0, w->runs.cap, s)) != hipSuccess) return e;
+  } else if (w->epoch + n >= (1u << 30)) {
+    w->epoch = 0;
+    if ((e = hipMemsetAsync(w->runs.ptr, 0, w->runs.cap, s)) != hipSuccess) return e;
+  }
+  *out = w->runs.ptr;
+  *epoch = w->epoch + 1;
+  w->epoch += n;
+  return hipSuccess;
+}
+
+hipError_t find_stream_ws(FECEncoderCtx* ctx, hipStream_t s, StreamWorkspace** out) {
   StreamWorkspace* w = nullptr;
   for (auto& e : ctx->stream_ws)
     if (e->s == s) {
@@ -542,15 +588,7 @@ hipError_t stream_workspace(FECEncoderCtx* ctx, hipStream_t s, size_t bytes, voi
     w->s = s;
   }
   w->last_use = ++ctx->ws_clock;
-  if (bytes > w->buf.cap) {
-    if (w->buf.ptr) {
-      const hipError_t e = hipStreamSynchronize(s);  // queued calls may still read the old one
-      if (e != hipSuccess) return e;
-    }
-    const hipError_t e = w->buf.ensure(bytes);
-    if (e != hipSuccess) return e;
-  }
-  *out = w->buf.ptr;
+  *out = w;
   return hipSuccess;
 }
 
@@ -616,6 +654,34 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
     if (!plan->dense || qfec::decode_needs_rec_off(a)) {
       set_error("packed recover: no mask-addressed form for k=%u r=%u P=%u (use fec_recover_batch_rs_dev)", k, r, P);
       return FEC_ERR_RANGE;
+    }
+    // Sparse loss (the scan form's share, or QUICFEC_PACKED_RUNS=1): one launch, recover_runs --
+    // each workgroup finds its rows' place by decoupled look-back and writes them as one run
+    // (C5: 0.229-0.235 vs 0.242-0.268 ms for the slot rows; profiles/r04_probe_runs_*.txt).
+    // Dense loss keeps the prefix launches + decode_fused (the runs form rebuilds a workgroup's
+    // groups wave by wave: 2.7-2.8 vs 2.2-2.45 ms at C3).  QUICFEC_PACKED_RUNS=0: never.
+    const long runs_env = [] {
+      const char* v = std::getenv("QUICFEC_PACKED_RUNS");
+      return v && *v ? std::atol(v) : -1L;
+    }();
+    if (runs_env != 0 && (runs_env == 1 || a.scan == qfec::kDecodeScanGroups) && qfec::runs_supported(k, r, P)) {
+      qfec::RunsLaunch ra{};
+      ra.data = d_data;
+      ra.parity = d_parity;
+      ra.masks = d_masks;
+      ra.groups = G;
+      ra.k = k;
+      ra.r = r;
+      ra.P = P;
+      ra.codebook = a.codebook;
+      ra.meta = a.meta;
+      ra.out = d_out;
+      ra.row_start = row_start;
+      ra.total = row_total;
+      ra.status = d_status;
+      QFEC_HIP(runs_workspace(ctx, s, G, &ra.workspace, &ra.epoch));
+      QFEC_HIP(qfec::launch_recover_runs(ra, s));
+      return FEC_OK;
     }
     a.rec_off = row_start;
     a.packed_rows = true;

@@ -5,7 +5,11 @@
 
 --tag NAME: the run timed one decode API only (bench.py --decode-api X --no-other-api), so its
 recover kernel is stored as "recover_NAME" (packed / slots) and merged into an existing out.json
-of the same build, which then holds one entry per API.
+of the same build and workload, which then holds one entry per API.
+
+The profiled bench's own JSON line (<fetch_dir>.json, as scripts/gpu_pmc.sh writes it) names the
+workload the counters were taken on; it is recorded as "workload" (bench.py workload_of_line),
+and bench.py uses the bytes only for a run of that exact workload (and library build).
 
 Corrections (MI355X_MICROARCH.md §HBM and cdna_hip_programming.md §7):
   * FETCH_SIZE / WRITE_SIZE are in KiB;
@@ -53,6 +57,26 @@ def short(name: str) -> str:
     return name[:40]
 
 
+def bench_workload(fdir: Path):
+    """The workload of the profiled bench run: its JSON line in <fdir>.json (last line that parses)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", Path(__file__).resolve().parents[1] / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    p = Path(str(fdir) + ".json")
+    if not p.exists():
+        return None
+    line = None
+    for ln in p.read_text().splitlines():
+        try:
+            d = json.loads(ln)
+        except ValueError:
+            continue
+        if isinstance(d, dict) and "config" in d:
+            line = d
+    return bench.workload_of_line(line) if line else None
+
+
 def main():
     argv = sys.argv[1:]
     tag = None
@@ -69,10 +93,12 @@ def main():
     res = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes)",
            "correction": "FETCH_SIZE x2 (gfx950 wide-stream read), KiB -> bytes",
            # bench.py uses these bytes only while the loaded library is this build
-           "lib_sha256": hashlib.sha256(lib.read_bytes()).hexdigest()}
+           "lib_sha256": hashlib.sha256(lib.read_bytes()).hexdigest(),
+           # ... and on this workload only
+           "workload": bench_workload(fdir)}
     if tag and out.exists():
         prev = json.loads(out.read_text())
-        if prev.get("lib_sha256") == res["lib_sha256"]:
+        if prev.get("lib_sha256") == res["lib_sha256"] and prev.get("workload") == res["workload"]:
             res = {**prev, **res}
     for name in set(fetch) | set(write):
         s = short(name)

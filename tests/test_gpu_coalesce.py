@@ -358,3 +358,43 @@ lib.fec_encoder_free(ctx)
     assert out.returncode == 0, out.stderr[-2000:]
     first_us = float(out.stdout.strip().splitlines()[-1])
     assert first_us < 5000, f"first legacy call took {first_us:.0f} us"
+
+
+def _exit_path_run(mode, calls=300):
+    import json
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "quic-test_amd" / "lib" / "exit_path_test"
+    assert exe.exists(), "build() makes quic-test_amd/lib/exit_path_test (csrc Makefile target tests)"
+    out = subprocess.run([str(exe), mode, str(calls)], capture_output=True, text=True, timeout=90)
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert out.returncode == 0 and lines, (out.returncode, out.stdout, out.stderr)
+    return json.loads(lines[-1])
+
+
+@pytest.mark.parametrize("mode", ["resident", "coalescer", "pageable"])
+def test_exit_makes_no_hip_call(mode):
+    """A process that made legacy calls on each path (resident encoder, shared launches,
+    pageable slab + repair buffer) and returns from main with its encoders alive exits with no
+    HIP call from libfec_hip.so after exit began (the program counts them through its own
+    definitions of the runtime entry points; tests/csrc/exit_path_test.cpp).  A HIP call there
+    aborted a process under rocprofv3 (f13ed47)."""
+    rec = _exit_path_run(mode)
+    if "skip" in rec:
+        pytest.skip(rec["skip"])
+    assert rec["repairs_ok"] is True and rec["calls"] == 300
+    assert rec["calls_after_exit"] == 0, rec["names"]
+
+
+def test_never_serving_resident_poisons_itself():
+    """A resident instance that never serves (QUICFEC_RESIDENT_TEST_NOLAUNCH: a launch is recorded
+    but nothing runs) fails the call that waited on it within the deadline (200 ms here) and takes
+    itself out of service: every later call -- past the ring's 1,024 slots -- completes on the
+    shared-launch path with the right bytes instead of hanging, and the exit stays HIP-free."""
+    import time
+    t0 = time.monotonic()
+    rec = _exit_path_run("nolaunch", calls=1_500)
+    assert time.monotonic() - t0 < 60
+    assert rec["first_rc"] == -2                        # FEC_ERR_HIP
+    assert rec["repairs_ok"] is True and rec["calls"] == 1_500
+    assert rec["calls_after_exit"] == 0, rec["names"]

@@ -249,3 +249,169 @@ def test_full_size_packed_recover(gpu_ctx, oracle_mod, torch_cuda, profile):
         assert bool((data.view(G, k, P)[lost] == 0xEE).all())
     finally:
         gpu_ctx.decode_loss_hint(-1.0)
+
+
+def _iid_masks(rng, G, n, loss):
+    w = np.left_shift(np.uint64(1), np.arange(n, dtype=np.uint64))
+    return ((rng.random((G, n)) < loss) * w).sum(axis=1, dtype=np.uint64)
+
+
+def _check_packed(gpu_ctx, torch, oracle_mod, k, r, P, G, masks, out_offset=0):
+    broken, par, st_exp, start, exp = _case(oracle_mod, k, r, P, G, masks)
+    dd, dp, dm = _dev(torch, broken), _dev(torch, par), _dev(torch, masks.view(np.int64))
+    base = torch.full((max(1, G * r) * P + out_offset,), 0x5A, dtype=torch.uint8, device="cuda")
+    out = base[out_offset:]
+    rs = torch.full((max(1, G),), 0x7FFFFFFF, dtype=torch.int32, device="cuda")
+    tot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    st = torch.full((max(1, G),), 7, dtype=torch.uint8, device="cuda")
+    gpu_ctx.recover_packed_dev(dd, dp, dm, G, k, r, P, out, rs, tot, st)
+    gpu_ctx.synchronize()
+    n = len(exp)
+    assert int(tot.item()) == n
+    assert np.array_equal(rs.cpu().numpy().view(np.uint32), start)
+    assert np.array_equal(st.cpu().numpy(), st_exp)
+    o = out.cpu().numpy().reshape(G * r, P)
+    assert np.array_equal(o[:n], exp)
+    assert (o[n:] == 0x5A).all()                                   # nothing past the last row
+    assert (base[:out_offset].cpu().numpy() == 0x5A).all()        # nothing before the first
+    assert np.array_equal(dd.cpu().numpy(), broken)                # data untouched
+
+
+@pytest.mark.parametrize("k,r,P", [(10, 3, 1200), (10, 3, 700), (10, 3, 1400), (10, 3, 2000), (10, 3, 300),
+                                   (10, 3, 1024), (10, 3, 1040), (10, 3, 1201), (10, 1, 1200), (10, 2, 1200),
+                                   (10, 2, 700), (4, 2, 513), (4, 2, 1200)])
+@pytest.mark.parametrize("stage", ["default", "0", "16384", "65536"])
+def test_packed_runs_one_launch(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, k, r, P, stage):
+    """The one-launch packed recover (recover_runs: decoupled look-back row starts, rows staged
+    per workgroup in an LDS image and written as one run) on every mask-addressed piece layout,
+    forced for mixed loss (QUICFEC_PACKED_RUNS=1), with the image off, small (most rows past it go
+    straight to HBM) and large; bit-exact against the oracle."""
+    monkeypatch.setenv("QUICFEC_PACKED_RUNS", "1")
+    if stage != "default":
+        monkeypatch.setenv("QUICFEC_RUNS_STAGE", stage)
+    G = 3_001
+    rng = np.random.default_rng(k * 1000 + r * 100 + P + len(stage))
+    masks = np.zeros(G, dtype=np.uint64)
+    for g in range(G):
+        for s in rng.permutation(k + r)[: rng.integers(0, r + 2)]:
+            masks[g] |= np.uint64(1) << np.uint64(int(s))
+    _check_packed(gpu_ctx, torch_cuda, oracle_mod, k, r, P, G, masks)
+
+
+@pytest.mark.parametrize("case", ["chunks", "odd_output", "sparse_hint", "tiny", "one_group_per_tile"])
+def test_packed_runs_edges(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, case):
+    """recover_runs edges: chunked launches (QUICFEC_MAX_WAVE_BLOCKS=2, each chunk's rows start
+    after the previous chunk's total), an output at an odd address (no LDS image: rows straight
+    to HBM), the library's own choice from the loss hint, calls of 1-7 groups, and tiles where a
+    single group rebuilds."""
+    torch = torch_cuda
+    k, r, P = 10, 3, 1200
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    off = 0
+    if case == "chunks":
+        monkeypatch.setenv("QUICFEC_PACKED_RUNS", "1")
+        monkeypatch.setenv("QUICFEC_MAX_WAVE_BLOCKS", "2")
+        G = 5_555
+        masks = _iid_masks(rng, G, k + r, 0.05)
+    elif case == "odd_output":
+        monkeypatch.setenv("QUICFEC_PACKED_RUNS", "1")
+        G, off = 2_049, 5
+        masks = _iid_masks(rng, G, k + r, 0.08)
+    elif case == "sparse_hint":
+        G = 20_000
+        masks = _iid_masks(rng, G, k + r, 0.01)
+        gpu_ctx.decode_loss_hint(1.0 - 0.99 ** k)
+    elif case == "tiny":
+        monkeypatch.setenv("QUICFEC_PACKED_RUNS", "1")
+        for G in range(1, 8):
+            masks = _iid_masks(rng, G, k + r, 0.3)
+            _check_packed(gpu_ctx, torch, oracle_mod, k, r, P, G, masks)
+        return
+    else:
+        monkeypatch.setenv("QUICFEC_PACKED_RUNS", "1")
+        G = 4_096
+        masks = np.zeros(G, dtype=np.uint64)
+        masks[::700] = np.uint64(0b101)                                 # 2 lost data shards
+    try:
+        _check_packed(gpu_ctx, torch, oracle_mod, k, r, P, G, masks, out_offset=off)
+    finally:
+        gpu_ctx.decode_loss_hint(-1.0)
+
+
+def test_packed_runs_back_to_back(gpu_ctx, oracle_mod, torch_cuda, monkeypatch):
+    """Several one-launch packed recovers queued on one stream without a synchronise between
+    them, growing and shrinking: every launch takes fresh look-back epochs (words left by the
+    earlier launches never match) and the workspace grows under queued work."""
+    monkeypatch.setenv("QUICFEC_PACKED_RUNS", "1")
+    torch = torch_cuda
+    k, r, P = 10, 3, 700
+    rng = np.random.default_rng(4242)
+    runs = []
+    for G in (1_031, 60_000, 7, 60_000, 300):
+        masks = _iid_masks(rng, G, k + r, 0.06)
+        broken, par, st_exp, start, exp = _case(oracle_mod, k, r, P, G, masks)
+        dd, dp, dm = _dev(torch, broken), _dev(torch, par), _dev(torch, masks.view(np.int64))
+        out = torch.full((G * r * P,), 0x5A, dtype=torch.uint8, device="cuda")
+        rs = torch.zeros(G, dtype=torch.int32, device="cuda")
+        tot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+        gpu_ctx.recover_packed_dev(dd, dp, dm, G, k, r, P, out, rs, tot)
+        runs.append((G, out, rs, tot, start, exp, dd, dp, dm))
+    gpu_ctx.synchronize()
+    for G, out, rs, tot, start, exp, *_ in runs:
+        n = len(exp)
+        assert int(tot.item()) == n, G
+        assert np.array_equal(rs.cpu().numpy().view(np.uint32), start), G
+        assert np.array_equal(out.cpu().numpy().reshape(G * r, P)[:n], exp), G
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("profile", ["c3_two_erasures", "c5_satellite_iid"])
+def test_full_size_slot_recover(gpu_ctx, oracle_mod, torch_cuda, profile):
+    """fec_recover_batch_rs_dev (rebuilt packets at (g*r + m)*P, the bench's C3 decode) at
+    BASELINE size: every group's slots against the original packets, statuses against the
+    masks, sampled groups against the oracle's decode."""
+    torch = torch_cuda
+    k, r, P, G = 10, 3, 1200, 1_000_000
+    data = torch.empty(G * k * P, dtype=torch.uint8, device="cuda")
+    par = torch.empty(G * r * P, dtype=torch.uint8, device="cuda")
+    gpu_ctx.fill_random_dev(data, data.numel(), SEED + 21)
+    gpu_ctx.encode_dev(data, G, k, r, P, par)
+    rng = np.random.default_rng(SEED + 22)
+    if profile == "c3_two_erasures":
+        pos = np.argsort(rng.random((G, k + r)), axis=1)[:, :2].astype(np.uint64)
+        masks = np.left_shift(np.uint64(1), pos).sum(axis=1, dtype=np.uint64)
+    else:
+        masks = _iid_masks(rng, G, k + r, 0.01)
+        gpu_ctx.decode_loss_hint(1.0 - 0.99 ** k)
+    try:
+        orig = data.clone()
+        dm = torch.from_numpy(masks.view(np.int64)).cuda()
+        bits = torch.arange(k, device="cuda", dtype=torch.int64)
+        lost = ((dm.view(G, 1) >> bits.view(1, k)) & 1).bool()
+        data.view(G, k, P)[lost] = 0xEE
+        out = torch.full((G * r * P,), 0x5A, dtype=torch.uint8, device="cuda")
+        st = torch.full((G,), 7, dtype=torch.uint8, device="cuda")
+        gpu_ctx.recover_dev(data, par, dm, G, k, r, P, out, st)
+        gpu_ctx.synchronize()
+        lost_h = ((masks[:, None] >> np.arange(k, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+        plost = ((masks[:, None] >> np.arange(k, k + r, dtype=np.uint64)[None, :]) & np.uint64(1)).sum(axis=1)
+        e = lost_h.sum(axis=1)
+        ok = e <= r - plost
+        assert np.array_equal(st.cpu().numpy(), (~ok).astype(np.uint8))
+        okd = torch.from_numpy(ok).cuda()
+        e_g = lost.sum(dim=1, keepdim=True)
+        slots = torch.arange(r, device="cuda").view(1, r) < e_g
+        got = out.view(G, r, P)[slots & okd.view(G, 1)]
+        want = orig.view(G, k, P)[lost & okd.view(G, 1)]
+        assert torch.equal(got, want)
+        # slots past a group's rebuilt rows, and every slot of unrecoverable groups, untouched
+        assert bool((out.view(G, r, P)[~(slots & okd.view(G, 1))] == 0x5A).all())
+        cand = np.nonzero(ok & (e > 0))[0]
+        for g in [int(x) for x in rng.choice(cand, size=min(48, len(cand)), replace=False)]:
+            blk = data[g * k * P:(g + 1) * k * P].cpu().numpy().copy()
+            pb = par[g * r * P:(g + 1) * r * P].cpu().numpy()
+            oracle_mod.rs_decode(blk, pb, masks[g:g + 1].copy(), 1, k, r, P)
+            ids = np.nonzero(lost_h[g])[0]
+            assert np.array_equal(out.view(G, r, P)[g, :len(ids)].cpu().numpy(), blk.reshape(k, P)[ids]), g
+    finally:
+        gpu_ctx.decode_loss_hint(-1.0)
