@@ -1084,6 +1084,10 @@ __device__ __forceinline__ uint32_t runs_rebuild(uint64_t g, uint64_t m, uint32_
   }
 #pragma unroll
   for (int s = 0; s < K; ++s) {
+    // survivor s's selectors stay in its iteration (left alone, LLVM hoists every survivor's
+    // selectors ahead of the arithmetic: 160 VGPRs, 3 waves per SIMD; see decode_fused kLdsTabs)
+#pragma unroll
+    for (int q = 0; q < NW; ++q) __asm__ volatile("" : "+v"(x[s][q]));
     uint32_t s0[NW], s1[NW], s2[NW];
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
@@ -1127,9 +1131,9 @@ __global__ __launch_bounds__(64 * WAVES) void recover_runs(const uint8_t* __rest
                                                     uint64_t* __restrict__ total_out, uint64_t* __restrict__ total_user,
                                                     uint32_t flags) {
   static_assert(R <= 3, "mask-addressed shapes: r <= 3");
-  static_assert(TG <= 64 * WAVES && TG % 64 == 0, "one classifying thread per group, whole waves");
+  static_assert(TG <= 64 * WAVES && (TG % 64 == 0 || TG < 64), "one classifying thread per group");
   constexpr uint32_t kTile = TG;
-  constexpr uint32_t kScanWaves = TG / 64;
+  constexpr uint32_t kScanWaves = TG >= 64 ? TG / 64 : 1;
   constexpr int NW = 4 * NM + NT;
   constexpr uint64_t kmask = (1ull << K) - 1;
   constexpr uint64_t rmask = (1ull << R) - 1;
@@ -1187,16 +1191,14 @@ __global__ __launch_bounds__(64 * WAVES) void recover_runs(const uint8_t* __rest
     s_mask[i] = m;
     s_item[i] = (tid << 16) | lrow;
   }
-  if (wave == 0) {
-    // decoupled look-back
+  // The run's first row (wave 0): decoupled look-back over the tiles before this one.
+  auto find_first = [&]() {
     const uint64_t tag = static_cast<uint64_t>(epoch) << kRunEpochShift;
     const uint32_t base = base_in != nullptr ? static_cast<uint32_t>(*base_in) : 0u;
     uint32_t excl = 0;
     if (tile == 0) {
-      excl = base;
-      if (lane == 0) __hip_atomic_store(&lb[0], tag | kRunIncl | (base + A), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      excl = base;  // published with its row count below
     } else {
-      if (lane == 0) __hip_atomic_store(&lb[tile], tag | kRunAgg | A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int64_t pos = static_cast<int64_t>(tile) - 1;
       for (;;) {
         const int64_t idx = pos - static_cast<int64_t>(lane);
@@ -1226,12 +1228,21 @@ __global__ __launch_bounds__(64 * WAVES) void recover_runs(const uint8_t* __rest
         if (total_user != nullptr) *total_user = static_cast<uint64_t>(excl) + A;
       }
     }
-  }
-  __syncthreads();
-  const uint32_t first = s_first;
-  if (tid < kTile && g < groups) row_start[g] = first + lrow;
+  };
+  // Publish this tile's row count at once (successors look back through it), then find the run's
+  // first row: before the rebuild when some rows go straight to HBM (they need their place), after
+  // it when every row fits the LDS image -- the look-back's wait then hides behind the rebuild.
   const uint32_t cap_rows = stage_bytes / P;
-  uint8_t* run = out + static_cast<uint64_t>(first) * P;
+  const bool defer = (flags & 1u) == 0 && A <= cap_rows;
+  // (tile 0 knows its first row already: the rows before this launch)
+  if (wave == 0 && lane == 0) {
+    const uint64_t tag = static_cast<uint64_t>(epoch) << kRunEpochShift;
+    const uint64_t w = tile == 0 ? tag | kRunIncl | ((base_in != nullptr ? static_cast<uint32_t>(*base_in) : 0u) + A)
+                                 : tag | kRunAgg | A;
+    __hip_atomic_store(&lb[tile], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (!defer && wave == 0) find_first();
+  __syncthreads();
   uint32_t toff[NT > 0 ? NT : 1];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -1260,12 +1271,12 @@ __global__ __launch_bounds__(64 * WAVES) void recover_runs(const uint8_t* __rest
                 u32x4{acc[mm][4 * q], acc[mm][4 * q + 1], acc[mm][4 * q + 2], acc[mm][4 * q + 3]};
 #pragma unroll
           for (int t = 0; t < NT; ++t) *reinterpret_cast<uint32_t*>(dst + toff[t]) = acc[mm][4 * NM + t];
-        } else {
-          uint8_t* dst = run + static_cast<uint64_t>(row) * P;
+        } else {  // past the image (never when defer): straight to the row's place
+          uint8_t* dst = out + (static_cast<uint64_t>(s_first) + row) * P;
 #pragma unroll
           for (int q = 0; q < NM; ++q)
             st16<POL>(dst + q * 1024u + lane * 16u,
-                           u32x4{acc[mm][4 * q], acc[mm][4 * q + 1], acc[mm][4 * q + 2], acc[mm][4 * q + 3]});
+                      u32x4{acc[mm][4 * q], acc[mm][4 * q + 1], acc[mm][4 * q + 2], acc[mm][4 * q + 3]});
 #pragma unroll
           for (int t = 0; t < NT; ++t) {
             if constexpr ((POL & kNtStore) != 0) __builtin_nontemporal_store(acc[mm][4 * NM + t], reinterpret_cast<u32u*>(dst + toff[t]));
@@ -1275,10 +1286,17 @@ __global__ __launch_bounds__(64 * WAVES) void recover_runs(const uint8_t* __rest
       }
     }
   }
+  if (defer) {
+    __syncthreads();  // (the image is complete, too)
+    if (wave == 0) find_first();
+  }
+  __syncthreads();
+  const uint32_t first = s_first;
+  if (tid < kTile && g < groups) row_start[g] = first + lrow;
   const uint32_t staged = (flags & 1u) ? 0u : (A < cap_rows ? A : cap_rows);
   if (staged == 0u) return;
-  __syncthreads();
   // the image leaves in 16-B pieces by consecutive threads: whole lines but at the run's ends
+  uint8_t* run = out + static_cast<uint64_t>(first) * P;
   const uint32_t n16 = staged * P / 16u;
   for (uint32_t c = tid; c < n16; c += 64u * WAVES)
     st16<POL>(run + c * 16u, *reinterpret_cast<const u32x4*>(run_image + c * 16u));

@@ -213,6 +213,13 @@ int main(int argc, char** argv) {
                       }, false, {}});
     RF("runs w8 nl st48K" + at, NL, 8, 512, 49152, 0, chk, outs[i])
     RF("runs w8 nl+ns st48K" + at, NL | NS, 8, 512, 49152, 0, chk, outs[i])
+    if (loss == 0) {  // dense: small tiles, every row in the image, look-back after the rebuild
+      RF("runs w8 tg8 nl+ns st29K" + at, NL | NS, 8, 8, 28800, 0, chk, outs[i])
+      RF("runs w8 tg8 nl st29K" + at, NL, 8, 8, 28800, 0, chk, outs[i])
+      RF("runs w8 tg16 nl+ns st58K" + at, NL | NS, 8, 16, 57600, 0, chk, outs[i])
+      RF("runs w4 tg8 nl+ns st29K" + at, NL | NS, 4, 8, 28800, 0, chk, outs[i])
+      RF("runs w8 tg8 nostore" + at, NL, 8, 8, 28800, 1, false, outs[i])
+    }
     if (loss > 0) {
       RF("runs w8 nl+ns st32K" + at, NL | NS, 8, 512, 32768, 0, chk, outs[i])
       RF("runs w4 nl+ns st24K" + at, NL | NS, 4, 256, 24576, 0, chk, outs[i])

@@ -43,9 +43,11 @@ K_COMPACT_OUT = 1024  # fec_kernels.hip kCompactOut: the recover (rebuilt packet
 
 def short(name: str) -> str:
     """Summary key of a kernel: encode, recover (decode forms with kCompactOut in their
-    policy template argument), decode (in place), or the kernel's own name."""
+    policy template argument, and recover_runs), decode (in place), or the kernel's own name."""
     if "encode_v16" in name or "encode_bits" in name:
         return "encode"
+    if "recover_runs" in name:  # the one-launch packed recover (always the recover layout)
+        return "recover"
     for key in ("decode_fused", "decode_wave", "decode_v16", "decode_tiled"):
         if key in name:
             args = name.split(key + "<", 1)[1].split(">", 1)[0].split(",")

@@ -22,6 +22,7 @@ def test_kernel_keys():
     assert short(ns + "decode_fused<10, 3, 1027, 1, 1, true, true, 0>(unsigned char const*, ...)") == "recover"
     assert short(ns + "decode_fused<10, 3, 3, 1, 1, true, true, 0>(unsigned char const*, ...)") == "decode"
     assert short("qfec::(anonymous namespace)::classify(unsigned long const*, ...)") == "classify"
+    assert short(ns + "recover_runs<10, 3, 1, 1, 3, 4, 256>(unsigned char const*, ...)") == "recover"
 
 
 def test_committed_pmc_files_have_the_bench_keys():
