@@ -993,7 +993,7 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
 // to back, group g's from row row_start[g] (exclusive prefix sum of the rows every group
 // rebuilds: its lost data shards when recoverable, else 0).
 //
-// A workgroup owns kRunGroups consecutive groups (one erasure mask per thread), so all of
+// A workgroup owns a tile of consecutive groups (one erasure mask per thread), so all of
 // their rebuilt rows form ONE contiguous run of the packed list:
 //  1. every thread classifies its group (status byte; rows), the block scans the rows and
 //     lists the groups to rebuild in LDS, in group order;
@@ -1010,7 +1010,6 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
 // Look-back words: epoch (bits 34..63) | flag (bits 32..33: kRunAgg, kRunIncl) | rows.  The
 // epoch is the launch's, so words left by earlier launches never match (no reset launch).
 // ---------------------------------------------------------------------------------
-constexpr uint32_t kRunGroups = 256;
 constexpr uint64_t kRunAgg = 1ull << 32;
 constexpr uint64_t kRunIncl = 2ull << 32;
 constexpr uint32_t kRunEpochShift = 34;
@@ -2356,6 +2355,12 @@ hipError_t launch_rows_prefix(const uint64_t* masks, uint64_t groups, uint32_t k
 
 namespace {
 
+// The library's form: 8 waves per workgroup, 512 groups per tile, NT loads and stores (tools/
+// probe_runs.hip over four boxes, C5: 0.229-0.251 ms vs 0.241-0.268 for the slot rows and
+// 0.241-0.262 for the two-step packed rows; 4 waves x 256 groups 0.247-0.253; profiles/r04_probe_runs_*.txt).
+constexpr int kRunWaves = 8;
+constexpr uint32_t kRunGroups = 64u * kRunWaves;
+
 uint64_t runs_blocks_per_launch(uint64_t groups) {
   const uint64_t nb = (groups + kRunGroups - 1) / kRunGroups;
   const uint64_t mb = max_wave_blocks();
@@ -2380,7 +2385,7 @@ hipError_t run_recover_runs(const RunsLaunch& a, uint32_t stage, hipStream_t s) 
     const uint64_t g0 = c * per;
     const uint64_t gn = a.groups - g0 < per ? a.groups - g0 : per;
     const uint32_t nb = static_cast<uint32_t>((gn + kRunGroups - 1) / kRunGroups);
-    hipLaunchKernelGGL((recover_runs<K, R, NM, NT, kNtLoad | kNtStore, 4>), dim3(nb), dim3(256), stage, s, a.data + g0 * K * static_cast<uint64_t>(a.P),
+    hipLaunchKernelGGL((recover_runs<K, R, NM, NT, kNtLoad | kNtStore, kRunWaves>), dim3(nb), dim3(64 * kRunWaves), stage, s, a.data + g0 * K * static_cast<uint64_t>(a.P),
                        a.parity + g0 * R * static_cast<uint64_t>(a.P), a.masks + g0, gn, a.P, a.codebook, rm, a.out,
                        a.row_start + g0, a.status ? a.status + g0 : nullptr, lb, ticket, a.epoch + c, stage,
                        c > 0 ? totals + (c - 1) : nullptr, totals + c, c + 1 == launches ? a.total : nullptr, 0u);

@@ -115,7 +115,7 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s);
 uint64_t rows_prefix_workspace_bytes(uint64_t groups);
 hipError_t launch_rows_prefix(const uint64_t* masks, uint64_t groups, uint32_t k, uint32_t r, uint32_t* row_start,
                               uint32_t* block_sums, uint64_t* total, hipStream_t s);
-// Packed recover in one launch (recover_runs, fec_kernels.hip): every workgroup owns 256
+// Packed recover in one launch (recover_runs, fec_kernels.hip): every workgroup owns 512
 // consecutive groups, finds its run's first row by decoupled look-back (no prefix launches)
 // and writes its rebuilt rows as one contiguous run, staged through an LDS image of up to
 // stage bytes.  Mask-addressed shapes only (runs_supported).
@@ -139,8 +139,9 @@ struct RunsLaunch {
   uint32_t epoch;
   int stage_bytes = -1;      // LDS run image: -1 tuned default (QUICFEC_RUNS_STAGE), 0 none
 };
-// LDS run image per workgroup (tools/probe_runs.hip).
-constexpr int kRunsStageBytes = 40 * 1024;
+// LDS run image per workgroup of 512 groups (tools/probe_runs.hip): C5's
+// ~59 rows per tile fit 48 KB (40 rows) mostly; two workgroups per CU.
+constexpr int kRunsStageBytes = 48 * 1024;
 bool runs_supported(uint32_t k, uint32_t r, uint32_t P);
 uint32_t runs_launches(uint64_t groups);
 uint64_t runs_workspace_bytes(uint64_t groups);
