@@ -213,6 +213,27 @@ int main(int argc, char** argv) {
                       }, false, {}});
     RF("runs w8 nl st48K" + at, NL, 8, 512, 49152, 0, chk, outs[i])
     RF("runs w8 nl+ns st48K" + at, NL | NS, 8, 512, 49152, 0, chk, outs[i])
+    if (loss == 0 && std::getenv("PROBE_SLOTS_POLICY")) {  // the slot-row recover's store policy by buffer
+      vars.push_back({"slots nt-ld+nt-st (lib)" + at, [&, o = outs[i]] {
+                        DecodeLaunch a = dl;
+                        a.out = o;
+                        return run_decode_fused<10, 3, kNtStore | kNtLoad | kCompactOut, 1, 1, true>(a, nullptr);
+                      }, false, {}});
+      vars.push_back({"slots nt-ld plain-st" + at, [&, o = outs[i]] {
+                        DecodeLaunch a = dl;
+                        a.out = o;
+                        return run_decode_fused<10, 3, kNtLoad | kCompactOut, 1, 1, true>(a, nullptr);
+                      }, false, {}});
+      vars.push_back({"slots plain-ld nt-st" + at, [&, o = outs[i]] {
+                        DecodeLaunch a = dl;
+                        a.out = o;
+                        return run_decode_fused<10, 3, kNtStore | kCompactOut, 1, 1, true>(a, nullptr);
+                      }, false, {}});
+      vars.push_back({"slots nostore-probe copy" + at, [&, o = outs[i]] {  // parity -> out copy of the rows' size
+                        return launch_copy_words(par, o, uint64_t(G) * 3 * P / 2 / 16 * 16, nullptr);
+                      }, false, {}});
+      continue;
+    }
     if (loss == 0) {  // dense: small tiles, every row in the image, look-back after the rebuild
       RF("runs w8 tg8 nl+ns st29K" + at, NL | NS, 8, 8, 28800, 0, chk, outs[i])
       RF("runs w8 tg8 nl st29K" + at, NL, 8, 8, 28800, 0, chk, outs[i])

@@ -146,3 +146,63 @@ def test_random_batchers(quicfec_mod, oracle_mod, block):
                 ids, rows = db.wait(int(t), timeout_us=5_000_000)
                 assert ids == sorted(s for s in lost if s < k)
                 assert all(np.array_equal(row, shards[j]) for j, row in zip(ids, rows)), (k, r, slot, mg, dl)
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_random_packed_recover(gpu_ctx, oracle_mod, torch_cuda, block):
+    """The packed recover with random mask-addressed shapes, sizes and loss rates, through both
+    of its forms chosen at random per call (the one-launch recover_runs and the prefix launches +
+    decode_fused), one context, calls of different shapes interleaved: rows, row starts, total and
+    statuses against the oracle."""
+    torch = torch_cuda
+    rng = np.random.default_rng(SEED + 200 + block)
+    shapes = [(10, 3), (10, 2), (10, 1), (4, 2)]
+    saved = os.environ.get("QUICFEC_PACKED_RUNS")
+    try:
+        for _ in range(8):
+            k, r = shapes[int(rng.integers(0, len(shapes)))]
+            P = int(rng.choice([1200, int(rng.integers(257, 2048))]))
+            G = int(rng.integers(1, 6000))
+            loss = float(rng.choice([0.005, 0.02, 0.1, 0.3]))
+            mode = str(rng.choice(["auto", "1", "0"]))
+            if mode == "auto":
+                os.environ.pop("QUICFEC_PACKED_RUNS", None)
+            else:
+                os.environ["QUICFEC_PACKED_RUNS"] = mode
+            gpu_ctx.decode_loss_hint(1.0 - (1.0 - loss) ** k if rng.random() < 0.5 else -1.0)
+            w = np.left_shift(np.uint64(1), np.arange(k + r, dtype=np.uint64))
+            masks = ((rng.random((G, k + r)) < loss) * w).sum(axis=1, dtype=np.uint64)
+            data = oracle_mod.splitmix_bytes(G * k * P, int(rng.integers(0, 1 << 30)))
+            par = oracle_mod.rs_encode(data, G, k, r, P, nthreads=4)
+            lost = ((masks[:, None] >> np.arange(k, dtype=np.uint64)[None, :]) & np.uint64(1)).astype(bool)
+            broken = data.copy().reshape(G, k, P)
+            broken[lost] = 0xEE
+            ref = broken.copy().reshape(-1)
+            _, st_exp = oracle_mod.rs_decode(ref, par, masks, G, k, r, P, nthreads=4)
+            ok = st_exp == 0
+            rows = np.where(ok, lost.sum(axis=1), 0)
+            start = np.concatenate([[0], np.cumsum(rows)[:-1]]).astype(np.uint32)
+            exp = ref.reshape(G, k, P)[lost & ok[:, None]]
+            dd = torch.from_numpy(broken.reshape(-1)).cuda()
+            dp = torch.from_numpy(par).cuda()
+            dm = torch.from_numpy(masks.view(np.int64)).cuda()
+            out = torch.full((G * r * P,), 0x5A, dtype=torch.uint8, device="cuda")
+            rs = torch.zeros(G, dtype=torch.int32, device="cuda")
+            tot = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+            st = torch.full((G,), 7, dtype=torch.uint8, device="cuda")
+            gpu_ctx.recover_packed_dev(dd, dp, dm, G, k, r, P, out, rs, tot, st)
+            gpu_ctx.synchronize()
+            tag = (k, r, P, G, loss, mode)
+            n = len(exp)
+            assert int(tot.item()) == n, tag
+            assert np.array_equal(rs.cpu().numpy().view(np.uint32), start), tag
+            assert np.array_equal(st.cpu().numpy(), st_exp), tag
+            o = out.cpu().numpy().reshape(G * r, P)
+            assert np.array_equal(o[:n], exp), tag
+            assert (o[n:] == 0x5A).all(), tag
+    finally:
+        gpu_ctx.decode_loss_hint(-1.0)
+        if saved is None:
+            os.environ.pop("QUICFEC_PACKED_RUNS", None)
+        else:
+            os.environ["QUICFEC_PACKED_RUNS"] = saved
