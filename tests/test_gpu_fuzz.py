@@ -15,6 +15,8 @@ pytestmark = pytest.mark.gpu
 # committed 12 blocks of 10 cases)
 SEED = int(os.environ.get("QUICFEC_FUZZ_SEED", str(0x5EED0F00)), 0)
 BLOCKS = int(os.environ.get("QUICFEC_FUZZ_BLOCKS", "12"))
+# the packed-recover sweep: 4 blocks of 8 calls by default, a third of QUICFEC_FUZZ_BLOCKS when wider
+PACKED_BLOCKS = max(4, BLOCKS // 3)
 
 
 def _case(rng):
@@ -148,7 +150,7 @@ def test_random_batchers(quicfec_mod, oracle_mod, block):
                 assert all(np.array_equal(row, shards[j]) for j, row in zip(ids, rows)), (k, r, slot, mg, dl)
 
 
-@pytest.mark.parametrize("block", range(4))
+@pytest.mark.parametrize("block", range(PACKED_BLOCKS))
 def test_random_packed_recover(gpu_ctx, oracle_mod, torch_cuda, block):
     """The packed recover with random mask-addressed shapes, sizes and loss rates, through both
     of its forms chosen at random per call (the one-launch recover_runs and the prefix launches +
