@@ -572,8 +572,8 @@ class Resident {
     if (n == 0) return;
     const double us = 1000.0 / double(tick_khz);
     std::fprintf(stderr,
-                 "{\"resident_stamps\": {\"batches\": %u, \"us\": {\"poll\": %.2f, \"acquire\": %.2f, \"work\": %.2f, "
-                 "\"release\": %.2f, \"done\": %.2f}, \"mean_slots\": %.2f, \"mean_polls\": %.2f}}\n",
+                 "{\"resident_stamps\": {\"batches\": %u, \"us\": {\"poll\": %.2f, \"acquire\": %.2f, \"loads\": %.2f, "
+                 "\"store_issue\": %.2f, \"acked_barrier_done\": %.2f}, \"mean_slots\": %.2f, \"mean_polls\": %.2f}}\n",
                  n, sum[0] / n * us, sum[1] / n * us, sum[2] / n * us, sum[3] / n * us, sum[4] / n * us, sum[5] / n,
                  sum[6] / n);
   }

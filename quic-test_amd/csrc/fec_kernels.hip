@@ -1742,12 +1742,16 @@ __device__ __forceinline__ void sys_store_relaxed(uint64_t* p, uint64_t v) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
 #error "legacy_server assumes gfx94x/gfx95x volatile stores are sc0 sc1 write-through (sys_store_16b)"
 #endif
-__device__ __forceinline__ void sys_store_16b(uint8_t* p, u32x4 v) { *reinterpret_cast<volatile u32x4u*>(p) = v; }
+__device__ __forceinline__ void sys_store_16b(uint8_t* p, u32x4 v) {
+  *reinterpret_cast<volatile __attribute__((address_space(1))) u32x4u*>(reinterpret_cast<uintptr_t>(p)) = v;
+}
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // 16 bytes of host memory as they are now (system-coherent load, no cache).
-__device__ __forceinline__ u64x2 sys_load_16(const uint64_t* p) { return *reinterpret_cast<const volatile u64x2*>(p); }
+__device__ __forceinline__ u64x2 sys_load_16(const uint64_t* p) {
+  return *reinterpret_cast<const volatile __attribute__((address_space(1))) u64x2*>(reinterpret_cast<uintptr_t>(p));
+}
 
 __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot* __restrict__ ring,
                                                                 uint64_t* __restrict__ done,
@@ -1769,7 +1773,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
   // Diagnostic stamps (stamps != nullptr, QUICFEC_RESIDENT_STAMPS): thread 0's wall clock at the
   // phases of each served batch, into a ring of 256 records of 8 words in host memory that no
   // other code reads; never part of a result.
-  uint64_t st_batches = 0, st_polls = 0, st_t[6] = {};
+  uint64_t st_batches = 0, st_polls = 0, st_t[7] = {};
   for (uint32_t it = 0; it < kServerMaxPolls; ++it) {
     const uint64_t next = s_next;
     if (stamps != nullptr && tid == 0) st_t[0] = static_cast<uint64_t>(wall_clock64());
@@ -1848,15 +1852,33 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
 #pragma unroll
           for (uint32_t j = 0; j < kServerPackets; ++j) ad[j] = s_head[i][2 + j];
         } else {
-          // written by the host before the slot's first group and header, seen complete above
+          // written by the host before the slot's first group and header, seen complete above;
+          // relaxed system-scope loads (uncached, all ten in flight: volatile loads were each
+          // followed by a full wait, one PCIe round trip apiece)
           const uint64_t* src = ring[(next + i) % kServerSlots].addr + g * kServerPackets;
 #pragma unroll
-          for (uint32_t j = 0; j < kServerPackets; ++j) ad[j] = *reinterpret_cast<const volatile uint64_t*>(src + j);
+          for (uint32_t j = 0; j < kServerPackets; ++j)
+            ad[j] = __hip_atomic_load(reinterpret_cast<const __attribute__((address_space(1))) uint64_t*>(
+                                          reinterpret_cast<uintptr_t>(src + j)),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        u32x4 acc = ld16<0>(reinterpret_cast<const uint8_t*>(ad[0] & kServerAddrMask) + coff);
+        // All ten packet loads in flight at once, as global (address space 1) loads: the addresses
+        // come from integers, so plain pointers compile to flat loads, which count on lgkmcnt too
+        // and were issued two at a time with a full wait between pairs -- five dependent PCIe
+        // round trips, ~8 us of a ~12-us call (the server's stamps).
+        u32x4 v[kServerPackets];
 #pragma unroll
-        for (uint32_t j = 1; j < kServerPackets; ++j)
-          acc ^= ld16<0>(reinterpret_cast<const uint8_t*>(ad[j] & kServerAddrMask) + coff);
+        for (uint32_t j = 0; j < kServerPackets; ++j)
+          v[j] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4u*>((ad[j] & kServerAddrMask) + coff);
+#pragma unroll
+        for (uint32_t j = 0; j < kServerPackets; ++j) __asm__ volatile("" : "+v"(v[j]));  // no load sunk into the XOR
+        u32x4 acc = v[0];
+#pragma unroll
+        for (uint32_t j = 1; j < kServerPackets; ++j) acc ^= v[j];
+        if (stamps != nullptr && tid == 0 && w == 0) {  // thread 0's packet loads have returned
+          __asm__ volatile("" : "+v"(acc));
+          st_t[6] = static_cast<uint64_t>(wall_clock64());
+        }
         uint8_t* dst = reinterpret_cast<uint8_t*>(s_head[i][0] & kServerAddrMask) + static_cast<uint64_t>(g) * P + coff;
         sys_store_16b(dst, acc);
       }
@@ -1879,9 +1901,9 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
         uint64_t* rec = stamps + (st_batches % 256) * 8;
         rec[0] = st_t[1] - st_t[0];  // the poll that found the run
         rec[1] = st_t[2] - st_t[1];  // decision + acquire fence
-        rec[2] = st_t[3] - st_t[2];  // thread 0's work items
-        rec[3] = st_t[4] - st_t[3];  // release fence
-        rec[4] = st_t[5] - st_t[4];  // barrier + done stores
+        rec[2] = st_t[6] - st_t[2];  // thread 0's first work item: its 10 packet loads
+        rec[3] = st_t[3] - st_t[6];  // its store (and any further items)
+        rec[4] = st_t[5] - st_t[3];  // stores acknowledged + barrier + done stores
         rec[5] = n;
         rec[6] = st_polls;           // polls since the previous batch, this one included
         __threadfence_system();
