@@ -1757,16 +1757,26 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
                                                                 uint64_t* __restrict__ done,
                                                                 ServerControl* __restrict__ ctl, uint64_t start_seq,
                                                                 uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                                                uint64_t* __restrict__ stamps) {
+                                                                uint64_t* __restrict__ stamps, uint32_t spec_on) {
   __shared__ uint64_t s_next;
   __shared__ uint32_t s_n, s_exit, s_stop;
   __shared__ uint32_t s_first[kServerPoll + 1];  // work items before slot i of the run
   __shared__ uint32_t s_P[kServerPoll], s_cpp[kServerPoll];
   __shared__ uint64_t s_head[kServerPoll][kServerHeadWords];  // out, shape, addr[0..13] (tagged)
+  // The speculative poll: while a batch is being served, the last kSpecThreads threads read the
+  // slots after it (and the stop word); the next iteration uses those words instead of polling
+  // again when it starts at s_spec_seq.  A slot completed after the read simply looks incomplete
+  // and is found by the following poll (tags, as in the regular poll).
+  __shared__ uint64_t s_spec[kServerPoll][kServerHeadWords];
+  __shared__ uint64_t s_spec_seq;
+  __shared__ uint32_t s_spec_stop;
+  constexpr uint32_t kSpecThreads = kServerPoll * kServerHeadWords / 2 + 1;
+  constexpr uint32_t kSpecFirst = kServerThreads - kSpecThreads;
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   uint64_t t0 = 0, t_last = 0;  // thread 0 only
   if (tid == 0) {
     s_next = start_seq;
+    s_spec_seq = ~0ull;
     t0 = t_last = static_cast<uint64_t>(wall_clock64());
   }
   __syncthreads();
@@ -1778,16 +1788,24 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
     const uint64_t next = s_next;
     if (stamps != nullptr && tid == 0) st_t[0] = static_cast<uint64_t>(wall_clock64());
     // the poll: the first two lines of each of the next kServerPoll slots, 16 B a lane, and the
-    // host's stop word, all in one round trip
+    // host's stop word, all in one round trip -- or the words the previous batch's speculative
+    // poll read for this very seq
+    const bool spec = s_spec_seq == next;
     if (tid < kServerPoll * kServerHeadWords / 2) {
       const uint32_t i = tid / (kServerHeadWords / 2), piece = tid % (kServerHeadWords / 2);
-      const u64x2 v = sys_load_16(reinterpret_cast<const uint64_t*>(ring + (next + i) % kServerSlots) + 2 * piece);
-      s_head[i][2 * piece] = v.x;
-      s_head[i][2 * piece + 1] = v.y;
+      if (spec) {
+        s_head[i][2 * piece] = s_spec[i][2 * piece];
+        s_head[i][2 * piece + 1] = s_spec[i][2 * piece + 1];
+      } else {
+        const u64x2 v = sys_load_16(reinterpret_cast<const uint64_t*>(ring + (next + i) % kServerSlots) + 2 * piece);
+        s_head[i][2 * piece] = v.x;
+        s_head[i][2 * piece + 1] = v.y;
+      }
     } else if (tid == kServerPoll * kServerHeadWords / 2) {
-      s_stop = *reinterpret_cast<const volatile uint64_t*>(&ctl->stop) != 0 ? 1u : 0u;
+      s_stop = spec ? s_spec_stop : (*reinterpret_cast<const volatile uint64_t*>(&ctl->stop) != 0 ? 1u : 0u);
     }
     __syncthreads();
+    if (tid == 0) s_spec_seq = ~0ull;  // used once (read by every thread above, before the barrier)
     if (tid < 64) {
       const uint64_t seq = next + lane;
       const uint64_t tag = (seq / kServerSlots) & 0xFFu;
@@ -1839,6 +1857,19 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
       // PCIe read and the work step 2.8x slower (12.6 vs 4.5 us a batch).
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       if (stamps != nullptr && tid == 0) st_t[2] = static_cast<uint64_t>(wall_clock64());
+      // the speculative poll of the slots after this run, in flight with the packet loads
+      u64x2 sv = {0ull, 0ull};
+      if (spec_on && tid >= kSpecFirst) {
+        const uint32_t p = tid - kSpecFirst;
+        if (p < kSpecThreads - 1) {
+          const uint32_t i = p / (kServerHeadWords / 2), piece = p % (kServerHeadWords / 2);
+          sv = sys_load_16(reinterpret_cast<const uint64_t*>(ring + (next + n + i) % kServerSlots) + 2 * piece);
+        } else {
+          sv.x = __hip_atomic_load(reinterpret_cast<const __attribute__((address_space(1))) uint64_t*>(
+                                       reinterpret_cast<uintptr_t>(&ctl->stop)),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
       const uint32_t total = s_first[n];
       for (uint32_t w = tid; w < total; w += kServerThreads) {
         uint32_t i = 0;
@@ -1889,6 +1920,17 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
       // one caller 8.0 vs 10.9 us a call, 16 callers 550k vs 330k calls/s against plain stores
       // and a system release fence (its L2 write-back 1.7-2.9 us a batch).
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      if (spec_on && tid >= kSpecFirst) {
+        const uint32_t p = tid - kSpecFirst;
+        if (p < kSpecThreads - 1) {
+          const uint32_t i = p / (kServerHeadWords / 2), piece = p % (kServerHeadWords / 2);
+          s_spec[i][2 * piece] = sv.x;
+          s_spec[i][2 * piece + 1] = sv.y;
+        } else {
+          s_spec_stop = sv.x != 0 ? 1u : 0u;
+          s_spec_seq = next + n;
+        }
+      }
       if (stamps != nullptr && tid == 0) st_t[4] = static_cast<uint64_t>(wall_clock64());
       __syncthreads();
       if (tid < n) sys_store_relaxed(&done[(next + tid) % kServerSlots], next + tid + 1);
@@ -1910,7 +1952,8 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
         sys_store_release(&rec[7], ++st_batches);
         st_polls = 0;
       }
-    } else if (!leave) {
+    } else if (!leave && !spec) {
+      // (a speculative poll that found nothing new is followed by a real poll at once)
       __builtin_amdgcn_s_sleep(8);
     }
     __syncthreads();
@@ -2594,9 +2637,10 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
 }
 
 hipError_t launch_legacy_server(const ServerSlot* ring, uint64_t* done, ServerControl* ctl, uint64_t start_seq,
-                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks, uint64_t* stamps, hipStream_t s) {
+                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks, uint64_t* stamps, bool spec,
+                                hipStream_t s) {
   hipLaunchKernelGGL(legacy_server, dim3(1), dim3(kServerThreads), 0, s, ring, done, ctl, start_seq, gen, idle_ticks,
-                     life_ticks, stamps);
+                     life_ticks, stamps, spec ? 1u : 0u);
   return hipGetLastError();
 }
 

@@ -3,9 +3,9 @@
 set -e
 B=./quic-test_amd/lib/batcher_latency
 for s in 1 16; do
-  QUICFEC_RESIDENT_STAMPS=1 timeout -k 10 60 $B legacy $s 0 2 > gpurun_out/stampsB_$s.json 2> gpurun_out/stampsB_$s.err || [ $? -eq 1 ]
-  cat gpurun_out/stampsB_$s.json; grep resident_stamps gpurun_out/stampsB_$s.err || true
+  QUICFEC_RESIDENT_STAMPS=1 timeout -k 10 60 $B legacy $s 0 2 > gpurun_out/stampsC_$s.json 2> gpurun_out/stampsC_$s.err || [ $? -eq 1 ]
+  cat gpurun_out/stampsC_$s.json; grep resident_stamps gpurun_out/stampsC_$s.err || true
 done
-QUICFEC_RESIDENT_STAMPS=1 timeout -k 10 60 $B legacy_raw 20000 > gpurun_out/stampsB_raw.json 2> gpurun_out/stampsB_raw.err || [ $? -eq 1 ]
-cat gpurun_out/stampsB_raw.json; grep resident_stamps gpurun_out/stampsB_raw.err || true
-timeout -k 10 300 python -u -m pytest tests/test_gpu_coalesce.py -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/coalesceB.log 2>&1; tail -2 gpurun_out/coalesceB.log
+QUICFEC_RESIDENT_STAMPS=1 timeout -k 10 60 $B legacy_raw 20000 > gpurun_out/stampsC_raw.json 2> gpurun_out/stampsC_raw.err || [ $? -eq 1 ]
+cat gpurun_out/stampsC_raw.json; grep resident_stamps gpurun_out/stampsC_raw.err || true
+timeout -k 10 300 python -u -m pytest tests/test_gpu_coalesce.py -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/coalesceC.log 2>&1; tail -2 gpurun_out/coalesceC.log
