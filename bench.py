@@ -583,6 +583,9 @@ def parse_args(argv=None):
                          "C4 (k=20 r=5 encode) and C5 (satellite loss, device-resident and host-resident with "
                          "H2D/D2H); auto = on when N > 1")
     ap.add_argument("--leg-groups", type=int, default=0, help="groups per GPU of the legs (default: each config's)")
+    ap.add_argument("--e2e-groups", type=int, default=0,
+                    help="groups per rank of the host-resident legs (default: all at N = 1, 250k per rank at N > 1, "
+                         "so N ranks' page-locked buffers stay within one node's RAM)")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -889,7 +892,13 @@ class Bench:
                "verified": verified, "decode_api": api if cfg["decode"] else None,
                "kernels": kernels, "roofline": roofline, "workload_key": wl}
         if e2e:
-            res["e2e_pinned"] = e2e_pinned(ctx, data, parity, masks if cfg["decode"] else None, G, cfg)
+            # host-resident legs on the first Ge groups: the whole batch at N = 1 (15.6 GB page-locked
+            # at C5), --e2e-groups (default 250k, ~3.9 GB) per rank when N ranks share one node's RAM
+            Ge = min(G, args.e2e_groups if args.e2e_groups else (G if world == 1 else 250_000))
+            k_, r_, P_ = cfg["k"], cfg["r"], cfg["P"]
+            res["e2e_pinned"] = e2e_pinned(ctx, data[:Ge * k_ * P_], parity[:Ge * r_ * P_],
+                                           masks[:Ge] if cfg["decode"] else None, Ge, cfg)
+            res["e2e_pinned"]["groups_per_rank"] = Ge
         if os.environ.get("QUICFEC_BENCH_ADDRS") == "1":  # placement diagnostics (A/B runs)
             res["buffers"] = {n: hex(t.data_ptr()) for n, t in (("data", data), ("parity", parity), ("rebuilt", rebuilt))
                               if t is not None}
