@@ -268,8 +268,11 @@ const char* fec_batcher_last_error(void);
 /* ---- legacy-call coalescing (fec_coalesce.cpp) ----
  * Calls from page-locked slabs (fec_alloc_slab, as the Go wrapper packs them) of 1..8 groups
  * go to a resident encoder instead: one workgroup per device that stays launched while calls
- * keep coming and serves a ring of submission slots in page-locked memory, so a call costs no
- * kernel launch (QUICFEC_RESIDENT=0 turns it off).  The rest:
+ * keep coming and serves a ring of submission slots, so a call costs no kernel launch
+ * (QUICFEC_RESIDENT=0 turns it off).  On a large-BAR device the ring is in device memory the
+ * host writes directly (QUICFEC_RESIDENT_VRAM=0: page-locked host memory), and calls of at most
+ * 4 groups with packet_size <= 1536 and a multiple of 4 have their packets copied into their
+ * slot -- from any host memory, pageable slabs included.  The rest:
  * The reference's unchanged call site encodes one group per fec_encode_batch call, each stream
  * on its own context (encoder_hybrid.go:115 via fec_cgo.go:138, client.go:783).  Host-resident
  * legacy calls of at most QUICFEC_COALESCE_MAX_GROUPS groups (default 64) are joined, across
@@ -293,6 +296,8 @@ typedef struct {
   uint64_t resident_pre_ns;    /* sums over resident calls: entry until the slot was published, */
   uint64_t resident_wait_ns;   /*   published until its done word was seen, */
   uint64_t resident_post_ns;   /*   and from there to the return */
+  uint64_t resident_inline;    /* resident calls whose packets the host copied into the slot */
+  uint64_t resident_vram;      /* devices whose resident ring is in device memory (not reset) */
 } FECCoalesceStats;
 
 /* Process-wide totals over every device and packet size; reset = 1 zeroes them after the read. */

@@ -38,6 +38,13 @@
 // and polls the slot's done word; the workgroup takes every complete slot in order each time it
 // polls (one PCIe round trip reads the next 64 slots' headers and first groups), so concurrent
 // callers share one pass without any host-side batch.
+// VRAM ring (large-BAR devices, the default where setup_vram succeeds; QUICFEC_RESIDENT_VRAM=0
+// keeps the page-locked ring): the slots live in uncached device memory the host writes
+// through the BAR, and a call of <= 4 groups with P % 4 == 0 and P <= 1536 -- the Go wrapper's
+// (1 group, 1200 B) -- has its packets copied into its slot as lap-tagged 16-B chunks
+// (pack_inline).  The server's poll and packet loads are then device-local: the call's one
+// PCIe crossing each way is the host's stores and the device's repair-row stores.  Any slab
+// memory works for those calls, pageable included.
 // No kernel launch per call: the resident instance leaves after QUICFEC_RESIDENT_IDLE_US
 // (default 2000) without work or QUICFEC_RESIDENT_LIFE_US (default 50000) of life, and the next
 // caller that finds it gone (its `exited` word equals the instance's generation) launches the
@@ -383,6 +390,7 @@ bool alloc_coherent(Pinned& m, size_t bytes) {
 constexpr uint32_t kResidentOutBytes = 16u << 10;  // per slot: repair rows of callers whose buffer is pageable
 
 std::atomic<uint64_t> g_res_calls{0}, g_res_launches{0}, g_res_pre_ns{0}, g_res_wait_ns{0}, g_res_post_ns{0};
+std::atomic<uint64_t> g_res_inline{0}, g_res_vram{0};
 
 // The stream the resident instance runs on.  A persistent kernel occupies its hardware queue:
 // every later kernel on a stream that shares that queue waits until the instance leaves (up to
@@ -434,6 +442,8 @@ class Resident {
     if (!alloc_coherent(r->ring, sizeof(ServerSlot) * kServerSlots) ||
         !alloc_coherent(r->done, sizeof(uint64_t) * kServerSlots) || !alloc_coherent(r->ctl, sizeof(ServerControl)))
       return nullptr;
+    r->ring_w = reinterpret_cast<ServerSlot*>(r->ring.host);
+    r->ring_d = reinterpret_cast<const ServerSlot*>(r->ring.dev);
     r->deadline = std::chrono::milliseconds(std::max(1L, env_long("QUICFEC_RESIDENT_DEADLINE_MS", 10000)));
     // tests: an instance that never serves (relaunch records a launch without launching)
     r->no_launch = env_long("QUICFEC_RESIDENT_TEST_NOLAUNCH", 0) != 0;
@@ -446,6 +456,7 @@ class Resident {
     r->tick_khz = static_cast<uint64_t>(khz);
     // no word of a slot that was never written may carry lap 0's tag
     std::memset(r->ring.host, 0xFF, sizeof(ServerSlot) * kServerSlots);
+    if (env_long("QUICFEC_RESIDENT_VRAM", 1) != 0) r->setup_vram();
     r->collected.reset(new std::atomic<uint64_t>[kServerSlots]);
     for (uint32_t i = 0; i < kServerSlots; ++i) r->collected[i].store(0, std::memory_order_relaxed);
     return r.release();
@@ -467,10 +478,20 @@ class Resident {
   // runs the call on another path.
   static constexpr int kNotTaken = 1;
 
-  int encode(const uint8_t* slab_dev, const uint32_t* offsets, uint32_t G, uint32_t P, uint8_t* repair_out,
-             uint8_t* repair_dev, uint64_t t_enter) {
-    uint8_t* out_dev = nullptr;
+  // Whether a call of G groups of P bytes can have its packets copied into its slot (the VRAM
+  // ring): then the slab may be any host memory.
+  bool inlines(uint32_t G, uint32_t P) const {
+    return vinl != nullptr && G <= kInlineMaxGroups && P <= kInlineMaxP && P % 4 == 0;
+  }
+
+  // slab: the caller's slab; slab_dev: the device's address for it when it is page-locked, else
+  // nullptr (the call is then taken only with its packets inline).
+  int encode(const uint8_t* slab, const uint8_t* slab_dev, const uint32_t* offsets, uint32_t G, uint32_t P,
+             uint8_t* repair_out, uint8_t* repair_dev, uint64_t t_enter) {
     if (!repair_dev && !ensure_outs()) return kNotTaken;
+    // (outs slots are 16 KB apart: 4-aligned like the base)
+    const bool inline_pk = inlines(G, P) && (reinterpret_cast<uintptr_t>(repair_dev ? repair_dev : outs.dev) & 3u) == 0;
+    if (!inline_pk && slab_dev == nullptr) return kNotTaken;
     const uint64_t base = reinterpret_cast<uint64_t>(slab_dev);
     const uint64_t seq = next_seq.fetch_add(1, std::memory_order_relaxed);
     const uint32_t si = static_cast<uint32_t>(seq % kServerSlots);
@@ -494,16 +515,26 @@ class Resident {
       backoff(spins);
     }
     if (!usable()) return kNotTaken;
-    ServerSlot* sl = reinterpret_cast<ServerSlot*>(ring.host) + si;
-    out_dev = repair_dev ? repair_dev : outs.dev + size_t(si) * kResidentOutBytes;
-    // groups after the first, then the first group and the header: the device reads the former
-    // only after it has seen every word of the latter with this lap's tag
-    for (uint32_t i = kServerPackets; i < G * kServerPackets; ++i) sl->addr[i] = (base + offsets[i]) | tag;
-    std::atomic_thread_fence(std::memory_order_release);
-    for (uint32_t i = 0; i < kServerPackets; ++i) __atomic_store_n(&sl->addr[i], (base + offsets[i]) | tag, __ATOMIC_RELAXED);
-    __atomic_store_n(&sl->out, reinterpret_cast<uint64_t>(out_dev) | tag, __ATOMIC_RELAXED);
-    __atomic_store_n(&sl->shape, uint64_t(P) | (uint64_t(G) << 16) | tag, __ATOMIC_RELEASE);
+    ServerSlot* sl = ring_w + si;
+    uint8_t* const out_dev = repair_dev ? repair_dev : outs.dev + size_t(si) * kResidentOutBytes;
+    if (inline_pk) {
+      // the packets into the slot's data area (each chunk carries the lap), then the header
+      pack_inline(vinl + size_t(si) * kInlineSlotBytes, slab, offsets, G, P, static_cast<uint32_t>(seq / kServerSlots) + 1u);
+      __atomic_store_n(&sl->out, reinterpret_cast<uint64_t>(out_dev) | tag, __ATOMIC_RELAXED);
+      __atomic_store_n(&sl->shape, uint64_t(P) | (uint64_t(G) << 16) | kServerInline | tag, __ATOMIC_RELAXED);
+    } else {
+      // groups after the first, then the first group and the header: the device reads the former
+      // only after it has seen every word of the latter with this lap's tag
+      for (uint32_t i = kServerPackets; i < G * kServerPackets; ++i) sl->addr[i] = (base + offsets[i]) | tag;
+      std::atomic_thread_fence(std::memory_order_release);
+      for (uint32_t i = 0; i < kServerPackets; ++i) __atomic_store_n(&sl->addr[i], (base + offsets[i]) | tag, __ATOMIC_RELAXED);
+      __atomic_store_n(&sl->out, reinterpret_cast<uint64_t>(out_dev) | tag, __ATOMIC_RELAXED);
+      __atomic_store_n(&sl->shape, uint64_t(P) | (uint64_t(G) << 16) | tag, __ATOMIC_RELEASE);
+    }
+    // through the BAR the stores sit in write-combining buffers until a serialising fence (mfence)
+    if (vinl) std::atomic_thread_fence(std::memory_order_seq_cst);
     g_res_calls.fetch_add(1, std::memory_order_relaxed);
+    if (inline_pk) g_res_inline.fetch_add(1, std::memory_order_relaxed);
     const uint64_t t_pub = now_ns();
     int rc = FEC_OK;
     const auto t_fail = std::chrono::steady_clock::now() + deadline;
@@ -531,6 +562,7 @@ class Resident {
       // the device is hung, and the caller's buffers handed to this call must not be reused
       // (include/fec_xor_simd.h, fec_encode_batch).
       __atomic_store_n(&sl->shape, uint64_t(P) | tag, __ATOMIC_RELEASE);
+      if (vinl) std::atomic_thread_fence(std::memory_order_seq_cst);
       poison();
       const auto t_drain = std::chrono::steady_clock::now() + deadline;
       const ServerControl* c = reinterpret_cast<const ServerControl*>(ctl.host);
@@ -598,6 +630,91 @@ class Resident {
   bool no_launch = false;                     // QUICFEC_RESIDENT_TEST_NOLAUNCH
   bool spec = false;                          // QUICFEC_RESIDENT_SPEC
   std::atomic<bool> outs_ready{false};
+  // The slots as the host writes them and as the device reads them: the page-locked ring, or
+  // (setup_vram) one address for both, uncached device memory the host writes through the BAR.
+  ServerSlot* ring_w = nullptr;
+  const ServerSlot* ring_d = nullptr;
+  uint8_t* vinl = nullptr;  // VRAM ring: the slots' inline data areas (kInlineSlotBytes each)
+
+  // Moves the ring into VRAM when the host can store to device memory directly (a large-BAR
+  // device; profiles/r04_probe_vram_host.jsonl: a host -> VRAM -> device -> host round trip in
+  // 4.4 us, 8.1 us through page-locked memory).  Checked before it is used: the allocation must
+  // be mapped in this process (/proc/self/maps) and a host store must reach the device's copy.
+  // Any failure leaves the page-locked ring in place.  The device memory is never freed (like
+  // the rest of a Resident, it goes with the process).
+  void setup_vram() {
+    int large_bar = 0;
+    if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) != hipSuccess || !large_bar) {
+      (void)hipGetLastError();
+      return;
+    }
+    const size_t ring_bytes = sizeof(ServerSlot) * kServerSlots, inl_bytes = size_t(kInlineSlotBytes) * kServerSlots;
+    void *vr = nullptr, *vi = nullptr;
+    bool ok = hipExtMallocWithFlags(&vr, ring_bytes, hipDeviceMallocUncached) == hipSuccess &&
+              hipExtMallocWithFlags(&vi, inl_bytes, hipDeviceMallocUncached) == hipSuccess && host_mapped(vr, ring_bytes) &&
+              host_mapped(vi, inl_bytes);
+    if (ok) {
+      uint64_t probe[2] = {0x5EED0001CAFEF00Dull, 0x0123456789ABCDEFull}, back[2] = {0, 0};
+      std::memcpy(vr, probe, sizeof(probe));
+      std::atomic_thread_fence(std::memory_order_seq_cst);
+      ok = hipMemcpy(back, vr, sizeof(back), hipMemcpyDeviceToHost) == hipSuccess && std::memcmp(back, probe, sizeof(back)) == 0;
+    }
+    // no header word with lap 0's tag, no chunk with lap 0's word (lap + 1 = 1)
+    ok = ok && hipMemsetAsync(vr, 0xFF, ring_bytes, stream) == hipSuccess && hipMemsetAsync(vi, 0, inl_bytes, stream) == hipSuccess &&
+         hipStreamSynchronize(stream) == hipSuccess;
+    if (!ok) {
+      (void)hipGetLastError();
+      if (vr) (void)hipFree(vr);
+      if (vi) (void)hipFree(vi);
+      return;
+    }
+    ring_w = static_cast<ServerSlot*>(vr);
+    ring_d = static_cast<const ServerSlot*>(vr);
+    vinl = static_cast<uint8_t*>(vi);
+    g_res_vram.fetch_add(1, std::memory_order_relaxed);
+  }
+
+  // Whether [p, p + n) lies in one mapping of this process's address space.
+  static bool host_mapped(const void* p, size_t n) {
+    FILE* f = std::fopen("/proc/self/maps", "r");
+    if (!f) return false;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    bool found = false;
+    char line[512];
+    while (!found && std::fgets(line, sizeof(line), f)) {
+      unsigned long lo = 0, hi = 0;
+      if (std::sscanf(line, "%lx-%lx", &lo, &hi) == 2 && a >= lo && a + n <= hi) found = true;
+    }
+    std::fclose(f);
+    return found;
+  }
+
+  // An inline slot's packets into its data area through the BAR (fec_kernels.hpp kServerInline):
+  // packet p = g * 10 + j as nch 16-B chunks, payload bytes [12c, 12c + 12) and lap1 in the
+  // fourth word; each chunk one 16-B store (write-combined).
+  static void pack_inline(uint8_t* area, const uint8_t* slab, const uint32_t* offsets, uint32_t G, uint32_t P,
+                          uint32_t lap1) {
+    typedef uint32_t v4u __attribute__((vector_size(16)));
+    const uint32_t nch = (P + kInlinePayload - 1) / kInlinePayload;
+    const uint32_t nfast = P >= 16 ? (P - 16) / kInlinePayload + 1 : 0;  // chunks whose 16-B read stays in the packet
+    for (uint32_t p = 0; p < G * kServerPackets; ++p) {
+      const uint8_t* src = slab + offsets[p];
+      volatile v4u* dst = reinterpret_cast<volatile v4u*>(area + size_t(p) * nch * 16);
+      uint32_t c = 0;
+      for (; c < nfast; ++c) {
+        v4u v;
+        std::memcpy(&v, src + size_t(c) * kInlinePayload, 16);
+        v[3] = lap1;
+        dst[c] = v;
+      }
+      for (; c < nch; ++c) {
+        v4u v = {0u, 0u, 0u, 0u};
+        std::memcpy(&v, src + size_t(c) * kInlinePayload, std::min(kInlinePayload, P - c * kInlinePayload));
+        v[3] = lap1;
+        dst[c] = v;
+      }
+    }
+  }
 
   void poison() {
     broken.store(true, std::memory_order_release);
@@ -643,8 +760,7 @@ class Resident {
       return FEC_OK;
     }
     BindDevice bd(device);
-    const hipError_t e = bd.ok ? launch_legacy_server(reinterpret_cast<const ServerSlot*>(ring.dev),
-                                                      reinterpret_cast<uint64_t*>(done.dev),
+    const hipError_t e = bd.ok ? launch_legacy_server(ring_d, vinl, reinterpret_cast<uint64_t*>(done.dev),
                                                       reinterpret_cast<ServerControl*>(ctl.dev), start, g, idle_ticks,
                                                       life_ticks, stamps.host ? reinterpret_cast<uint64_t*>(stamps.dev) : nullptr,
                                                       spec, stream)
@@ -736,13 +852,16 @@ bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* off
   if (sm == HostMem::kDevice || rm == HostMem::kDevice || classify_host_pointer(offsets, nullptr) == HostMem::kDevice)
     return false;  // device-resident callers batch by themselves
   const bool repair_pinned = rm == HostMem::kPinned;
-  if (sm == HostMem::kPinned && env_long("QUICFEC_RESIDENT", 1) != 0 && Resident::fits(num_groups, packet_size, repair_pinned) &&
-      reinterpret_cast<uint64_t>(sdev) + 0xFFFFFFFFull + packet_size <= kServerAddrMask &&
+  // The resident encoder: packets addressed in the caller's page-locked slab, or (VRAM ring)
+  // copied into the slot from any host memory.
+  const bool slab_addressable =
+      sm == HostMem::kPinned && reinterpret_cast<uint64_t>(sdev) + 0xFFFFFFFFull + packet_size <= kServerAddrMask;
+  if (env_long("QUICFEC_RESIDENT", 1) != 0 && Resident::fits(num_groups, packet_size, repair_pinned) &&
       reinterpret_cast<uint64_t>(rdev) <= kServerAddrMask) {
     Resident* r = resident_for(device);
-    if (r && r->usable()) {
-      const int res = r->encode(static_cast<const uint8_t*>(sdev), offsets, num_groups, packet_size, repair_out,
-                                repair_pinned ? static_cast<uint8_t*>(rdev) : nullptr, t_enter);
+    if (r && r->usable() && (slab_addressable || r->inlines(num_groups, packet_size))) {
+      const int res = r->encode(slab, slab_addressable ? static_cast<const uint8_t*>(sdev) : nullptr, offsets, num_groups,
+                                packet_size, repair_out, repair_pinned ? static_cast<uint8_t*>(rdev) : nullptr, t_enter);
       if (res != Resident::kNotTaken) {
         *rc = res;
         return true;
@@ -777,12 +896,15 @@ QFEC_EXPORT int fec_coalesce_stats(FECCoalesceStats* out, int reset) {
   out->resident_pre_ns = g_res_pre_ns.load();
   out->resident_wait_ns = g_res_wait_ns.load();
   out->resident_post_ns = g_res_post_ns.load();
+  out->resident_inline = g_res_inline.load();
+  out->resident_vram = g_res_vram.load();
   if (reset) {
     g_res_calls = 0;
     g_res_launches = 0;
     g_res_pre_ns = 0;
     g_res_wait_ns = 0;
     g_res_post_ns = 0;
+    g_res_inline = 0;
     g_close_ns = 0;
     g_launch_ns = 0;
     g_done_ns = 0;

@@ -1753,7 +1753,21 @@ __device__ __forceinline__ u64x2 sys_load_16(const uint64_t* p) {
   return *reinterpret_cast<const volatile __attribute__((address_space(1))) u64x2*>(reinterpret_cast<uintptr_t>(p));
 }
 
+// A 32-bit word to host memory, system-coherent, no wait after it (a volatile store would be
+// followed by one: a PCIe acknowledgement apiece).
+__device__ __forceinline__ void sys_store_32(uint8_t* p, uint32_t v) {
+  __hip_atomic_store(reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(p)), v,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The VRAM ring (inl != nullptr, fec_kernels.hpp kServerInline): the poll reads the slots from
+// device memory -- local, not a PCIe round trip -- and an inline slot's work item is one 16-B
+// chunk column (g, c): its 10 chunks loaded from the slot's data area, their lap words checked,
+// the 12 payload bytes XORed and stored as three 32-bit words.  A chunk whose lap word is not
+// yet this slot's (the host's stores through the BAR landed in another order) marks the slot
+// bad: the run is served up to the first bad slot and the poll comes back for the rest.
 __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot* __restrict__ ring,
+                                                                const uint8_t* __restrict__ inl,
                                                                 uint64_t* __restrict__ done,
                                                                 ServerControl* __restrict__ ctl, uint64_t start_seq,
                                                                 uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
@@ -1761,7 +1775,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
   __shared__ uint64_t s_next;
   __shared__ uint32_t s_n, s_exit, s_stop;
   __shared__ uint32_t s_first[kServerPoll + 1];  // work items before slot i of the run
-  __shared__ uint32_t s_P[kServerPoll], s_cpp[kServerPoll];
+  __shared__ uint32_t s_P[kServerPoll], s_cpp[kServerPoll], s_inl[kServerPoll], s_bad[kServerPoll];
   __shared__ uint64_t s_head[kServerPoll][kServerHeadWords];  // out, shape, addr[0..13] (tagged)
   // The speculative poll: while a batch is being served, the last kSpecThreads threads read the
   // slots after it (and the stop word); the next iteration uses those words instead of polling
@@ -1802,7 +1816,11 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
         s_head[i][2 * piece + 1] = v.y;
       }
     } else if (tid == kServerPoll * kServerHeadWords / 2) {
-      s_stop = spec ? s_spec_stop : (*reinterpret_cast<const volatile uint64_t*>(&ctl->stop) != 0 ? 1u : 0u);
+      // with the ring in VRAM the stop word (host memory) would make every poll a PCIe round
+      // trip again: every 16th poll reads it (the idle and life bounds hold regardless)
+      s_stop = spec ? s_spec_stop
+               : (inl == nullptr || (it & 15u) == 0) ? (*reinterpret_cast<const volatile uint64_t*>(&ctl->stop) != 0 ? 1u : 0u)
+                                                     : 0u;
     }
     __syncthreads();
     if (tid == 0) s_spec_seq = ~0ull;  // used once (read by every thread above, before the barrier)
@@ -1810,10 +1828,14 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
       const uint64_t seq = next + lane;
       const uint64_t tag = (seq / kServerSlots) & 0xFFu;
       bool ok = lane < kServerPoll;
+      bool inline_slot = false;
       if (ok) {
-        // out, shape and the first group's 10 addresses (words 0 .. 11)
+        // out, shape and (unless the packets are inline) the first group's 10 addresses (words 0 .. 11)
+        inline_slot = inl != nullptr && (s_head[lane][1] & kServerInline) != 0;
+        const uint32_t nw = inline_slot ? 2u : 2u + kServerPackets;
 #pragma unroll
-        for (uint32_t w = 0; w < 2 + kServerPackets; ++w) ok = ok && (s_head[lane][w] >> kServerTagShift) == tag;
+        for (uint32_t w = 0; w < 2 + kServerPackets; ++w) ok = ok && (w >= nw || (s_head[lane][w] >> kServerTagShift) == tag);
+        s_bad[lane] = 0;
       }
       const uint64_t bal = __ballot(ok);
       const uint32_t n = ~bal == 0 ? 64u : static_cast<uint32_t>(__builtin_ctzll(~bal));
@@ -1821,10 +1843,12 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
       if (lane < n) {
         const uint64_t sh = s_head[lane][1];
         const uint32_t P = static_cast<uint32_t>(sh & 0xFFFFu), G = static_cast<uint32_t>((sh >> 16) & 0xFFu);
-        const uint32_t cpp = (P + 15u) / 16u;
+        const uint32_t cpp = inline_slot ? (P + kInlinePayload - 1u) / kInlinePayload : (P + 15u) / 16u;
         s_P[lane] = P;
         s_cpp[lane] = cpp;
-        work = G * cpp;
+        s_inl[lane] = inline_slot ? 1u : 0u;
+        // (an inline shape past the data area is never written by the host: nothing is read for it)
+        work = inline_slot && (G > kInlineMaxGroups || P > kInlineMaxP) ? 0u : G * cpp;
       }
       uint32_t incl = work;
 #pragma unroll
@@ -1877,6 +1901,37 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
         const uint32_t local = w - s_first[i];
         const uint32_t cpp = s_cpp[i], P = s_P[i];
         const uint32_t g = local / cpp, col = local - g * cpp;
+        if (s_inl[i] != 0) {
+          const uint64_t seq = next + i;
+          const uint8_t* src = inl + static_cast<uint64_t>(seq % kServerSlots) * kInlineSlotBytes +
+                               (static_cast<uint64_t>(g) * kServerPackets * cpp + col) * 16u;
+          u32x4 v[kServerPackets];
+#pragma unroll
+          for (uint32_t j = 0; j < kServerPackets; ++j)
+            v[j] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(
+                reinterpret_cast<uintptr_t>(src + static_cast<uint64_t>(j) * cpp * 16u));
+#pragma unroll
+          for (uint32_t j = 0; j < kServerPackets; ++j) __asm__ volatile("" : "+v"(v[j]));
+          const uint32_t lap1 = static_cast<uint32_t>(seq / kServerSlots) + 1u;
+          bool fresh = true;
+          u32x4 acc = v[0];
+#pragma unroll
+          for (uint32_t j = 0; j < kServerPackets; ++j) fresh = fresh && v[j].w == lap1;
+#pragma unroll
+          for (uint32_t j = 1; j < kServerPackets; ++j) acc ^= v[j];
+          if (!fresh) {
+            s_bad[i] = 1u;
+            continue;
+          }
+          if (stamps != nullptr && tid == 0 && w == 0) st_t[6] = static_cast<uint64_t>(wall_clock64());
+          uint8_t* dst = reinterpret_cast<uint8_t*>(s_head[i][0] & kServerAddrMask) + static_cast<uint64_t>(g) * P +
+                         col * kInlinePayload;
+          const uint32_t rem = P - col * kInlinePayload;  // whole words (the host inlines P % 4 == 0 only)
+          sys_store_32(dst, acc.x);
+          if (rem > 4u) sys_store_32(dst + 4, acc.y);
+          if (rem > 8u) sys_store_32(dst + 8, acc.z);
+          continue;
+        }
         const uint32_t coff = col * 16u + 16u <= P ? col * 16u : P - 16u;
         uint64_t ad[kServerPackets];
         if (g == 0) {
@@ -1892,6 +1947,16 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
             ad[j] = __hip_atomic_load(reinterpret_cast<const __attribute__((address_space(1))) uint64_t*>(
                                           reinterpret_cast<uintptr_t>(src + j)),
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          // tagged like the header: in a VRAM ring the host's stores through the BAR carry no
+          // order, and a word of the previous lap marks the slot bad (served by a later poll)
+          const uint64_t tag = ((next + i) / kServerSlots) & 0xFFu;
+          bool fresh = true;
+#pragma unroll
+          for (uint32_t j = 0; j < kServerPackets; ++j) fresh = fresh && (ad[j] >> kServerTagShift) == tag;
+          if (!fresh) {
+            s_bad[i] = 1u;
+            continue;
+          }
         }
         // All ten packet loads in flight at once, as global (address space 1) loads: the addresses
         // come from integers, so plain pointers compile to flat loads, which count on lgkmcnt too
@@ -1933,10 +1998,19 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
       }
       if (stamps != nullptr && tid == 0) st_t[4] = static_cast<uint64_t>(wall_clock64());
       __syncthreads();
-      if (tid < n) sys_store_relaxed(&done[(next + tid) % kServerSlots], next + tid + 1);
+      // the run up to its first slot with a chunk not yet landed (VRAM ring; n in any other case)
+      uint32_t n_ok = n;
+      if (tid < 64) {
+        for (uint32_t k = 0; k < n; ++k)
+          if (s_bad[k] != 0) {
+            n_ok = k;
+            break;
+          }
+      }
+      if (tid < n_ok) sys_store_relaxed(&done[(next + tid) % kServerSlots], next + tid + 1);
       if (tid == 0) {
-        s_next = next + n;
-        sys_store_relaxed(&ctl->progress, next + n);
+        s_next = next + n_ok;
+        sys_store_relaxed(&ctl->progress, next + n_ok);
       }
       if (stamps != nullptr && tid == 0) {
         st_t[5] = static_cast<uint64_t>(wall_clock64());
@@ -2636,11 +2710,11 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
   return hipSuccess;
 }
 
-hipError_t launch_legacy_server(const ServerSlot* ring, uint64_t* done, ServerControl* ctl, uint64_t start_seq,
-                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks, uint64_t* stamps, bool spec,
-                                hipStream_t s) {
-  hipLaunchKernelGGL(legacy_server, dim3(1), dim3(kServerThreads), 0, s, ring, done, ctl, start_seq, gen, idle_ticks,
-                     life_ticks, stamps, spec ? 1u : 0u);
+hipError_t launch_legacy_server(const ServerSlot* ring, const uint8_t* inl, uint64_t* done, ServerControl* ctl,
+                                uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+                                uint64_t* stamps, bool spec, hipStream_t s) {
+  hipLaunchKernelGGL(legacy_server, dim3(1), dim3(kServerThreads), 0, s, ring, inl, done, ctl, start_seq, gen,
+                     idle_ticks, life_ticks, stamps, spec ? 1u : 0u);
   return hipGetLastError();
 }
 

@@ -167,9 +167,22 @@ constexpr uint64_t kServerTagShift = 56;  // addresses below 2^56 (user virtual 
 constexpr uint64_t kServerAddrMask = (1ull << kServerTagShift) - 1;
 struct alignas(64) ServerSlot {
   uint64_t out;             // tag | device address of the repair rows, row g at out + g * P
-  uint64_t shape;           // tag | P (bits 0..15) | groups (bits 16..23; 0 = nothing to do)
+  uint64_t shape;           // tag | P (bits 0..15) | groups (bits 16..23; 0 = nothing to do) | kServerInline
   uint64_t addr[kServerMaxGroups * kServerPackets];  // tag | device address of packet (g, j) at [g * 10 + j]
 };
+// VRAM ring (large-BAR devices, fec_coalesce.cpp Resident): the slots and the packets of small
+// calls live in uncached device memory that the host writes through the BAR, so the server's
+// poll and packet loads stay on the device.  An inline slot (shape bit kServerInline) carries
+// no addresses: its packets are copied by the host into the slot's data area, packet (g, j) as
+// chunks of 16 B -- 12 payload bytes (payload bytes [12c, 12c + 12) at chunk c, zero past P)
+// and, in the fourth 32-bit word, the slot's lap + 1 -- at chunk (g * 10 + j) * nch + c,
+// nch = ceil(P / 12).  Every chunk is self-validating like the header words: no ordering of the
+// host's stores through the BAR is assumed.
+constexpr uint64_t kServerInline = 1ull << 24;
+constexpr uint32_t kInlineMaxGroups = 4;
+constexpr uint32_t kInlineMaxP = 1536;
+constexpr uint32_t kInlinePayload = 12;  // payload bytes of a 16-B chunk
+constexpr uint32_t kInlineSlotBytes = kInlineMaxGroups * kServerPackets * (kInlineMaxP / kInlinePayload) * 16;
 struct alignas(64) ServerControl {
   uint64_t stop;            // host -> device: leave at the next poll
   uint64_t pad0[7];
@@ -182,9 +195,11 @@ struct alignas(64) ServerControl {
 // host sets ctl->stop; on leaving it stores progress and then exited = gen.
 // stamps: nullptr, or 256 x 8 words of host memory for the diagnostic phase stamps (QUICFEC_RESIDENT_STAMPS).
 // spec: speculative poll (the slots after a batch read while it is served; QUICFEC_RESIDENT_SPEC).
-hipError_t launch_legacy_server(const ServerSlot* ring, uint64_t* done, ServerControl* ctl, uint64_t start_seq,
-                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks, uint64_t* stamps, bool spec,
-                                hipStream_t s);
+// inl: the inline data areas (kInlineSlotBytes per slot) when the ring is in VRAM, else nullptr;
+// then the host's stop word (host memory) is read by every 16th poll only, not every poll.
+hipError_t launch_legacy_server(const ServerSlot* ring, const uint8_t* inl, uint64_t* done, ServerControl* ctl,
+                                uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+                                uint64_t* stamps, bool spec, hipStream_t s);
 
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);

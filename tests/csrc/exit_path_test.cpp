@@ -11,8 +11,14 @@
 // dlsym(RTLD_NEXT)), and counts the calls that come FROM libfec_hip.so (dladdr of the return
 // address) after an atexit hook registered behind the library's has run.
 //
-//   exit_path_test [resident|coalescer|pageable|nolaunch] [calls]
-//   -> one JSON line at exit: {"mode", "calls", "repairs_ok", "first_rc", "calls_after_exit", "names"}
+// The mixed modes cycle through shapes on both sides of the VRAM ring's inline bounds (1..8
+// groups, P 16..2048, odd P, scattered offsets) over page-locked and pageable slabs and repair
+// buffers; the *hostring modes keep the resident ring in page-locked host memory
+// (QUICFEC_RESIDENT_VRAM=0: the ring kind is fixed per process).
+//
+//   exit_path_test [resident|hostring|coalescer|pageable|nolaunch|mixed|mixed_hostring] [calls]
+//   -> one JSON line at exit: {"mode", "calls", "repairs_ok", "first_rc", "calls_after_exit", "names",
+//                              "resident_calls", "resident_inline", "resident_vram"}
 // Built by quic-test_amd/csrc/Makefile (target tests); run by tests/test_gpu_coalesce.py.
 #include <dlfcn.h>
 
@@ -37,6 +43,7 @@ std::mutex g_mu;
 std::string g_names;
 std::string g_mode = "resident";
 int g_calls = 0, g_first_rc = 0;
+unsigned long long g_resident_calls = 0, g_resident_inline = 0, g_resident_vram = 0;
 bool g_ok = true;
 
 bool from_library(void* ret) {
@@ -60,8 +67,9 @@ void mark_exit() { g_exiting.store(true, std::memory_order_release); }
 
 void report() {
   std::printf("{\"mode\": \"%s\", \"calls\": %d, \"repairs_ok\": %s, \"first_rc\": %d, \"calls_after_exit\": %d, "
-              "\"names\": \"%s\"}\n",
-              g_mode.c_str(), g_calls, g_ok ? "true" : "false", g_first_rc, g_after.load(), g_names.c_str());
+              "\"names\": \"%s\", \"resident_calls\": %llu, \"resident_inline\": %llu, \"resident_vram\": %llu}\n",
+              g_mode.c_str(), g_calls, g_ok ? "true" : "false", g_first_rc, g_after.load(), g_names.c_str(), g_resident_calls,
+              g_resident_inline, g_resident_vram);
   std::fflush(stdout);
 }
 
@@ -93,7 +101,9 @@ int main(int argc, char** argv) {
   std::atexit(report);  // first registered: runs last
   if (argc > 1) g_mode = argv[1];
   const int calls = argc > 2 ? std::atoi(argv[2]) : 200;
+  const bool mixed = g_mode.rfind("mixed", 0) == 0;
   if (g_mode == "coalescer") setenv("QUICFEC_RESIDENT", "0", 1);
+  if (g_mode == "hostring" || g_mode == "mixed_hostring") setenv("QUICFEC_RESIDENT_VRAM", "0", 1);
   if (g_mode == "nolaunch") {
     setenv("QUICFEC_RESIDENT_TEST_NOLAUNCH", "1", 1);
     setenv("QUICFEC_RESIDENT_DEADLINE_MS", "200", 1);
@@ -103,24 +113,37 @@ int main(int argc, char** argv) {
     std::printf("{\"skip\": \"no GPU\"}\n");
     return 0;
   }
-  constexpr uint32_t P = 1200, K = 10;
+  constexpr uint32_t K = 10, kMaxG = 8, kMaxP = 2048, kSlab = kMaxG * K * kMaxP + 4096;
+  // mixed: shapes on both sides of the inline bounds (<= 4 groups, P % 4 == 0, P <= 1536)
+  static const uint32_t kShapes[][2] = {{1, 1200}, {4, 1536}, {2, 16}, {3, 100}, {1, 1201}, {5, 1200},
+                                        {8, 1500}, {1, 2048}, {4, 20}, {2, 1538}, {1, 1500}, {6, 333}};
   const bool pageable = g_mode == "pageable";
-  uint8_t* slab = static_cast<uint8_t*>(pageable ? std::malloc(K * P) : fec_alloc_slab(K * P));
-  uint8_t* repair = static_cast<uint8_t*>(pageable ? std::malloc(P) : fec_alloc_repair_buffer(P));
-  uint32_t offsets[K];
-  for (uint32_t j = 0; j < K; ++j) offsets[j] = j * P;
+  uint8_t* slab_pin = static_cast<uint8_t*>(fec_alloc_slab(kSlab));
+  uint8_t* rep_pin = static_cast<uint8_t*>(fec_alloc_repair_buffer(kMaxG * kMaxP));
+  uint8_t* slab_pg = static_cast<uint8_t*>(std::malloc(kSlab));
+  uint8_t* rep_pg = static_cast<uint8_t*>(std::malloc(kMaxG * kMaxP));
+  uint32_t offsets[kMaxG * K];
   uint64_t x = 0x5EED0000u;
-  std::vector<uint8_t> want(P);
+  auto rnd = [&x] {
+    x = x * 6364136223846793005ull + 1442695040888963407ull;
+    return static_cast<uint32_t>(x >> 33);
+  };
+  std::vector<uint8_t> want(kMaxG * kMaxP);
   for (int c = 0; c < calls; ++c) {
-    for (uint32_t i = 0; i < K * P; ++i) {
-      x = x * 6364136223846793005ull + 1442695040888963407ull;
-      slab[i] = static_cast<uint8_t>(x >> 56);
+    const uint32_t G = mixed ? kShapes[c % 12][0] : 1, P = mixed ? kShapes[c % 12][1] : 1200;
+    uint8_t* slab = (mixed ? (c / 12) % 2 == 1 : pageable) ? slab_pg : slab_pin;
+    uint8_t* repair = (mixed ? (c / 24) % 2 == 1 : pageable) ? rep_pg : rep_pin;
+    for (uint32_t i = 0; i < G * K; ++i) offsets[i] = mixed ? rnd() % (kSlab - P + 1) : i * P;
+    for (uint32_t i = 0; i < kSlab; i += 4) {
+      const uint32_t v = rnd();
+      std::memcpy(slab + i, &v, 4);
     }
     std::fill(want.begin(), want.end(), 0);
-    for (uint32_t j = 0; j < K; ++j)
-      for (uint32_t i = 0; i < P; ++i) want[i] ^= slab[offsets[j] + i];
-    std::memset(repair, 0, P);
-    const int rc = fec_encode_batch(ctx, slab, offsets, 1, P, repair);
+    for (uint32_t g = 0; g < G; ++g)
+      for (uint32_t j = 0; j < K; ++j)
+        for (uint32_t i = 0; i < P; ++i) want[g * P + i] ^= slab[offsets[g * K + j] + i];
+    std::memset(repair, 0xEE, G * P);
+    const int rc = fec_encode_batch(ctx, slab, offsets, G, P, repair);
     if (c == 0) g_first_rc = rc;
     if (g_mode == "nolaunch" && c == 0) {
       // the never-serving instance: this call fails (bounded by the deadline), nothing hangs
@@ -128,9 +151,14 @@ int main(int argc, char** argv) {
       ++g_calls;
       continue;
     }
-    if (rc != 0 || std::memcmp(repair, want.data(), P) != 0) g_ok = false;
+    if (rc != 0 || std::memcmp(repair, want.data(), size_t(G) * P) != 0) g_ok = false;
     ++g_calls;
   }
+  FECCoalesceStats st{};
+  fec_coalesce_stats(&st, 0);
+  g_resident_calls = st.resident_calls;
+  g_resident_inline = st.resident_inline;
+  g_resident_vram = st.resident_vram;
   std::atexit(mark_exit);  // registered after the library's shutdown_all: runs before it
-  return 0;               // encoders, slab and repair buffer stay alive (a Go process exiting)
+  return 0;               // encoders, slabs and repair buffers stay alive (a Go process exiting)
 }

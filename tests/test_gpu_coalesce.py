@@ -49,8 +49,9 @@ def _run_threads(n, fn):
 def test_concurrent_one_group_calls_match_reference(quicfec_mod, oracle_mod, xor_golden, manifest, pinned, resident,
                                                     monkeypatch):
     """16 streams, each with its own context (the Go wrapper's FECEncoderCXX), 1 group per call:
-    page-locked slabs go to the resident encoder (QUICFEC_RESIDENT=0: shared launches),
-    pageable ones to shared launches."""
+    page-locked slabs go to the resident encoder (QUICFEC_RESIDENT=0: shared launches);
+    pageable ones too when its ring is in device memory (the packets copied into the slot),
+    else to shared launches."""
     monkeypatch.setenv("QUICFEC_COALESCE", "1")
     monkeypatch.setenv("QUICFEC_RESIDENT", "1" if resident else "0")
     c = next(c for c in manifest["cases"] if c["name"] == "batch_k10_p1200_g64")
@@ -89,11 +90,14 @@ def test_concurrent_one_group_calls_match_reference(quicfec_mod, oracle_mod, xor
 
     _run_threads(S, stream)
     st = quicfec_mod.coalesce_stats()
-    if pinned and resident:
+    vram = st["resident_vram"] > 0
+    if resident and (pinned or vram):
         # every call served by the resident encoder (the ring of 1024 slots wrapped), a
-        # launch only when no instance was running
+        # launch only when no instance was running; in a VRAM ring every call (1 group,
+        # 1200 B) has its packets inline
         assert st["resident_calls"] == S * CALLS and st["calls"] == 0, st
         assert 1 <= st["resident_launches"] < S * CALLS // 8, st
+        assert st["resident_inline"] == (S * CALLS if vram else 0), st
     else:
         assert st["calls"] == S * CALLS and st["groups"] == S * CALLS
         # calls from different contexts shared launches
@@ -178,7 +182,10 @@ def test_large_and_device_calls_bypass(gpu_ctx, oracle_mod, quicfec_mod, torch_c
     rep4 = np.zeros(4 * P, dtype=np.uint8)
     assert gpu_ctx.encode_batch_legacy(slab, offs, 4, P, rep4) == 0
     assert np.array_equal(rep4, exp[:4 * P])
-    assert quicfec_mod.coalesce_stats()["calls"] == 1
+    st = quicfec_mod.coalesce_stats()
+    # shared launches, or (VRAM ring: 4 groups of 300 B go inline) the resident encoder
+    assert st["calls"] + st["resident_calls"] == 1
+    assert st["resident_calls"] == (1 if st["resident_vram"] else 0), st
 
 
 def test_resident_encoder_leaves_when_idle_and_comes_back(quicfec_mod, oracle_mod, monkeypatch):
@@ -372,7 +379,7 @@ def _exit_path_run(mode, calls=300):
     return json.loads(lines[-1])
 
 
-@pytest.mark.parametrize("mode", ["resident", "coalescer", "pageable"])
+@pytest.mark.parametrize("mode", ["resident", "hostring", "coalescer", "pageable"])
 def test_exit_makes_no_hip_call(mode):
     """A process that made legacy calls on each path (resident encoder, shared launches,
     pageable slab + repair buffer) and returns from main with its encoders alive exits with no
@@ -398,3 +405,26 @@ def test_never_serving_resident_poisons_itself():
     assert rec["first_rc"] == -2                        # FEC_ERR_HIP
     assert rec["repairs_ok"] is True and rec["calls"] == 1_500
     assert rec["calls_after_exit"] == 0, rec["names"]
+
+
+@pytest.mark.parametrize("mode", ["mixed", "mixed_hostring"])
+def test_resident_ring_kinds_mixed_shapes(mode):
+    """Both resident ring kinds, each in a process of its own (the kind is fixed per process):
+    360 calls cycling through shapes on both sides of the VRAM ring's inline bounds (1..8
+    groups; P 16, 20, 100, 333, 1200, 1201, 1500, 1536, 1538, 2048; scattered offsets) over
+    page-locked and pageable slabs and repair buffers -- every repair row checked against the
+    XOR on the CPU.  In the VRAM ring the inline calls take the resident path from pageable
+    slabs too; in the page-locked ring none is inline."""
+    rec = _exit_path_run(mode, calls=360)
+    if "skip" in rec:
+        pytest.skip(rec["skip"])
+    assert rec["repairs_ok"] is True and rec["calls"] == 360, rec
+    assert rec["calls_after_exit"] == 0, rec["names"]
+    assert rec["resident_calls"] > 0, rec
+    if mode == "mixed_hostring":
+        assert rec["resident_vram"] == 0 and rec["resident_inline"] == 0, rec
+    elif rec["resident_vram"]:
+        # inline shapes: (1,1200) (4,1536) (2,16) (3,100) (4,20) (1,1500) -- 6 of every 12 calls,
+        # whatever the slab; page-locked slabs add the rest of the <= 8-group shapes
+        assert rec["resident_inline"] == 180, rec
+        assert rec["resident_calls"] > rec["resident_inline"], rec
