@@ -451,7 +451,7 @@ class Resident {
     // (profiles/r04_resident_spec_ab.jsonl), back-to-back single calls 6.9-7.3 vs 8.0-8.1 us,
     // 8 and 16 streams level within the noise, 4 streams 15-18% slower (batches split: slots
     // arriving after the speculative read wait for a batch of their own).  QUICFEC_RESIDENT_SPEC=1.
-    r->spec = env_long("QUICFEC_RESIDENT_SPEC", 0) != 0;
+    if (env_long("QUICFEC_RESIDENT_SPEC", 0) != 0) r->flags |= kServerFlagSpec;
     if (env_long("QUICFEC_RESIDENT_STAMPS", 0) != 0 && !alloc_coherent(r->stamps, 256 * 8 * sizeof(uint64_t))) return nullptr;
     r->tick_khz = static_cast<uint64_t>(khz);
     // no word of a slot that was never written may carry lap 0's tag
@@ -628,7 +628,7 @@ class Resident {
   std::atomic<bool> broken{false};
   std::chrono::milliseconds deadline{10000};  // QUICFEC_RESIDENT_DEADLINE_MS
   bool no_launch = false;                     // QUICFEC_RESIDENT_TEST_NOLAUNCH
-  bool spec = false;                          // QUICFEC_RESIDENT_SPEC
+  uint32_t flags = 0;                         // legacy_server flags (QUICFEC_RESIDENT_SPEC)
   std::atomic<bool> outs_ready{false};
   // The slots as the host writes them and as the device reads them: the page-locked ring, or
   // (setup_vram) one address for both, uncached device memory the host writes through the BAR.
@@ -763,7 +763,7 @@ class Resident {
     const hipError_t e = bd.ok ? launch_legacy_server(ring_d, vinl, reinterpret_cast<uint64_t*>(done.dev),
                                                       reinterpret_cast<ServerControl*>(ctl.dev), start, g, idle_ticks,
                                                       life_ticks, stamps.host ? reinterpret_cast<uint64_t*>(stamps.dev) : nullptr,
-                                                      spec, stream)
+                                                      flags, stream)
                                : hipErrorInvalidDevice;
     if (e != hipSuccess) {
       (void)hipGetLastError();

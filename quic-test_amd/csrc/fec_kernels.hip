@@ -1754,10 +1754,23 @@ __device__ __forceinline__ u64x2 sys_load_16(const uint64_t* p) {
 }
 
 // A 32-bit word to host memory, system-coherent, no wait after it (a volatile store would be
-// followed by one: a PCIe acknowledgement apiece).
+// followed by one: a PCIe acknowledgement apiece).  Only for a lone word (a row's last chunk).
 __device__ __forceinline__ void sys_store_32(uint8_t* p, uint32_t v) {
   __hip_atomic_store(reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(p)), v,
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// 12 bytes to host memory in one vector store, system-coherent (sc0 sc1 as sys_store_16b): a
+// wave's lanes at a 12-B stride then cover whole lines in one instruction, where three 32-bit
+// stores each write every third word of a line.  No wait after it: the server's vmcnt(0)
+// before its done words covers it.
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ void sys_store_12b(uint8_t* p, u32x3 v) {
+  __asm__ volatile("global_store_dwordx3 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void sys_store_8b(uint8_t* p, uint32_t a, uint32_t b) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  __asm__ volatile("global_store_dwordx2 %0, %1, off sc0 sc1" : : "v"(p), "v"(u32x2{a, b}) : "memory");
 }
 
 // The VRAM ring (inl != nullptr, fec_kernels.hpp kServerInline): the poll reads the slots from
@@ -1771,7 +1784,8 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
                                                                 uint64_t* __restrict__ done,
                                                                 ServerControl* __restrict__ ctl, uint64_t start_seq,
                                                                 uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                                                uint64_t* __restrict__ stamps, uint32_t spec_on) {
+                                                                uint64_t* __restrict__ stamps, uint32_t flags) {
+  const bool spec_on = (flags & kServerFlagSpec) != 0;
   __shared__ uint64_t s_next;
   __shared__ uint32_t s_n, s_exit, s_stop;
   __shared__ uint32_t s_first[kServerPoll + 1];  // work items before slot i of the run
@@ -1926,10 +1940,20 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
           if (stamps != nullptr && tid == 0 && w == 0) st_t[6] = static_cast<uint64_t>(wall_clock64());
           uint8_t* dst = reinterpret_cast<uint8_t*>(s_head[i][0] & kServerAddrMask) + static_cast<uint64_t>(g) * P +
                          col * kInlinePayload;
+          // one store per chunk: the lanes' 12-B pieces cover whole lines in one instruction.
+          // (Three 32-bit stores, each writing every third word of a line, took 31 us a call
+          // instead of 6.9: every batch was found only by the poll that also read the stop word
+          // from host memory -- the partial-line writes, and the done word behind them, left
+          // the device only when a read to the host pushed them.  scripts/experiments/
+          // r04_i_vram_stamps.sh, profiles/r04_vram_store_forms.txt.)
           const uint32_t rem = P - col * kInlinePayload;  // whole words (the host inlines P % 4 == 0 only)
-          sys_store_32(dst, acc.x);
-          if (rem > 4u) sys_store_32(dst + 4, acc.y);
-          if (rem > 8u) sys_store_32(dst + 8, acc.z);
+          if (rem >= 12u) {
+            sys_store_12b(dst, u32x3{acc.x, acc.y, acc.z});
+          } else if (rem == 8u) {
+            sys_store_8b(dst, acc.x, acc.y);
+          } else {
+            sys_store_32(dst, acc.x);
+          }
           continue;
         }
         const uint32_t coff = col * 16u + 16u <= P ? col * 16u : P - 16u;
@@ -2712,9 +2736,9 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
 
 hipError_t launch_legacy_server(const ServerSlot* ring, const uint8_t* inl, uint64_t* done, ServerControl* ctl,
                                 uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                uint64_t* stamps, bool spec, hipStream_t s) {
+                                uint64_t* stamps, uint32_t flags, hipStream_t s) {
   hipLaunchKernelGGL(legacy_server, dim3(1), dim3(kServerThreads), 0, s, ring, inl, done, ctl, start_seq, gen,
-                     idle_ticks, life_ticks, stamps, spec ? 1u : 0u);
+                     idle_ticks, life_ticks, stamps, flags);
   return hipGetLastError();
 }
 

@@ -194,12 +194,14 @@ struct alignas(64) ServerControl {
 // idle_ticks, or lived life_ticks (wall-clock ticks, hipDeviceAttributeWallClockRate), or the
 // host sets ctl->stop; on leaving it stores progress and then exited = gen.
 // stamps: nullptr, or 256 x 8 words of host memory for the diagnostic phase stamps (QUICFEC_RESIDENT_STAMPS).
-// spec: speculative poll (the slots after a batch read while it is served; QUICFEC_RESIDENT_SPEC).
+// speculative poll: the slots after a batch read while it is served (QUICFEC_RESIDENT_SPEC).
 // inl: the inline data areas (kInlineSlotBytes per slot) when the ring is in VRAM, else nullptr;
 // then the host's stop word (host memory) is read by every 16th poll only, not every poll.
+// flags: kServerFlagSpec.
+constexpr uint32_t kServerFlagSpec = 1u;
 hipError_t launch_legacy_server(const ServerSlot* ring, const uint8_t* inl, uint64_t* done, ServerControl* ctl,
                                 uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                uint64_t* stamps, bool spec, hipStream_t s);
+                                uint64_t* stamps, uint32_t flags, hipStream_t s);
 
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);
