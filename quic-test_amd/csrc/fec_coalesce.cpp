@@ -388,6 +388,8 @@ bool alloc_coherent(Pinned& m, size_t bytes) {
 }
 
 constexpr uint32_t kResidentOutBytes = 16u << 10;  // per slot: repair rows of callers whose buffer is pageable
+// per slot of the VRAM ring: an inline call's tagged repair chunks (kInlineMaxGroups x 128 x 16 B)
+constexpr uint32_t kInlineOutBytes = kInlineMaxGroups * (kInlineMaxP / kInlinePayload) * 16;
 
 std::atomic<uint64_t> g_res_calls{0}, g_res_launches{0}, g_res_pre_ns{0}, g_res_wait_ns{0}, g_res_post_ns{0};
 std::atomic<uint64_t> g_res_inline{0}, g_res_vram{0};
@@ -447,11 +449,6 @@ class Resident {
     r->deadline = std::chrono::milliseconds(std::max(1L, env_long("QUICFEC_RESIDENT_DEADLINE_MS", 10000)));
     // tests: an instance that never serves (relaunch records a launch without launching)
     r->no_launch = env_long("QUICFEC_RESIDENT_TEST_NOLAUNCH", 0) != 0;
-    // the speculative poll (legacy_server), off by default: same box, alternating
-    // (profiles/r04_resident_spec_ab.jsonl), back-to-back single calls 6.9-7.3 vs 8.0-8.1 us,
-    // 8 and 16 streams level within the noise, 4 streams 15-18% slower (batches split: slots
-    // arriving after the speculative read wait for a batch of their own).  QUICFEC_RESIDENT_SPEC=1.
-    if (env_long("QUICFEC_RESIDENT_SPEC", 0) != 0) r->flags |= kServerFlagSpec;
     if (env_long("QUICFEC_RESIDENT_STAMPS", 0) != 0 && !alloc_coherent(r->stamps, 256 * 8 * sizeof(uint64_t))) return nullptr;
     r->tick_khz = static_cast<uint64_t>(khz);
     // no word of a slot that was never written may carry lap 0's tag
@@ -488,10 +485,9 @@ class Resident {
   // nullptr (the call is then taken only with its packets inline).
   int encode(const uint8_t* slab, const uint8_t* slab_dev, const uint32_t* offsets, uint32_t G, uint32_t P,
              uint8_t* repair_out, uint8_t* repair_dev, uint64_t t_enter) {
-    if (!repair_dev && !ensure_outs()) return kNotTaken;
-    // (outs slots are 16 KB apart: 4-aligned like the base)
-    const bool inline_pk = inlines(G, P) && (reinterpret_cast<uintptr_t>(repair_dev ? repair_dev : outs.dev) & 3u) == 0;
+    const bool inline_pk = inlines(G, P);
     if (!inline_pk && slab_dev == nullptr) return kNotTaken;
+    if (!inline_pk && !repair_dev && !ensure_outs()) return kNotTaken;
     const uint64_t base = reinterpret_cast<uint64_t>(slab_dev);
     const uint64_t seq = next_seq.fetch_add(1, std::memory_order_relaxed);
     const uint32_t si = static_cast<uint32_t>(seq % kServerSlots);
@@ -516,10 +512,13 @@ class Resident {
     }
     if (!usable()) return kNotTaken;
     ServerSlot* sl = ring_w + si;
-    uint8_t* const out_dev = repair_dev ? repair_dev : outs.dev + size_t(si) * kResidentOutBytes;
+    const uint32_t lap1 = static_cast<uint32_t>(seq / kServerSlots) + 1u, nch = (P + kInlinePayload - 1) / kInlinePayload;
+    uint8_t* const out_dev = inline_pk   ? iouts.dev + size_t(si) * kInlineOutBytes
+                             : repair_dev ? repair_dev
+                                          : outs.dev + size_t(si) * kResidentOutBytes;
     if (inline_pk) {
       // the packets into the slot's data area (each chunk carries the lap), then the header
-      pack_inline(vinl + size_t(si) * kInlineSlotBytes, slab, offsets, G, P, static_cast<uint32_t>(seq / kServerSlots) + 1u);
+      pack_inline(vinl + size_t(si) * kInlineSlotBytes, slab, offsets, G, P, lap1);
       __atomic_store_n(&sl->out, reinterpret_cast<uint64_t>(out_dev) | tag, __ATOMIC_RELAXED);
       __atomic_store_n(&sl->shape, uint64_t(P) | (uint64_t(G) << 16) | kServerInline | tag, __ATOMIC_RELAXED);
     } else {
@@ -538,8 +537,20 @@ class Resident {
     const uint64_t t_pub = now_ns();
     int rc = FEC_OK;
     const auto t_fail = std::chrono::steady_clock::now() + deadline;
+    // an inline call's rows are complete when every chunk of its staging carries the lap (the
+    // last one is watched first; chunks land in any order)
+    const uint8_t* const stg = inline_pk ? iouts.host + size_t(si) * kInlineOutBytes : nullptr;
+    uint32_t landed = 0;
+    auto rows_landed = [&]() {
+      if (__atomic_load_n(reinterpret_cast<const uint32_t*>(stg + size_t(G * nch - 1) * 16 + 12), __ATOMIC_ACQUIRE) != lap1)
+        return false;
+      while (landed < G * nch &&
+             __atomic_load_n(reinterpret_cast<const uint32_t*>(stg + size_t(landed) * 16 + 12), __ATOMIC_ACQUIRE) == lap1)
+        ++landed;
+      return landed == G * nch;
+    };
     for (uint32_t spins = 0;; ++spins) {
-      if (__atomic_load_n(dw, __ATOMIC_ACQUIRE) == seq + 1) break;
+      if (inline_pk ? rows_landed() : __atomic_load_n(dw, __ATOMIC_ACQUIRE) == seq + 1) break;
       // no instance serving (never launched, or it left): launch one from its progress mark
       if ((spins & 15u) == 0 && !instance_alive()) {
         rc = relaunch();
@@ -570,6 +581,11 @@ class Resident {
                                __atomic_load_n(dw, __ATOMIC_ACQUIRE) != seq + 1 && std::chrono::steady_clock::now() < t_drain;
            ++spins)
         backoff(spins);
+    } else if (inline_pk) {
+      for (uint32_t g = 0; g < G; ++g)
+        for (uint32_t c = 0; c < nch; ++c)
+          std::memcpy(repair_out + size_t(g) * P + c * kInlinePayload, stg + (size_t(g) * nch + c) * 16,
+                      std::min(kInlinePayload, P - c * kInlinePayload));
     } else if (!repair_dev) {
       std::memcpy(repair_out, outs.host + size_t(si) * kResidentOutBytes, size_t(G) * P);
     }
@@ -628,13 +644,13 @@ class Resident {
   std::atomic<bool> broken{false};
   std::chrono::milliseconds deadline{10000};  // QUICFEC_RESIDENT_DEADLINE_MS
   bool no_launch = false;                     // QUICFEC_RESIDENT_TEST_NOLAUNCH
-  uint32_t flags = 0;                         // legacy_server flags (QUICFEC_RESIDENT_SPEC)
   std::atomic<bool> outs_ready{false};
   // The slots as the host writes them and as the device reads them: the page-locked ring, or
   // (setup_vram) one address for both, uncached device memory the host writes through the BAR.
   ServerSlot* ring_w = nullptr;
   const ServerSlot* ring_d = nullptr;
   uint8_t* vinl = nullptr;  // VRAM ring: the slots' inline data areas (kInlineSlotBytes each)
+  Pinned iouts;             // VRAM ring: the inline slots' tagged output staging (kInlineOutBytes each)
 
   // Moves the ring into VRAM when the host can store to device memory directly (a large-BAR
   // device; profiles/r04_probe_vram_host.jsonl: a host -> VRAM -> device -> host round trip in
@@ -643,6 +659,8 @@ class Resident {
   // Any failure leaves the page-locked ring in place.  The device memory is never freed (like
   // the rest of a Resident, it goes with the process).
   void setup_vram() {
+    // zeroed: no chunk with a lap word (lap + 1 >= 1) before the device writes it
+    if (!alloc_coherent(iouts, size_t(kInlineOutBytes) * kServerSlots)) return;
     int large_bar = 0;
     if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) != hipSuccess || !large_bar) {
       (void)hipGetLastError();
@@ -763,7 +781,7 @@ class Resident {
     const hipError_t e = bd.ok ? launch_legacy_server(ring_d, vinl, reinterpret_cast<uint64_t*>(done.dev),
                                                       reinterpret_cast<ServerControl*>(ctl.dev), start, g, idle_ticks,
                                                       life_ticks, stamps.host ? reinterpret_cast<uint64_t*>(stamps.dev) : nullptr,
-                                                      flags, stream)
+                                                      stream)
                                : hipErrorInvalidDevice;
     if (e != hipSuccess) {
       (void)hipGetLastError();

@@ -1733,81 +1733,75 @@ __device__ __forceinline__ void sys_store_relaxed(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// 16 bytes to host memory at any address, written system-coherent (sc0 sc1: no cache keeps a copy).
-// ISA assumption, not the HIP memory model's guarantee: on gfx94x / gfx95x a volatile global
-// store is emitted with sc0 sc1 (write-through to memory), so legacy_server's vmcnt(0) after its
-// repair-row stores means the rows are in host memory before it stores the done words (no
-// release fence; profiles/r03_resident_store_ab.txt).  The library is built for gfx950 only
-// (Makefile ARCH); a build for another target stops here instead of silently relying on it.
+// 16 bytes to host memory at any address, written system-coherent (sc0 sc1: write-through, no
+// cache keeps a copy), so legacy_server's vmcnt(0) after its repair-row stores means the rows
+// are in host memory before it stores the done words (no release fence;
+// profiles/r03_resident_store_ab.txt).  That is the gfx94x / gfx95x ISA's meaning of sc0 sc1,
+// not the HIP memory model's guarantee: a build for another target stops here.
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
-#error "legacy_server assumes gfx94x/gfx95x volatile stores are sc0 sc1 write-through (sys_store_16b)"
+#error "legacy_server assumes gfx94x/gfx95x sc0 sc1 stores are write-through (sys_store_16b)"
 #endif
+// Written as the instruction itself: a volatile store compiles to the same instruction but is
+// followed by s_waitcnt vmcnt(0), one PCIe acknowledgement per store before the thread goes on
+// (the VRAM ring's stamps: 1.7 us a batch spent there).  The server's own vmcnt(0) before its
+// done words is the one wait the rows need; the "memory" clobber keeps the compiler's memory
+// operations on their side of it, and an extra outstanding store only makes the compiler's own
+// vmcnt waits (in-order completion on gfx9) stricter.
 __device__ __forceinline__ void sys_store_16b(uint8_t* p, u32x4 v) {
-  *reinterpret_cast<volatile __attribute__((address_space(1))) u32x4u*>(reinterpret_cast<uintptr_t>(p)) = v;
+  __asm__ volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
 }
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// The server's workgroup barrier: every value it publishes between its waves is in LDS, so the
+// fences are LDS-only (s_waitcnt lgkmcnt(0) + s_barrier).  __syncthreads' workgroup fence also
+// waits vmcnt(0) -- the PCIe acknowledgement of every repair-row store, which an inline batch
+// does not need (its rows carry lap words) and an addressed batch waits for explicitly.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 // 16 bytes of host memory as they are now (system-coherent load, no cache).
 __device__ __forceinline__ u64x2 sys_load_16(const uint64_t* p) {
   return *reinterpret_cast<const volatile __attribute__((address_space(1))) u64x2*>(reinterpret_cast<uintptr_t>(p));
 }
 
-// A 32-bit word to host memory, system-coherent, no wait after it (a volatile store would be
-// followed by one: a PCIe acknowledgement apiece).  Only for a lone word (a row's last chunk).
-__device__ __forceinline__ void sys_store_32(uint8_t* p, uint32_t v) {
-  __hip_atomic_store(reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(reinterpret_cast<uintptr_t>(p)), v,
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// 12 bytes to host memory in one vector store, system-coherent (sc0 sc1 as sys_store_16b): a
-// wave's lanes at a 12-B stride then cover whole lines in one instruction, where three 32-bit
-// stores each write every third word of a line.  No wait after it: the server's vmcnt(0)
-// before its done words covers it.
-typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-__device__ __forceinline__ void sys_store_12b(uint8_t* p, u32x3 v) {
-  __asm__ volatile("global_store_dwordx3 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void sys_store_8b(uint8_t* p, uint32_t a, uint32_t b) {
-  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  __asm__ volatile("global_store_dwordx2 %0, %1, off sc0 sc1" : : "v"(p), "v"(u32x2{a, b}) : "memory");
-}
-
 // The VRAM ring (inl != nullptr, fec_kernels.hpp kServerInline): the poll reads the slots from
 // device memory -- local, not a PCIe round trip -- and an inline slot's work item is one 16-B
-// chunk column (g, c): its 10 chunks loaded from the slot's data area, their lap words checked,
-// the 12 payload bytes XORed and stored as three 32-bit words.  A chunk whose lap word is not
-// yet this slot's (the host's stores through the BAR landed in another order) marks the slot
-// bad: the run is served up to the first bad slot and the poll comes back for the rest.
+// chunk column (g, c): its 10 chunks loaded from the slot's data area (or, at the head of the
+// run, from the poll's prefetch), their lap words checked, the 12 payload bytes XORed and
+// stored with the lap word as chunk (g, c) of the slot's output staging.  A chunk whose lap
+// word is not yet this slot's (the host's stores through the BAR landed in another order)
+// marks the slot bad: the run is served up to the first bad slot and the poll comes back for
+// the rest.  The host takes an inline slot's rows by their lap words, so its done word needs
+// no acknowledgement of the row stores: a batch of inline slots only waits for them when it
+// also holds an addressed slot.
 __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot* __restrict__ ring,
                                                                 const uint8_t* __restrict__ inl,
                                                                 uint64_t* __restrict__ done,
                                                                 ServerControl* __restrict__ ctl, uint64_t start_seq,
                                                                 uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                                                uint64_t* __restrict__ stamps, uint32_t flags) {
-  const bool spec_on = (flags & kServerFlagSpec) != 0;
+                                                                uint64_t* __restrict__ stamps) {
   __shared__ uint64_t s_next;
-  __shared__ uint32_t s_n, s_exit, s_stop;
+  __shared__ uint32_t s_n, s_exit, s_stop, s_ack;
   __shared__ uint32_t s_first[kServerPoll + 1];  // work items before slot i of the run
   __shared__ uint32_t s_P[kServerPoll], s_cpp[kServerPoll], s_inl[kServerPoll], s_bad[kServerPoll];
   __shared__ uint64_t s_head[kServerPoll][kServerHeadWords];  // out, shape, addr[0..13] (tagged)
-  // The speculative poll: while a batch is being served, the last kSpecThreads threads read the
-  // slots after it (and the stop word); the next iteration uses those words instead of polling
-  // again when it starts at s_spec_seq.  A slot completed after the read simply looks incomplete
-  // and is found by the following poll (tags, as in the regular poll).
-  __shared__ uint64_t s_spec[kServerPoll][kServerHeadWords];
-  __shared__ uint64_t s_spec_seq;
-  __shared__ uint32_t s_spec_stop;
-  constexpr uint32_t kSpecThreads = kServerPoll * kServerHeadWords / 2 + 1;
-  constexpr uint32_t kSpecFirst = kServerThreads - kSpecThreads;
+  // VRAM ring: every poll also reads the first 16 KB of the next slot's inline data area, one
+  // 16-B chunk a thread, in flight with the header loads -- an inline slot found complete at
+  // the head of the run then takes its chunks from here instead of a second dependent round
+  // trip to memory (1 group of P <= 1224: 10 * ceil(P / 12) chunks <= 1024).  Read before the
+  // slot is known complete: the chunks' lap words decide, as for any chunk.
+  __shared__ u32x4 s_pre[kServerThreads];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   uint64_t t0 = 0, t_last = 0;  // thread 0 only
   if (tid == 0) {
     s_next = start_seq;
-    s_spec_seq = ~0ull;
     t0 = t_last = static_cast<uint64_t>(wall_clock64());
   }
-  __syncthreads();
+  lds_barrier();
   // Diagnostic stamps (stamps != nullptr, QUICFEC_RESIDENT_STAMPS): thread 0's wall clock at the
   // phases of each served batch, into a ring of 256 records of 8 words in host memory that no
   // other code reads; never part of a result.
@@ -1816,28 +1810,24 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
     const uint64_t next = s_next;
     if (stamps != nullptr && tid == 0) st_t[0] = static_cast<uint64_t>(wall_clock64());
     // the poll: the first two lines of each of the next kServerPoll slots, 16 B a lane, and the
-    // host's stop word, all in one round trip -- or the words the previous batch's speculative
-    // poll read for this very seq
-    const bool spec = s_spec_seq == next;
+    // host's stop word, all in one round trip
+    u32x4 pre = {0u, 0u, 0u, 0u};
+    if (inl != nullptr)
+      pre = __builtin_nontemporal_load(reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(
+          reinterpret_cast<uintptr_t>(inl + static_cast<uint64_t>(next % kServerSlots) * kInlineSlotBytes) + tid * 16u));
     if (tid < kServerPoll * kServerHeadWords / 2) {
       const uint32_t i = tid / (kServerHeadWords / 2), piece = tid % (kServerHeadWords / 2);
-      if (spec) {
-        s_head[i][2 * piece] = s_spec[i][2 * piece];
-        s_head[i][2 * piece + 1] = s_spec[i][2 * piece + 1];
-      } else {
-        const u64x2 v = sys_load_16(reinterpret_cast<const uint64_t*>(ring + (next + i) % kServerSlots) + 2 * piece);
-        s_head[i][2 * piece] = v.x;
-        s_head[i][2 * piece + 1] = v.y;
-      }
+      const u64x2 v = sys_load_16(reinterpret_cast<const uint64_t*>(ring + (next + i) % kServerSlots) + 2 * piece);
+      s_head[i][2 * piece] = v.x;
+      s_head[i][2 * piece + 1] = v.y;
     } else if (tid == kServerPoll * kServerHeadWords / 2) {
       // with the ring in VRAM the stop word (host memory) would make every poll a PCIe round
       // trip again: every 16th poll reads it (the idle and life bounds hold regardless)
-      s_stop = spec ? s_spec_stop
-               : (inl == nullptr || (it & 15u) == 0) ? (*reinterpret_cast<const volatile uint64_t*>(&ctl->stop) != 0 ? 1u : 0u)
-                                                     : 0u;
+      s_stop = (inl == nullptr || (it & 15u) == 0) ? (*reinterpret_cast<const volatile uint64_t*>(&ctl->stop) != 0 ? 1u : 0u)
+                                                   : 0u;
     }
-    __syncthreads();
-    if (tid == 0) s_spec_seq = ~0ull;  // used once (read by every thread above, before the barrier)
+    s_pre[tid] = pre;
+    lds_barrier();
     if (tid < 64) {
       const uint64_t seq = next + lane;
       const uint64_t tag = (seq / kServerSlots) & 0xFFu;
@@ -1853,6 +1843,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
       }
       const uint64_t bal = __ballot(ok);
       const uint32_t n = ~bal == 0 ? 64u : static_cast<uint32_t>(__builtin_ctzll(~bal));
+      const uint64_t addressed = __ballot(lane < n && !inline_slot);  // rows straight to the caller
       uint32_t work = 0;
       if (lane < n) {
         const uint64_t sh = s_head[lane][1];
@@ -1877,10 +1868,11 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
         if (n > 0) t_last = now;
         const bool stop = s_stop != 0;
         s_n = n;
+        s_ack = addressed != 0 ? 1u : 0u;
         s_exit = (stop || now - t0 > life_ticks || (n == 0 && now - t_last > idle_ticks)) ? 1u : 0u;
       }
     }
-    __syncthreads();
+    lds_barrier();
     const uint32_t n = s_n;
     const bool leave = s_exit != 0;
     if (stamps != nullptr && tid == 0) {
@@ -1895,19 +1887,6 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
       // PCIe read and the work step 2.8x slower (12.6 vs 4.5 us a batch).
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       if (stamps != nullptr && tid == 0) st_t[2] = static_cast<uint64_t>(wall_clock64());
-      // the speculative poll of the slots after this run, in flight with the packet loads
-      u64x2 sv = {0ull, 0ull};
-      if (spec_on && tid >= kSpecFirst) {
-        const uint32_t p = tid - kSpecFirst;
-        if (p < kSpecThreads - 1) {
-          const uint32_t i = p / (kServerHeadWords / 2), piece = p % (kServerHeadWords / 2);
-          sv = sys_load_16(reinterpret_cast<const uint64_t*>(ring + (next + n + i) % kServerSlots) + 2 * piece);
-        } else {
-          sv.x = __hip_atomic_load(reinterpret_cast<const __attribute__((address_space(1))) uint64_t*>(
-                                       reinterpret_cast<uintptr_t>(&ctl->stop)),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
       const uint32_t total = s_first[n];
       for (uint32_t w = tid; w < total; w += kServerThreads) {
         uint32_t i = 0;
@@ -1917,15 +1896,21 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
         const uint32_t g = local / cpp, col = local - g * cpp;
         if (s_inl[i] != 0) {
           const uint64_t seq = next + i;
-          const uint8_t* src = inl + static_cast<uint64_t>(seq % kServerSlots) * kInlineSlotBytes +
-                               (static_cast<uint64_t>(g) * kServerPackets * cpp + col) * 16u;
+          const uint32_t c0 = g * kServerPackets * cpp + col;  // chunk (g, 0, col)
           u32x4 v[kServerPackets];
+          if (i == 0 && (g + 1) * kServerPackets * cpp <= kServerThreads) {
+            // the head of the run: the poll brought its chunks
 #pragma unroll
-          for (uint32_t j = 0; j < kServerPackets; ++j)
-            v[j] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(
-                reinterpret_cast<uintptr_t>(src + static_cast<uint64_t>(j) * cpp * 16u));
+            for (uint32_t j = 0; j < kServerPackets; ++j) v[j] = s_pre[c0 + j * cpp];
+          } else {
+            const uint8_t* src = inl + static_cast<uint64_t>(seq % kServerSlots) * kInlineSlotBytes + c0 * 16u;
 #pragma unroll
-          for (uint32_t j = 0; j < kServerPackets; ++j) __asm__ volatile("" : "+v"(v[j]));
+            for (uint32_t j = 0; j < kServerPackets; ++j)
+              v[j] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(
+                  reinterpret_cast<uintptr_t>(src + static_cast<uint64_t>(j) * cpp * 16u));
+#pragma unroll
+            for (uint32_t j = 0; j < kServerPackets; ++j) __asm__ volatile("" : "+v"(v[j]));
+          }
           const uint32_t lap1 = static_cast<uint32_t>(seq / kServerSlots) + 1u;
           bool fresh = true;
           u32x4 acc = v[0];
@@ -1938,22 +1923,13 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
             continue;
           }
           if (stamps != nullptr && tid == 0 && w == 0) st_t[6] = static_cast<uint64_t>(wall_clock64());
-          uint8_t* dst = reinterpret_cast<uint8_t*>(s_head[i][0] & kServerAddrMask) + static_cast<uint64_t>(g) * P +
-                         col * kInlinePayload;
-          // one store per chunk: the lanes' 12-B pieces cover whole lines in one instruction.
-          // (Three 32-bit stores, each writing every third word of a line, took 31 us a call
-          // instead of 6.9: every batch was found only by the poll that also read the stop word
-          // from host memory -- the partial-line writes, and the done word behind them, left
-          // the device only when a read to the host pushed them.  scripts/experiments/
-          // r04_i_vram_stamps.sh, profiles/r04_vram_store_forms.txt.)
-          const uint32_t rem = P - col * kInlinePayload;  // whole words (the host inlines P % 4 == 0 only)
-          if (rem >= 12u) {
-            sys_store_12b(dst, u32x3{acc.x, acc.y, acc.z});
-          } else if (rem == 8u) {
-            sys_store_8b(dst, acc.x, acc.y);
-          } else {
-            sys_store_32(dst, acc.x);
-          }
+          // tagged rows, whole 16-B pieces side by side: a wave's stores cover whole lines (three
+          // 32-bit stores per 12 bytes, each writing every third word of a line, took 31 us a
+          // call instead of 6.9: every batch was found only by the poll that also read the stop
+          // word from host memory -- the partial-line writes and the done word behind them left
+          // the device only when a read to the host pushed them; profiles/r04_vram_store_forms.txt)
+          sys_store_16b(reinterpret_cast<uint8_t*>(s_head[i][0] & kServerAddrMask) + (static_cast<uint64_t>(g) * cpp + col) * 16u,
+                        u32x4{acc.x, acc.y, acc.z, lap1});
           continue;
         }
         const uint32_t coff = col * 16u + 16u <= P ? col * 16u : P - 16u;
@@ -2007,21 +1983,12 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
       // one of this thread's stores is acknowledged, then the workgroup's barrier, then the done
       // words -- no release fence.  Same box, alternating (profiles/r03_resident_store_ab.txt):
       // one caller 8.0 vs 10.9 us a call, 16 callers 550k vs 330k calls/s against plain stores
-      // and a system release fence (its L2 write-back 1.7-2.9 us a batch).
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      if (spec_on && tid >= kSpecFirst) {
-        const uint32_t p = tid - kSpecFirst;
-        if (p < kSpecThreads - 1) {
-          const uint32_t i = p / (kServerHeadWords / 2), piece = p % (kServerHeadWords / 2);
-          s_spec[i][2 * piece] = sv.x;
-          s_spec[i][2 * piece + 1] = sv.y;
-        } else {
-          s_spec_stop = sv.x != 0 ? 1u : 0u;
-          s_spec_seq = next + n;
-        }
-      }
+      // and a system release fence (its L2 write-back 1.7-2.9 us a batch).  Not for a batch of
+      // inline slots only: their rows carry lap words, and their done words only say the slot
+      // was consumed (its loads have returned).
+      if (s_ack != 0) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       if (stamps != nullptr && tid == 0) st_t[4] = static_cast<uint64_t>(wall_clock64());
-      __syncthreads();
+      lds_barrier();
       // the run up to its first slot with a chunk not yet landed (VRAM ring; n in any other case)
       uint32_t n_ok = n;
       if (tid < 64) {
@@ -2050,11 +2017,10 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
         sys_store_release(&rec[7], ++st_batches);
         st_polls = 0;
       }
-    } else if (!leave && !spec) {
-      // (a speculative poll that found nothing new is followed by a real poll at once)
+    } else if (!leave) {
       __builtin_amdgcn_s_sleep(8);
     }
-    __syncthreads();
+    lds_barrier();
     if (leave) break;
   }
   if (tid == 0) {
@@ -2736,9 +2702,9 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
 
 hipError_t launch_legacy_server(const ServerSlot* ring, const uint8_t* inl, uint64_t* done, ServerControl* ctl,
                                 uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                uint64_t* stamps, uint32_t flags, hipStream_t s) {
+                                uint64_t* stamps, hipStream_t s) {
   hipLaunchKernelGGL(legacy_server, dim3(1), dim3(kServerThreads), 0, s, ring, inl, done, ctl, start_seq, gen,
-                     idle_ticks, life_ticks, stamps, flags);
+                     idle_ticks, life_ticks, stamps);
   return hipGetLastError();
 }
 

@@ -177,7 +177,10 @@ struct alignas(64) ServerSlot {
 // chunks of 16 B -- 12 payload bytes (payload bytes [12c, 12c + 12) at chunk c, zero past P)
 // and, in the fourth 32-bit word, the slot's lap + 1 -- at chunk (g * 10 + j) * nch + c,
 // nch = ceil(P / 12).  Every chunk is self-validating like the header words: no ordering of the
-// host's stores through the BAR is assumed.
+// host's stores through the BAR is assumed.  The rows come back the same way: an inline slot's
+// `out` is its output staging in page-locked host memory, repair chunk (g, c) -- payload bytes
+// [12c, 12c + 12) of row g and the lap + 1 word -- at out + (g * nch + c) * 16, and the host
+// takes the rows once every chunk carries the lap (the done word then only says "consumed").
 constexpr uint64_t kServerInline = 1ull << 24;
 constexpr uint32_t kInlineMaxGroups = 4;
 constexpr uint32_t kInlineMaxP = 1536;
@@ -194,14 +197,11 @@ struct alignas(64) ServerControl {
 // idle_ticks, or lived life_ticks (wall-clock ticks, hipDeviceAttributeWallClockRate), or the
 // host sets ctl->stop; on leaving it stores progress and then exited = gen.
 // stamps: nullptr, or 256 x 8 words of host memory for the diagnostic phase stamps (QUICFEC_RESIDENT_STAMPS).
-// speculative poll: the slots after a batch read while it is served (QUICFEC_RESIDENT_SPEC).
 // inl: the inline data areas (kInlineSlotBytes per slot) when the ring is in VRAM, else nullptr;
 // then the host's stop word (host memory) is read by every 16th poll only, not every poll.
-// flags: kServerFlagSpec.
-constexpr uint32_t kServerFlagSpec = 1u;
 hipError_t launch_legacy_server(const ServerSlot* ring, const uint8_t* inl, uint64_t* done, ServerControl* ctl,
                                 uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                uint64_t* stamps, uint32_t flags, hipStream_t s);
+                                uint64_t* stamps, hipStream_t s);
 
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);

@@ -17,3 +17,7 @@ for rep in 1 2; do
   done
 done
 cat gpurun_out/r04h/ab.jsonl
+# the server's phase stamps on the VRAM ring, one stream and 16
+QUICFEC_RESIDENT_STAMPS=1 timeout -k 10 60 $B legacy_raw 5000 > gpurun_out/r04h/stamps_raw.json 2> gpurun_out/r04h/stamps_raw.err || [ $? -eq 1 ]
+QUICFEC_RESIDENT_STAMPS=1 timeout -k 10 60 $B legacy 16 0 1 > gpurun_out/r04h/stamps_s16.json 2> gpurun_out/r04h/stamps_s16.err || [ $? -eq 1 ]
+grep -h resident_stamps gpurun_out/r04h/stamps_*.err

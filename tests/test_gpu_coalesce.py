@@ -200,6 +200,7 @@ def test_resident_encoder_leaves_when_idle_and_comes_back(quicfec_mod, oracle_mo
     sp, rp = lib.fec_alloc_slab(10 * P), lib.fec_alloc_repair_buffer(P)
     offs = (np.arange(10, dtype=np.uint32) * P).astype(np.uint32)
     try:
+        time.sleep(0.05)  # an instance an earlier test's last call launched has left
         quicfec_mod.coalesce_stats(reset=True)
         for rnd in range(4):
             grp = oracle_mod.splitmix_bytes(10 * P, 4242 + rnd)
