@@ -1886,7 +1886,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
       // the packets system-coherent instead (sc0 sc1, no fence) made every 16-B load its own
       // PCIe read and the work step 2.8x slower (12.6 vs 4.5 us a batch).
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      if (stamps != nullptr && tid == 0) st_t[2] = static_cast<uint64_t>(wall_clock64());
+      if (stamps != nullptr && tid == 0) st_t[2] = st_t[6] = static_cast<uint64_t>(wall_clock64());  // (a bad slot: no item)
       const uint32_t total = s_first[n];
       for (uint32_t w = tid; w < total; w += kServerThreads) {
         uint32_t i = 0;
