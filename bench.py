@@ -488,6 +488,38 @@ def e2e_pinned(ctx, d_data, d_parity, d_masks, G: int, cfg: dict, reps: int = 3)
     return out
 
 
+CALL_SITE_TOOL = REPO / "quic-test_amd" / "lib" / "call_site"
+
+
+def call_site(seconds: float = 1.0) -> dict:
+    """The reference's unchanged product call site next to the headline: every QUIC stream's own
+    HybridFECEncoder making one fec_encode_batch call per group of 10 x 1200 B
+    (encoder_hybrid.go:115 -> fec_cgo.go:138), through the C++ mirror, measured by
+    quic-test_amd/lib/call_site (tools/call_site.cpp) in a process of its own, as a Go binary
+    would be: raw calls with FECEncoderCXX's buffers, then 1 and 16 streams back to back.  Every
+    repair is checked against the XOR inside the tool (no oracle).  Not the headline metric."""
+    import subprocess
+    if not CALL_SITE_TOOL.exists():
+        return {"skipped": "quic-test_amd/lib/call_site not built (__graft_entry__.build())"}
+    out = {"reference_call": "encoder_hybrid.go:115 -> fec_cgo.go:138 fec_encode_batch, 1 group of 10 x 1200 B per call",
+           "tool": "quic-test_amd/lib/call_site"}
+    for name, argv in (("raw", ["raw", "20000"]), ("streams_1", ["streams", "1", str(seconds)]),
+                       ("streams_16", ["streams", "16", str(seconds)])):
+        try:
+            p = subprocess.run([str(CALL_SITE_TOOL), *argv], capture_output=True, text=True, timeout=120)
+        except subprocess.TimeoutExpired:
+            out[name] = {"error": "timed out"}
+            break
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        if not lines:
+            out[name] = {"error": f"exit {p.returncode}: {p.stderr.strip()[-300:]}"}
+            break
+        rec = json.loads(lines[-1])
+        out[name] = {k: rec[k] for k in ("groups_per_s", "delay_us", "errors", "resident_inline", "resident_vram")
+                     if k in rec}
+    return out
+
+
 def packed_supported(k: int, r: int, P: int) -> bool:
     """Shapes with a mask-addressed (inline-classify) recover form, which the packed API needs
     (include/fec_hip.h fec_recover_batch_rs_dev_packed)."""
@@ -586,6 +618,9 @@ def parse_args(argv=None):
     ap.add_argument("--e2e-groups", type=int, default=0,
                     help="groups per rank of the host-resident legs (default: all at N = 1, 250k per rank at N > 1, "
                          "so N ranks' page-locked buffers stay within one node's RAM)")
+    ap.add_argument("--no-call-site", action="store_true",
+                    help="skip the call_site section (the reference's one-group-per-call site; N = 1, runs with "
+                         "the cpu_baseline leg, so --no-cpu-baseline skips it too)")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -964,6 +999,9 @@ def main() -> int:
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)
+    site = None  # beside the headline like cpu_baseline, and skipped with it (profiled and A/B runs)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_call_site:
+        site = call_site()
 
     if rank == 0:
         k, r, P = cfg["k"], cfg["r"], cfg["P"]
@@ -985,6 +1023,8 @@ def main() -> int:
         }
         if "e2e_pinned" in head:
             out["e2e_pinned"] = head["e2e_pinned"]
+        if site is not None:
+            out["call_site"] = site
         if "buffers" in head:
             out["buffers"] = head["buffers"]
         if legs:

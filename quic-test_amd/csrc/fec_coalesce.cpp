@@ -692,7 +692,7 @@ class Resident {
     g_res_vram.fetch_add(1, std::memory_order_relaxed);
   }
 
-  // Whether [p, p + n) lies in one mapping of this process's address space.
+  // Whether [p, p + n) lies in one readable and writable mapping of this process.
   static bool host_mapped(const void* p, size_t n) {
     FILE* f = std::fopen("/proc/self/maps", "r");
     if (!f) return false;
@@ -701,7 +701,9 @@ class Resident {
     char line[512];
     while (!found && std::fgets(line, sizeof(line), f)) {
       unsigned long lo = 0, hi = 0;
-      if (std::sscanf(line, "%lx-%lx", &lo, &hi) == 2 && a >= lo && a + n <= hi) found = true;
+      char perms[8] = {};
+      if (std::sscanf(line, "%lx-%lx %7s", &lo, &hi, perms) == 3 && a >= lo && a + n <= hi)
+        found = perms[0] == 'r' && perms[1] == 'w';
     }
     std::fclose(f);
     return found;

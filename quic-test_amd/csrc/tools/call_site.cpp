@@ -1,0 +1,138 @@
+// call_site.cpp — the reference's unchanged FEC call site, timed for bench.py's `call_site`
+// section.  Every stream owns a HybridFECEncoder (the C++ mirror of encoder_hybrid.go) and
+// feeds it 1200-B packets back to back; the 10th packet of a group makes one fec_encode_batch
+// call with that one group (encoder_hybrid.go:115 -> fec_cgo.go:138).  `raw` times
+// fec_encode_batch alone with FECEncoderCXX's buffers (fec_cgo.go:64/76).  Every repair payload
+// is checked against the XOR computed here -- no oracle, so bench.py may run it outside its
+// cpu_baseline leg.  Links only libfec_hip.so and the mirror (libquicfec_host.so).
+//
+//   call_site raw CALLS
+//   call_site streams S SECONDS
+//   -> one JSON line: {"mode", "streams", "groups", "seconds", "groups_per_s", "delay_us": {p50, p99},
+//                      "errors", "resident_calls", "resident_inline", "resident_vram"}
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "fec.hpp"
+#include "fec_hip.h"
+
+using namespace quicfec;
+using Clock = std::chrono::steady_clock;
+
+namespace {
+
+constexpr uint32_t kK = 10, kP = 1200, kGroups = 16;
+
+// kGroups groups of 10 packets and each group's XOR
+struct Data {
+  std::vector<uint8_t> pk, xr;
+  Data() : pk(size_t(kGroups) * kK * kP), xr(size_t(kGroups) * kP, 0) {
+    uint64_t x = 0x5EED0C5Eull;
+    for (auto& b : pk) {
+      x = x * 6364136223846793005ull + 1442695040888963407ull;
+      b = static_cast<uint8_t>(x >> 56);
+    }
+    for (uint32_t g = 0; g < kGroups; ++g)
+      for (uint32_t j = 0; j < kK; ++j)
+        for (uint32_t i = 0; i < kP; ++i) xr[size_t(g) * kP + i] ^= pk[(size_t(g) * kK + j) * kP + i];
+  }
+};
+
+void report(const char* mode, int streams, std::vector<double>& us, double seconds, long errors) {
+  std::sort(us.begin(), us.end());
+  auto pct = [&](double p) { return us.empty() ? 0.0 : us[std::min(us.size() - 1, size_t(p * us.size()))]; };
+  FECCoalesceStats cs{};
+  fec_coalesce_stats(&cs, 0);
+  std::printf("{\"mode\": \"%s\", \"streams\": %d, \"groups\": %zu, \"seconds\": %.3f, \"groups_per_s\": %.1f, "
+              "\"delay_us\": {\"p50\": %.2f, \"p99\": %.2f}, \"errors\": %ld, \"resident_calls\": %llu, "
+              "\"resident_inline\": %llu, \"resident_vram\": %llu}\n",
+              mode, streams, us.size(), seconds, double(us.size()) / seconds, pct(0.5), pct(0.99), errors,
+              (unsigned long long)cs.resident_calls, (unsigned long long)cs.resident_inline,
+              (unsigned long long)cs.resident_vram);
+  std::fflush(stdout);
+}
+
+int raw(int calls) {
+  const Data d;
+  FECEncoderCtx* ctx = fec_encoder_new(0.1, 1024);
+  if (!ctx) return 2;
+  auto* slab = static_cast<uint8_t*>(fec_alloc_slab(size_t(kK) * kP));
+  auto* rep = static_cast<uint8_t*>(fec_alloc_repair_buffer(kP));
+  uint32_t offs[kK];
+  for (uint32_t j = 0; j < kK; ++j) offs[j] = j * kP;
+  FECCoalesceStats cs{};
+  fec_coalesce_stats(&cs, 1);
+  std::vector<double> us;
+  us.reserve(size_t(calls));
+  long errors = 0;
+  const auto t0 = Clock::now();
+  for (int c = 0; c < calls; ++c) {
+    const uint32_t g = uint32_t(c) % kGroups;
+    std::memcpy(slab, d.pk.data() + size_t(g) * kK * kP, size_t(kK) * kP);  // the wrapper's copy into its slab
+    const auto a = Clock::now();
+    if (fec_encode_batch(ctx, slab, offs, 1, kP, rep) != 0) ++errors;
+    us.push_back(std::chrono::duration<double, std::micro>(Clock::now() - a).count());
+    if (std::memcmp(rep, d.xr.data() + size_t(g) * kP, kP) != 0) ++errors;
+  }
+  const double secs = std::chrono::duration<double>(Clock::now() - t0).count();
+  report("raw", 1, us, secs, errors);
+  fec_free_slab(slab);
+  fec_free_repair_buffer(rep);
+  fec_encoder_free(ctx);
+  return errors ? 1 : 0;
+}
+
+int streams(int S, double seconds) {
+  const Data d;
+  FECCoalesceStats cs{};
+  fec_coalesce_stats(&cs, 1);
+  std::mutex mu;
+  std::vector<double> all;
+  std::atomic<long> errors{0};
+  const auto t0 = Clock::now();
+  const auto t_end = t0 + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(seconds));
+  std::vector<std::thread> th;
+  for (int s = 0; s < S; ++s)
+    th.emplace_back([&, s] {
+      HybridFECEncoder h(0.1);
+      if (!h.UseCXX()) ++errors;  // the GPU library must serve it
+      std::vector<double> lat;
+      for (uint64_t i = 0;; ++i) {
+        if (i % kK == 0 && Clock::now() >= t_end) break;
+        const uint32_t g = uint32_t((uint64_t(s) * 7 + i / kK) % kGroups);
+        const auto a = Clock::now();
+        AddPacketResult res = h.AddPacket(d.pk.data() + (size_t(g) * kK + i % kK) * kP, kP, i);
+        if (!res.err.ok()) ++errors;
+        if (res.needsRedundancy) {
+          lat.push_back(std::chrono::duration<double, std::micro>(Clock::now() - a).count());
+          // the repair packet: an 11-byte header, then the group's XOR (encoder_hybrid.go)
+          if (res.redundancy.size() != 11u + kP || std::memcmp(res.redundancy.data() + 11, d.xr.data() + size_t(g) * kP, kP))
+            ++errors;
+        }
+      }
+      h.Close();
+      std::lock_guard<std::mutex> lk(mu);
+      all.insert(all.end(), lat.begin(), lat.end());
+    });
+  for (auto& t : th) t.join();
+  report("streams", S, all, std::chrono::duration<double>(Clock::now() - t0).count(), errors.load());
+  return errors ? 1 : 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const std::string mode = argc > 1 ? argv[1] : "raw";
+  if (mode == "raw") return raw(argc > 2 ? std::atoi(argv[2]) : 20000);
+  if (mode == "streams") return streams(argc > 2 ? std::atoi(argv[2]) : 16, argc > 3 ? std::atof(argv[3]) : 1.0);
+  std::fprintf(stderr, "usage: call_site raw CALLS | call_site streams S SECONDS\n");
+  return 2;
+}

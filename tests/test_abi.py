@@ -184,3 +184,26 @@ def test_alloc_slab_numa_binds_node(quicfec_mod):
     q = lib.fec_alloc_slab_numa(64, -1)
     if q:
         lib.fec_free_slab(q)
+
+
+def test_product_and_bench_tools_link_no_oracle():
+    """The oracle is test infrastructure: the product library, the C++ mirror and the tool bench.py
+    runs outside its cpu_baseline leg (lib/call_site, the call_site section) link none of it."""
+    import subprocess
+    lib = REPO / "quic-test_amd" / "lib"
+    for name in ("libfec_hip.so", "libquicfec_host.so", "call_site"):
+        f = lib / name
+        assert f.exists(), f"{f} not built (__graft_entry__.build())"
+        dyn = subprocess.run(["readelf", "-d", str(f)], capture_output=True, text=True, check=True).stdout
+        needed = [ln for ln in dyn.splitlines() if "(NEEDED)" in ln]
+        assert needed and not any("oracle" in ln or "fec_ref" in ln for ln in needed), (name, needed)
+
+
+def test_bench_call_site_without_tool_is_skipped(monkeypatch, tmp_path):
+    """bench.py's call_site section reports a missing tool instead of failing the bench line."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", REPO / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    monkeypatch.setattr(bench, "CALL_SITE_TOOL", tmp_path / "missing")
+    assert "skipped" in bench.call_site()
