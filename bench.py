@@ -491,7 +491,7 @@ def e2e_pinned(ctx, d_data, d_parity, d_masks, G: int, cfg: dict, reps: int = 3)
 CALL_SITE_TOOL = REPO / "quic-test_amd" / "lib" / "call_site"
 
 
-def call_site(seconds: float = 1.0) -> dict:
+def call_site(seconds: float = 2.0) -> dict:
     """The reference's unchanged product call site next to the headline: every QUIC stream's own
     HybridFECEncoder making one fec_encode_batch call per group of 10 x 1200 B
     (encoder_hybrid.go:115 -> fec_cgo.go:138), through the C++ mirror, measured by
