@@ -32,6 +32,10 @@ case "${1:-run}" in
     # the unchanged call site from 16 streams through the resident encoder and shared launches
     $C -o $A/batcher_latency quic-test_amd/csrc/tools/batcher_latency.cpp -Iquic-test_amd/csrc -L$A -lquicfec_host -lfec_hip \
       oracle/liboracle.so -Wl,-rpath,'$ORIGIN' -Wl,-rpath,'$ORIGIN/../../oracle' -lpthread
+    # mixed shapes through both resident ring kinds (the VRAM ring's host-side packing and tagged
+    # row collection), pageable and page-locked buffers
+    $C -rdynamic -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -o $A/exit_path_test tests/csrc/exit_path_test.cpp \
+      -L$A -lfec_hip -ldl -Wl,-rpath,'$ORIGIN'
     [ "$SANK" = thread ] || cp /opt/rocm/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so $A/
     printf 'called_from_lib:libamdhip64.so\ncalled_from_lib:libhsa-runtime64.so\nrace:libamdhip64.so\nrace:libhsa-runtime64.so\n' > $A/tsan.supp
     ;;
@@ -43,5 +47,8 @@ case "${1:-run}" in
     timeout -k 10 300 $A/ctx_isolation_test
     QUICFEC_RESIDENT=1 timeout -k 10 120 $A/batcher_latency legacy 16 0 2
     QUICFEC_RESIDENT=0 timeout -k 10 120 $A/batcher_latency legacy 16 0 2
+    QUICFEC_RESIDENT_VRAM=0 timeout -k 10 120 $A/batcher_latency legacy 16 0 2
+    timeout -k 10 120 $A/exit_path_test mixed 360
+    timeout -k 10 120 $A/exit_path_test mixed_hostring 360
     ;;
 esac
