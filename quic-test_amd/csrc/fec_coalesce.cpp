@@ -568,16 +568,17 @@ class Resident {
     if (rc != FEC_OK) {
       // Not served.  Turn the slot into one with nothing to do (the slots after it are served in
       // order), poison the Resident (never relaunched), and ask a running instance to leave.  An
-      // instance that read the slot before the rewrite may still write the caller's repair rows
-      // and read its slab: wait, bounded, until it has served this seq or left.  Past that bound
-      // the device is hung, and the caller's buffers handed to this call must not be reused
-      // (include/fec_xor_simd.h, fec_encode_batch).
+      // instance that read an addressed slot before the rewrite may still write the caller's
+      // repair rows and read its slab: wait, bounded, until it has served this seq or left.  Past
+      // that bound the device is hung, and the caller's buffers handed to this call must not be
+      // reused (include/fec_xor_simd.h, fec_encode_batch).  An inline slot's reads and writes are
+      // the Resident's own memory: nothing of the caller's to wait for.
       __atomic_store_n(&sl->shape, uint64_t(P) | tag, __ATOMIC_RELEASE);
       if (vinl) std::atomic_thread_fence(std::memory_order_seq_cst);
       poison();
       const auto t_drain = std::chrono::steady_clock::now() + deadline;
       const ServerControl* c = reinterpret_cast<const ServerControl*>(ctl.host);
-      for (uint32_t spins = 0; instance_alive() && __atomic_load_n(&c->progress, __ATOMIC_ACQUIRE) <= seq &&
+      for (uint32_t spins = 0; !inline_pk && instance_alive() && __atomic_load_n(&c->progress, __ATOMIC_ACQUIRE) <= seq &&
                                __atomic_load_n(dw, __ATOMIC_ACQUIRE) != seq + 1 && std::chrono::steady_clock::now() < t_drain;
            ++spins)
         backoff(spins);
