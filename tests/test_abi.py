@@ -207,3 +207,25 @@ def test_bench_call_site_without_tool_is_skipped(monkeypatch, tmp_path):
     spec.loader.exec_module(bench)
     monkeypatch.setattr(bench, "CALL_SITE_TOOL", tmp_path / "missing")
     assert "skipped" in bench.call_site()
+
+
+def test_bench_call_site_reads_the_tool_lines(monkeypatch, tmp_path):
+    """bench.py's call_site section runs the tool once per leg (raw, 1 and 16 streams) and keeps
+    each leg's rate, delay percentiles, error count and ring kind from its last JSON line."""
+    import importlib.util
+    import stat
+    spec = importlib.util.spec_from_file_location("bench_mod2", REPO / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    tool = tmp_path / "call_site"
+    tool.write_text("#!/bin/sh\necho 'warming up'\n"
+                    "echo '{\"mode\": \"'$1'\", \"streams\": '${2:-1}', \"groups_per_s\": 1000.0, "
+                    "\"delay_us\": {\"p50\": 5.5, \"p99\": 9.0}, \"errors\": 0, \"resident_inline\": 7, "
+                    "\"resident_vram\": 1, \"extra\": 3}'\n")
+    tool.chmod(tool.stat().st_mode | stat.S_IEXEC)
+    monkeypatch.setattr(bench, "CALL_SITE_TOOL", tool)
+    out = bench.call_site(seconds=0.1)
+    assert set(out) >= {"raw", "streams_1", "streams_16", "reference_call"}
+    for leg in ("raw", "streams_1", "streams_16"):
+        assert out[leg] == {"groups_per_s": 1000.0, "delay_us": {"p50": 5.5, "p99": 9.0}, "errors": 0,
+                            "resident_inline": 7, "resident_vram": 1}
