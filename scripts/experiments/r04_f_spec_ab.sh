@@ -1,5 +1,6 @@
 # The resident encoder's speculative poll, A/B on one box (QUICFEC_RESIDENT_SPEC=1/0, alternating):
 # raw one-stream calls and the unchanged call site at 4 / 8 / 16 streams.
+# (QUICFEC_RESIDENT_SPEC existed only until the VRAM ring; the speculative poll was removed)
 set -e
 B=./quic-test_amd/lib/batcher_latency
 for rep in 1 2; do

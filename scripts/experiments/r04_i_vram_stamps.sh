@@ -1,6 +1,7 @@
 # Where the VRAM ring's ~30 us a call goes: the server's phase stamps (QUICFEC_RESIDENT_STAMPS)
 # for the three inline store forms (4: 12-B chunk columns as three 32-bit stores; 12: one 12-B
 # store each; 16: 16-B columns) and the page-locked ring, one stream and 16.  Output: gpurun_out/r04i/.
+# (QUICFEC_RESIDENT_INLINE_STORE existed only on the build this ran on; the library kept one form.)
 set -e
 mkdir -p gpurun_out/r04i
 B=./quic-test_amd/lib/batcher_latency
