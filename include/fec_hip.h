@@ -64,7 +64,8 @@ FECEncoderCtx* fec_encoder_new_device(double redundancy, uint32_t max_groups, in
 /* Device ordinal a context is bound to, or -1 for NULL. */
 int fec_encoder_device(const FECEncoderCtx* ctx);
 
-/* Library build identifier (kernel ISA + version), for logs. */
+/* Library build identifier, for logs: "libfec_hip <version> gfx950 src=<sha256 of the sources it was
+ * built from>" (quic-test_amd/csrc/src_hash.py defines the hash; tests/test_abi.py checks it). */
 const char* fec_hip_version(void);
 
 /* The r x k parity matrix M, row-major (r*k bytes).  0, or FEC_ERR_RANGE. */
@@ -298,6 +299,8 @@ typedef struct {
   uint64_t resident_post_ns;   /*   and from there to the return */
   uint64_t resident_inline;    /* resident calls whose packets the host copied into the slot */
   uint64_t resident_vram;      /* devices whose resident ring is in device memory (not reset) */
+  uint64_t resident_bad_slots; /* polls that found a published slot with a word not yet landed, retried (not reset) */
+  uint64_t resident_scrubs;    /* slots the resident encoder zeroed at a tag-epoch boundary (not reset) */
 } FECCoalesceStats;
 
 /* Process-wide totals over every device and packet size; reset = 1 zeroes them after the read. */

@@ -445,14 +445,22 @@ class Resident {
         !alloc_coherent(r->done, sizeof(uint64_t) * kServerSlots) || !alloc_coherent(r->ctl, sizeof(ServerControl)))
       return nullptr;
     r->ring_w = reinterpret_cast<ServerSlot*>(r->ring.host);
-    r->ring_d = reinterpret_cast<const ServerSlot*>(r->ring.dev);
+    r->ring_d = reinterpret_cast<ServerSlot*>(r->ring.dev);
     r->deadline = std::chrono::milliseconds(std::max(1L, env_long("QUICFEC_RESIDENT_DEADLINE_MS", 10000)));
     // tests: an instance that never serves (relaunch records a launch without launching)
     r->no_launch = env_long("QUICFEC_RESIDENT_TEST_NOLAUNCH", 0) != 0;
+    // tests: a short tag epoch (fec_kernels.hpp server_tag), so the scrubs at its boundaries run
+    // within a few thousand calls
+    r->epoch = static_cast<uint32_t>(std::min<long>(kServerEpoch, std::max(1L, env_long("QUICFEC_RESIDENT_TEST_EPOCH", kServerEpoch))));
+    // tests: every inline call lands one chunk in two 8-B pieces, the half with the tag first and
+    // the other ~100 us after the slot's header (a write-combined store evicted in pieces)
+    r->tear = env_long("QUICFEC_RESIDENT_TEST_TEAR", 0) != 0;
+    // tests: the call of this seq fails as if its deadline had passed (poisoning under load)
+    r->fail_at = static_cast<uint64_t>(env_long("QUICFEC_RESIDENT_TEST_FAIL_AT", -1));
     if (env_long("QUICFEC_RESIDENT_STAMPS", 0) != 0 && !alloc_coherent(r->stamps, 256 * 8 * sizeof(uint64_t))) return nullptr;
     r->tick_khz = static_cast<uint64_t>(khz);
-    // no word of a slot that was never written may carry lap 0's tag
-    std::memset(r->ring.host, 0xFF, sizeof(ServerSlot) * kServerSlots);
+    // no word of a slot that was never written carries a tag (tags are 1 .. epoch; alloc_coherent zeroed it)
+    std::memset(r->ring.host, 0, sizeof(ServerSlot) * kServerSlots);
     if (env_long("QUICFEC_RESIDENT_VRAM", 1) != 0) r->setup_vram();
     r->collected.reset(new std::atomic<uint64_t>[kServerSlots]);
     for (uint32_t i = 0; i < kServerSlots; ++i) r->collected[i].store(0, std::memory_order_relaxed);
@@ -469,6 +477,10 @@ class Resident {
   // False once a call timed out or a relaunch failed (poison): later legacy calls take the
   // coalescer / per-context paths, and no instance is launched again.
   bool usable() const { return !broken.load(std::memory_order_acquire); }
+
+  // The server's diagnostic counters (ServerControl): retried slots and epoch scrubs.
+  uint64_t bad_slots() const { return __atomic_load_n(&reinterpret_cast<const ServerControl*>(ctl.host)->bad_slots, __ATOMIC_ACQUIRE); }
+  uint64_t scrubs() const { return __atomic_load_n(&reinterpret_cast<const ServerControl*>(ctl.host)->scrubs, __ATOMIC_ACQUIRE); }
 
   // The call's result, or kNotTaken when the Resident is (or just became) unusable before the
   // call published its slot: nothing of the caller's was handed to the device, and the caller
@@ -491,7 +503,8 @@ class Resident {
     const uint64_t base = reinterpret_cast<uint64_t>(slab_dev);
     const uint64_t seq = next_seq.fetch_add(1, std::memory_order_relaxed);
     const uint32_t si = static_cast<uint32_t>(seq % kServerSlots);
-    const uint64_t tag = ((seq / kServerSlots) & 0xFFu) << kServerTagShift;
+    const uint32_t tag16 = server_tag(seq, epoch);
+    const uint64_t tag = uint64_t(tag16) << kServerTagShift;
     // the slot's previous occupant (seq - kServerSlots) has been served and collected; if that
     // does not happen within the deadline, or no instance can be launched to serve it, the
     // Resident is poisoned and this call is not taken (its slot stays untouched: overwriting it
@@ -512,23 +525,50 @@ class Resident {
     }
     if (!usable()) return kNotTaken;
     ServerSlot* sl = ring_w + si;
-    const uint32_t lap1 = static_cast<uint32_t>(seq / kServerSlots) + 1u, nch = (P + kInlinePayload - 1) / kInlinePayload;
+    const uint32_t nch = (P + kInlinePayload - 1) / kInlinePayload;
     uint8_t* const out_dev = inline_pk   ? iouts.dev + size_t(si) * kInlineOutBytes
                              : repair_dev ? repair_dev
                                           : outs.dev + size_t(si) * kResidentOutBytes;
+    // The first lap of a tag epoch: no chunk the server wrote into this slot's output staging in
+    // the previous epoch may carry a tag of this one (the server zeroed the slot's own words and
+    // data area after serving its last lap; fec_kernels.hpp server_tag).  The previous occupant's
+    // rows were all collected, so the device writes nothing here until this slot is published.
+    if (vinl && seq >= kServerSlots && (seq / kServerSlots) % epoch == 0) {
+      std::memset(iouts.host + size_t(si) * kInlineOutBytes, 0, kInlineOutBytes);
+      std::atomic_thread_fence(std::memory_order_seq_cst);
+    }
+    uint64_t torn = ~0ull;  // QUICFEC_RESIDENT_TEST_TEAR: the chunk whose low half is stored late
     if (inline_pk) {
-      // the packets into the slot's data area (each chunk carries the lap), then the header
-      pack_inline(vinl + size_t(si) * kInlineSlotBytes, slab, offsets, G, P, lap1);
+      // the packets into the slot's data area (both halves of each chunk carry the tag), then the header
+      uint8_t* const area = vinl + size_t(si) * kInlineSlotBytes;
+      if (tear) torn = (seq * 7919u) % (uint64_t(G) * kServerPackets * nch);
+      pack_inline(area, slab, offsets, G, P, tag16, torn);
       __atomic_store_n(&sl->out, reinterpret_cast<uint64_t>(out_dev) | tag, __ATOMIC_RELAXED);
       __atomic_store_n(&sl->shape, uint64_t(P) | (uint64_t(G) << 16) | kServerInline | tag, __ATOMIC_RELAXED);
+      if (torn != ~0ull) {
+        // the header out, the chunk's tagged high half landed, its low half ~100 us later
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(100);
+        while (std::chrono::steady_clock::now() < until) __builtin_ia32_pause();
+        store_half(area + torn * 16, chunk_half(slab + offsets[torn / nch], P, uint32_t(torn % nch) * kInlinePayload, tag16));
+      }
     } else {
-      // groups after the first, then the first group and the header: the device reads the former
-      // only after it has seen every word of the latter with this lap's tag
-      for (uint32_t i = kServerPackets; i < G * kServerPackets; ++i) sl->addr[i] = (base + offsets[i]) | tag;
+      // groups after the first, then the first group and the header (every word tagged: the
+      // device checks each one it reads, whatever order they land in)
+      const bool late = tear && G > 1;  // tests: the later groups' words ~100 us after the header
+      if (!late)
+        for (uint32_t i = kServerPackets; i < G * kServerPackets; ++i) sl->addr[i] = (base + offsets[i]) | tag;
       std::atomic_thread_fence(std::memory_order_release);
       for (uint32_t i = 0; i < kServerPackets; ++i) __atomic_store_n(&sl->addr[i], (base + offsets[i]) | tag, __ATOMIC_RELAXED);
       __atomic_store_n(&sl->out, reinterpret_cast<uint64_t>(out_dev) | tag, __ATOMIC_RELAXED);
       __atomic_store_n(&sl->shape, uint64_t(P) | (uint64_t(G) << 16) | tag, __ATOMIC_RELEASE);
+      if (late) {
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(100);
+        while (std::chrono::steady_clock::now() < until) __builtin_ia32_pause();
+        for (uint32_t i = kServerPackets; i < G * kServerPackets; ++i)
+          __atomic_store_n(&sl->addr[i], (base + offsets[i]) | tag, __ATOMIC_RELAXED);
+      }
     }
     // through the BAR the stores sit in write-combining buffers until a serialising fence (mfence)
     if (vinl) std::atomic_thread_fence(std::memory_order_seq_cst);
@@ -537,19 +577,24 @@ class Resident {
     const uint64_t t_pub = now_ns();
     int rc = FEC_OK;
     const auto t_fail = std::chrono::steady_clock::now() + deadline;
-    // an inline call's rows are complete when every chunk of its staging carries the lap (the
-    // last one is watched first; chunks land in any order)
+    // An inline call's rows are complete when both 8-B halves of every chunk of its staging
+    // carry the tag (the last chunk is watched first; chunks, and the halves of one chunk, land
+    // in any order: the device's 16-B store is not assumed to arrive in one piece).
     const uint8_t* const stg = inline_pk ? iouts.host + size_t(si) * kInlineOutBytes : nullptr;
     uint32_t landed = 0;
-    auto rows_landed = [&]() {
-      if (__atomic_load_n(reinterpret_cast<const uint32_t*>(stg + size_t(G * nch - 1) * 16 + 12), __ATOMIC_ACQUIRE) != lap1)
-        return false;
-      while (landed < G * nch &&
-             __atomic_load_n(reinterpret_cast<const uint32_t*>(stg + size_t(landed) * 16 + 12), __ATOMIC_ACQUIRE) == lap1)
-        ++landed;
-      return landed == G * nch;
+    auto half_ok = [&](uint32_t h) {  // 8-B half h of the staging carries this lap's tag
+      return (__atomic_load_n(reinterpret_cast<const uint64_t*>(stg) + h, __ATOMIC_ACQUIRE) >> 48) == tag16;
     };
-    for (uint32_t spins = 0;; ++spins) {
+    auto rows_landed = [&]() {
+      if (!half_ok(2 * (G * nch - 1) + 1)) return false;
+      while (landed < 2 * G * nch && half_ok(landed)) ++landed;
+      return landed == 2 * G * nch;
+    };
+    if (seq == fail_at) {  // tests: this call's deadline passes at once
+      set_last_error("fec_encode_batch: QUICFEC_RESIDENT_TEST_FAIL_AT");
+      rc = FEC_ERR_HIP;
+    }
+    for (uint32_t spins = 0; rc == FEC_OK; ++spins) {
       if (inline_pk ? rows_landed() : __atomic_load_n(dw, __ATOMIC_ACQUIRE) == seq + 1) break;
       // no instance serving (never launched, or it left): launch one from its progress mark
       if ((spins & 15u) == 0 && !instance_alive()) {
@@ -566,31 +611,42 @@ class Resident {
     }
     const uint64_t t_done = now_ns();
     if (rc != FEC_OK) {
-      // Not served.  Turn the slot into one with nothing to do (the slots after it are served in
-      // order), poison the Resident (never relaunched), and ask a running instance to leave.  An
-      // instance that read an addressed slot before the rewrite may still write the caller's
-      // repair rows and read its slab: wait, bounded, until it has served this seq or left.  Past
-      // that bound the device is hung, and the caller's buffers handed to this call must not be
-      // reused (include/fec_xor_simd.h, fec_encode_batch).  An inline slot's reads and writes are
-      // the Resident's own memory: nothing of the caller's to wait for.
-      __atomic_store_n(&sl->shape, uint64_t(P) | tag, __ATOMIC_RELEASE);
-      if (vinl) std::atomic_thread_fence(std::memory_order_seq_cst);
+      // Not served in time, or no instance can be launched (this call's deadline passed, or
+      // another call poisoned the Resident).  Poison it (never relaunched; the stop word asks a
+      // running instance to leave) and wait, bounded, until the instance has left: its done word
+      // for this seq is then final.  The slot is not rewritten, so whether the device served it
+      // never depends on a race with the host.  Served: the rows are in place (an instance's
+      // stores are performed before its exited word), and the call succeeds.  Not served: the
+      // device read nothing of this call's after the instance left, so the call is not taken and
+      // runs on the coalescer path like every later legacy call.  An instance that does not leave
+      // within the bound is hung: the call fails, and the caller's buffers handed to it must not
+      // be reused (include/fec_xor_simd.h, fec_encode_batch).
       poison();
       const auto t_drain = std::chrono::steady_clock::now() + deadline;
-      const ServerControl* c = reinterpret_cast<const ServerControl*>(ctl.host);
-      for (uint32_t spins = 0; !inline_pk && instance_alive() && __atomic_load_n(&c->progress, __ATOMIC_ACQUIRE) <= seq &&
-                               __atomic_load_n(dw, __ATOMIC_ACQUIRE) != seq + 1 && std::chrono::steady_clock::now() < t_drain;
-           ++spins)
-        backoff(spins);
-    } else if (inline_pk) {
+      for (uint32_t spins = 0; instance_alive() && std::chrono::steady_clock::now() < t_drain; ++spins) backoff(spins);
+      if (!instance_alive()) {
+        const bool served = __atomic_load_n(dw, __ATOMIC_ACQUIRE) == seq + 1 && (!inline_pk || rows_landed());
+        rc = served ? FEC_OK : kNotTaken;
+      }
+    }
+    if (rc == FEC_OK && inline_pk) {
       for (uint32_t g = 0; g < G; ++g)
-        for (uint32_t c = 0; c < nch; ++c)
-          std::memcpy(repair_out + size_t(g) * P + c * kInlinePayload, stg + (size_t(g) * nch + c) * 16,
-                      std::min(kInlinePayload, P - c * kInlinePayload));
-    } else if (!repair_dev) {
+        for (uint32_t c = 0; c < nch; ++c) {
+          const uint8_t* ch = stg + (size_t(g) * nch + c) * 16;
+          uint8_t* dst = repair_out + size_t(g) * P + c * kInlinePayload;
+          const uint32_t n = std::min(kInlinePayload, P - c * kInlinePayload);
+          std::memcpy(dst, ch, std::min(6u, n));
+          if (n > 6) std::memcpy(dst + 6, ch + 8, n - 6);
+        }
+    } else if (rc == FEC_OK && !repair_dev) {
       std::memcpy(repair_out, outs.host + size_t(si) * kResidentOutBytes, size_t(G) * P);
     }
     collected[si].store(seq + 1, std::memory_order_release);
+    if (rc == kNotTaken) {  // counted on the path that runs it
+      g_res_calls.fetch_sub(1, std::memory_order_relaxed);
+      if (inline_pk) g_res_inline.fetch_sub(1, std::memory_order_relaxed);
+      return rc;
+    }
     g_res_pre_ns.fetch_add(t_pub - t_enter, std::memory_order_relaxed);
     g_res_wait_ns.fetch_add(t_done - t_pub, std::memory_order_relaxed);
     g_res_post_ns.fetch_add(now_ns() - t_done, std::memory_order_relaxed);
@@ -645,11 +701,14 @@ class Resident {
   std::atomic<bool> broken{false};
   std::chrono::milliseconds deadline{10000};  // QUICFEC_RESIDENT_DEADLINE_MS
   bool no_launch = false;                     // QUICFEC_RESIDENT_TEST_NOLAUNCH
+  bool tear = false;                          // QUICFEC_RESIDENT_TEST_TEAR
+  uint64_t fail_at = ~0ull;                   // QUICFEC_RESIDENT_TEST_FAIL_AT
+  uint32_t epoch = kServerEpoch;              // QUICFEC_RESIDENT_TEST_EPOCH
   std::atomic<bool> outs_ready{false};
   // The slots as the host writes them and as the device reads them: the page-locked ring, or
   // (setup_vram) one address for both, uncached device memory the host writes through the BAR.
   ServerSlot* ring_w = nullptr;
-  const ServerSlot* ring_d = nullptr;
+  ServerSlot* ring_d = nullptr;
   uint8_t* vinl = nullptr;  // VRAM ring: the slots' inline data areas (kInlineSlotBytes each)
   Pinned iouts;             // VRAM ring: the inline slots' tagged output staging (kInlineOutBytes each)
 
@@ -660,8 +719,6 @@ class Resident {
   // Any failure leaves the page-locked ring in place.  The device memory is never freed (like
   // the rest of a Resident, it goes with the process).
   void setup_vram() {
-    // zeroed: no chunk with a lap word (lap + 1 >= 1) before the device writes it
-    if (!alloc_coherent(iouts, size_t(kInlineOutBytes) * kServerSlots)) return;
     int large_bar = 0;
     if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, device) != hipSuccess || !large_bar) {
       (void)hipGetLastError();
@@ -678,9 +735,12 @@ class Resident {
       std::atomic_thread_fence(std::memory_order_seq_cst);
       ok = hipMemcpy(back, vr, sizeof(back), hipMemcpyDeviceToHost) == hipSuccess && std::memcmp(back, probe, sizeof(back)) == 0;
     }
-    // no header word with lap 0's tag, no chunk with lap 0's word (lap + 1 = 1)
-    ok = ok && hipMemsetAsync(vr, 0xFF, ring_bytes, stream) == hipSuccess && hipMemsetAsync(vi, 0, inl_bytes, stream) == hipSuccess &&
+    // no word and no chunk half with a tag (tags are 1 .. epoch)
+    ok = ok && hipMemsetAsync(vr, 0, ring_bytes, stream) == hipSuccess && hipMemsetAsync(vi, 0, inl_bytes, stream) == hipSuccess &&
          hipStreamSynchronize(stream) == hipSuccess;
+    // the inline slots' output staging, only once the VRAM ring is usable (zeroed: no tagged half
+    // before the device writes one)
+    ok = ok && alloc_coherent(iouts, size_t(kInlineOutBytes) * kServerSlots);
     if (!ok) {
       (void)hipGetLastError();
       if (vr) (void)hipFree(vr);
@@ -688,7 +748,7 @@ class Resident {
       return;
     }
     ring_w = static_cast<ServerSlot*>(vr);
-    ring_d = static_cast<const ServerSlot*>(vr);
+    ring_d = static_cast<ServerSlot*>(vr);
     vinl = static_cast<uint8_t*>(vi);
     g_res_vram.fetch_add(1, std::memory_order_relaxed);
   }
@@ -710,30 +770,53 @@ class Resident {
     return found;
   }
 
+  // One 8-B half of an inline chunk: payload bytes [off, off + 6) of a packet of P bytes (zero
+  // past P) and the tag in the top two bytes (fec_kernels.hpp kServerInline).
+  static uint64_t chunk_half(const uint8_t* src, uint32_t P, uint32_t off, uint32_t tag16) {
+    uint64_t w = 0;
+    if (off + 8 <= P) {
+      std::memcpy(&w, src + off, 8);
+      w &= 0x0000FFFFFFFFFFFFull;
+    } else if (off < P) {
+      std::memcpy(&w, src + off, std::min(6u, P - off));
+    }
+    return w | (uint64_t(tag16) << 48);
+  }
+
+  static void store_half(uint8_t* p, uint64_t w) { *reinterpret_cast<volatile uint64_t*>(p) = w; }
+
   // An inline slot's packets into its data area through the BAR (fec_kernels.hpp kServerInline):
-  // packet p = g * 10 + j as nch 16-B chunks, payload bytes [12c, 12c + 12) and lap1 in the
-  // fourth word; each chunk one 16-B store (write-combined).
+  // packet p = g * 10 + j as nch 16-B chunks, each two 8-B halves of 6 payload bytes and the tag;
+  // each chunk one 16-B store (write-combined).  torn (tests, QUICFEC_RESIDENT_TEST_TEAR): that
+  // chunk gets only its high half here; the caller stores the low half after the header.
   static void pack_inline(uint8_t* area, const uint8_t* slab, const uint32_t* offsets, uint32_t G, uint32_t P,
-                          uint32_t lap1) {
-    typedef uint32_t v4u __attribute__((vector_size(16)));
+                          uint32_t tag16, uint64_t torn) {
+    typedef uint64_t v2u __attribute__((vector_size(16)));
     const uint32_t nch = (P + kInlinePayload - 1) / kInlinePayload;
-    const uint32_t nfast = P >= 16 ? (P - 16) / kInlinePayload + 1 : 0;  // chunks whose 16-B read stays in the packet
+    const uint32_t nfast = P >= 14 ? (P - 14) / kInlinePayload + 1 : 0;  // chunks whose two 8-B reads stay in the packet
+    const uint64_t tg = uint64_t(tag16) << 48, lo48 = 0x0000FFFFFFFFFFFFull;
     for (uint32_t p = 0; p < G * kServerPackets; ++p) {
       const uint8_t* src = slab + offsets[p];
-      volatile v4u* dst = reinterpret_cast<volatile v4u*>(area + size_t(p) * nch * 16);
+      volatile v2u* dst = reinterpret_cast<volatile v2u*>(area + size_t(p) * nch * 16);
+      if (torn / nch == p) {
+        // the test's torn packet: every chunk but the torn one whole; of that one only the tagged
+        // high half, its low half left as the previous lap wrote it
+        const uint32_t ct = static_cast<uint32_t>(torn % nch);
+        for (uint32_t c = 0; c < nch; ++c)
+          if (c != ct)
+            dst[c] = v2u{chunk_half(src, P, c * kInlinePayload, tag16), chunk_half(src, P, c * kInlinePayload + 6, tag16)};
+        store_half(area + (size_t(p) * nch + ct) * 16 + 8, chunk_half(src, P, ct * kInlinePayload + 6, tag16));
+        continue;
+      }
       uint32_t c = 0;
       for (; c < nfast; ++c) {
-        v4u v;
-        std::memcpy(&v, src + size_t(c) * kInlinePayload, 16);
-        v[3] = lap1;
-        dst[c] = v;
+        uint64_t a, b;
+        std::memcpy(&a, src + size_t(c) * kInlinePayload, 8);
+        std::memcpy(&b, src + size_t(c) * kInlinePayload + 6, 8);
+        dst[c] = v2u{(a & lo48) | tg, (b & lo48) | tg};
       }
-      for (; c < nch; ++c) {
-        v4u v = {0u, 0u, 0u, 0u};
-        std::memcpy(&v, src + size_t(c) * kInlinePayload, std::min(kInlinePayload, P - c * kInlinePayload));
-        v[3] = lap1;
-        dst[c] = v;
-      }
+      for (; c < nch; ++c)
+        dst[c] = v2u{chunk_half(src, P, c * kInlinePayload, tag16), chunk_half(src, P, c * kInlinePayload + 6, tag16)};
     }
   }
 
@@ -784,7 +867,7 @@ class Resident {
     const hipError_t e = bd.ok ? launch_legacy_server(ring_d, vinl, reinterpret_cast<uint64_t*>(done.dev),
                                                       reinterpret_cast<ServerControl*>(ctl.dev), start, g, idle_ticks,
                                                       life_ticks, stamps.host ? reinterpret_cast<uint64_t*>(stamps.dev) : nullptr,
-                                                      stream)
+                                                      epoch, stream)
                                : hipErrorInvalidDevice;
     if (e != hipSuccess) {
       (void)hipGetLastError();
@@ -919,6 +1002,16 @@ QFEC_EXPORT int fec_coalesce_stats(FECCoalesceStats* out, int reset) {
   out->resident_post_ns = g_res_post_ns.load();
   out->resident_inline = g_res_inline.load();
   out->resident_vram = g_res_vram.load();
+  out->resident_bad_slots = 0;
+  out->resident_scrubs = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (auto& kv : g_resident)
+      if (kv.second) {
+        out->resident_bad_slots += kv.second->bad_slots();
+        out->resident_scrubs += kv.second->scrubs();
+      }
+  }
   if (reset) {
     g_res_calls = 0;
     g_res_launches = 0;

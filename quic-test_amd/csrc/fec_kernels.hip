@@ -71,6 +71,16 @@ constexpr int kCoefBytes = 2048;
 // and dword instead of 6 v_perm + 2 v_bitop3 + 2 v_xor, and one v_bitop3 per pair on the
 // XOR row instead of two v_xor.
 constexpr int kPairMac = 4096;
+// encode_v16 / encode_bits (tiled, P % 16 == 0, every row of the code in this launch): the
+// workgroup's parity rows -- one contiguous window of tile * R * P bytes in HBM -- are staged in
+// the LDS the launch already reserves for its occupancy cap and stored by consecutive lanes as
+// consecutive 16-B pieces, so only the window's two end lines are partial.  Stored by the lanes
+// that computed them, a 1200-B row starts 48 B into a 128-B line and one store instruction
+// covers the end of one group's row and the start of another's: each row's edge lines leave as
+// pieces of different instructions (PMC writes 1.046x algorithmic at k=10 r=3, 1.053x at k=20
+// r=5).
+constexpr int kStageRows = 8192;
+constexpr int kEncodeStageDefault = 0;  // QUICFEC_ENCODE_STAGE unset
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
@@ -186,6 +196,15 @@ __device__ __forceinline__ const uint8_t* packet_ptr(const uint8_t* data, const 
   }
 }
 
+// kStageRows: after the workgroup's barrier, its staged window (bytes, a multiple of 16) leaves
+// LDS as consecutive 16-B pieces from consecutive lanes.
+template <int POL>
+__device__ __forceinline__ void stage_rows_out(const uint8_t* lds, uint8_t* dst, uint32_t bytes) {
+  __syncthreads();
+  for (uint32_t o = threadIdx.x * 16u; o < bytes; o += blockDim.x * 16u)
+    st16<POL>(dst + o, *reinterpret_cast<const u32x4*>(lds + o));
+}
+
 // ---------------------------------------------------------------------------------
 // Encode, 16-byte columns.  K > 0: compile-time group size, all K loads issued before
 // the arithmetic.  K == 0: runtime k, loop.  Rows [row0, row0 + R) of the parity; when
@@ -213,25 +232,33 @@ __global__ __launch_bounds__(512) void encode_v16(const uint8_t* __restrict__ da
   // is always 0.
   extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];
   if (never) occupancy_lds[threadIdx.x] = 0;
-  uint32_t gl, col;
+  // kStageRows: the rows through LDS (the launcher sizes the dynamic LDS for the window)
+  const bool stage = (POL & kStageRows) != 0 && tile > 0 && (P & 15u) == 0 && row0 == 0 && r_total == static_cast<uint32_t>(R);
+  uint32_t gl, col, gtile = 0, glocal = 0;
+  bool active = true;
   if (tile > 0) {
     const uint32_t lane = threadIdx.x;
     gl = lane / cpp;
     col = lane - gl * cpp;
-    if (gl >= tile) return;
-    gl += xcd_tile(blockIdx.x, gridDim.x) * tile;
-    if (gl >= groups) return;
+    glocal = gl;
+    active = gl < tile;
+    gtile = xcd_tile(blockIdx.x, gridDim.x) * tile;
+    gl += gtile;
+    active = active && gl < groups;
   } else {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nthreads) return;
+    active = t < nthreads;
     gl = t / cpp;
     col = t - gl * cpp;
   }
+  // (staged: an idle lane stays for the workgroup's barrier)
+  if (!active && !stage) return;
   const uint64_t g = g_first + gl;
   const uint32_t k = K > 0 ? static_cast<uint32_t>(K) : k_rt;
   const size_t coff = col_off16(col, P);
 
   u32x4 acc[R];
+  if (active) {
   if constexpr (K > 0) {
     u32x4 d[K];
 #pragma unroll
@@ -297,10 +324,22 @@ __global__ __launch_bounds__(512) void encode_v16(const uint8_t* __restrict__ da
       }
     }
   }
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    st16<POL>(parity + (g * r_total + row0 + static_cast<uint32_t>(i)) * static_cast<uint64_t>(P) + coff, acc[i]);
   }
+  if (!stage) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      st16<POL>(parity + (g * r_total + row0 + static_cast<uint32_t>(i)) * static_cast<uint64_t>(P) + coff, acc[i]);
+    }
+    return;
+  }
+  // staged: the tile's rows (tile groups x R rows, back to back as in HBM) into LDS, then out
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      *reinterpret_cast<u32x4*>(occupancy_lds + (glocal * R + static_cast<uint32_t>(i)) * P + coff) = acc[i];
+  }
+  stage_rows_out<POL>(occupancy_lds, parity + (g_first + gtile) * R * static_cast<uint64_t>(P),
+                      static_cast<uint32_t>((groups - gtile < tile ? groups - gtile : tile) * R * P));
 }
 
 // ---------------------------------------------------------------------------------
@@ -321,32 +360,53 @@ __global__ __launch_bounds__(512) void encode_bits(const uint8_t* __restrict__ d
                                                    uint64_t groups, uint32_t never) {
   extern __shared__ __attribute__((aligned(16))) uint8_t occupancy_lds[];
   if (never) occupancy_lds[threadIdx.x] = 0;
+  // kStageRows: the workgroup's 2 * tile groups' rows through LDS (the launcher sizes it)
+  const bool stage = (POL & kStageRows) != 0 && (P & 15u) == 0;
   const uint32_t lane = threadIdx.x;
-  uint32_t gl = lane / cpp;
-  const uint32_t c = lane - gl * cpp;
-  if (gl >= tile) return;
-  gl += xcd_tile(blockIdx.x, gridDim.x) * (2 * tile);
-  if (gl >= groups) return;
+  const uint32_t glocal = lane / cpp;
+  const uint32_t c = lane - glocal * cpp;
+  const uint32_t gtile = xcd_tile(blockIdx.x, gridDim.x) * (2 * tile);
+  const uint32_t gl = gtile + glocal;
+  const bool active = glocal < tile && gl < groups;
+  // (staged: an idle lane stays for the workgroup's barrier)
+  if (!active && !stage) return;
   const bool second = gl + tile < groups;
   const uint64_t g = g_first + gl, g2 = second ? g + tile : g;
   const uint32_t o = col_off16(c, P);
-  const uint8_t* base = data + g * K * static_cast<uint64_t>(P) + o;
-  const uint8_t* base2 = data + g2 * K * static_cast<uint64_t>(P) + o;
-  auto load = [&](int j, uint32_t(&x)[8]) {
-    const u32x4 a = ld16<POL>(base + static_cast<uint64_t>(j) * P), b = ld16<POL>(base2 + static_cast<uint64_t>(j) * P);
-    x[0] = a.x, x[1] = a.y, x[2] = a.z, x[3] = a.w;
-    x[4] = b.x, x[5] = b.y, x[6] = b.z, x[7] = b.w;
-  };
   uint32_t out[R][8];
-  bs::encode_stream<K, R, W>(load, out);
-#pragma unroll
-  for (int i = 0; i < R; ++i)
-    st16<POL>(parity + (g * R + i) * static_cast<uint64_t>(P) + o, u32x4{out[i][0], out[i][1], out[i][2], out[i][3]});
-  if (second) {
+  if (active) {
+    const uint8_t* base = data + g * K * static_cast<uint64_t>(P) + o;
+    const uint8_t* base2 = data + g2 * K * static_cast<uint64_t>(P) + o;
+    auto load = [&](int j, uint32_t(&x)[8]) {
+      const u32x4 a = ld16<POL>(base + static_cast<uint64_t>(j) * P), b = ld16<POL>(base2 + static_cast<uint64_t>(j) * P);
+      x[0] = a.x, x[1] = a.y, x[2] = a.z, x[3] = a.w;
+      x[4] = b.x, x[5] = b.y, x[6] = b.z, x[7] = b.w;
+    };
+    bs::encode_stream<K, R, W>(load, out);
+  }
+  if (!stage) {
 #pragma unroll
     for (int i = 0; i < R; ++i)
-      st16<POL>(parity + (g2 * R + i) * static_cast<uint64_t>(P) + o, u32x4{out[i][4], out[i][5], out[i][6], out[i][7]});
+      st16<POL>(parity + (g * R + i) * static_cast<uint64_t>(P) + o, u32x4{out[i][0], out[i][1], out[i][2], out[i][3]});
+    if (second) {
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+        st16<POL>(parity + (g2 * R + i) * static_cast<uint64_t>(P) + o, u32x4{out[i][4], out[i][5], out[i][6], out[i][7]});
+    }
+    return;
   }
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      *reinterpret_cast<u32x4*>(occupancy_lds + (glocal * R + static_cast<uint32_t>(i)) * P + o) =
+          u32x4{out[i][0], out[i][1], out[i][2], out[i][3]};
+      if (second)
+        *reinterpret_cast<u32x4*>(occupancy_lds + ((glocal + tile) * R + static_cast<uint32_t>(i)) * P + o) =
+            u32x4{out[i][4], out[i][5], out[i][6], out[i][7]};
+    }
+  }
+  stage_rows_out<POL>(occupancy_lds, parity + (g_first + gtile) * R * static_cast<uint64_t>(P),
+                      static_cast<uint32_t>((groups - gtile < 2 * tile ? groups - gtile : 2 * tile) * R * P));
 }
 
 // Encode, one lane per byte (any size / alignment).  All r rows.
@@ -1771,19 +1831,20 @@ __device__ __forceinline__ u64x2 sys_load_16(const uint64_t* p) {
 // The VRAM ring (inl != nullptr, fec_kernels.hpp kServerInline): the poll reads the slots from
 // device memory -- local, not a PCIe round trip -- and an inline slot's work item is one 16-B
 // chunk column (g, c): its 10 chunks loaded from the slot's data area (or, at the head of the
-// run, from the poll's prefetch), their lap words checked, the 12 payload bytes XORed and
-// stored with the lap word as chunk (g, c) of the slot's output staging.  A chunk whose lap
-// word is not yet this slot's (the host's stores through the BAR landed in another order)
-// marks the slot bad: the run is served up to the first bad slot and the poll comes back for
-// the rest.  The host takes an inline slot's rows by their lap words, so its done word needs
-// no acknowledgement of the row stores: a batch of inline slots only waits for them when it
-// also holds an addressed slot.
-__global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot* __restrict__ ring,
-                                                                const uint8_t* __restrict__ inl,
+// run, from the poll's prefetch), the tags of both 8-B halves of each checked, the 12 payload
+// bytes XORed and stored with the tag in both halves as chunk (g, c) of the slot's output
+// staging.  A half whose tag is not yet this slot's (the host's stores through the BAR landed
+// in another order, or a 16-B store arrived as two pieces) marks the slot bad: the run is served
+// up to the first bad slot and the poll comes back for the rest.  The host takes an inline
+// slot's rows by their tags, so its done word needs no acknowledgement of the row stores: a
+// batch of inline slots only waits for them when it also holds an addressed slot (or scrubs a
+// slot at an epoch boundary, fec_kernels.hpp server_tag).
+__global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __restrict__ ring,
+                                                                uint8_t* __restrict__ inl,
                                                                 uint64_t* __restrict__ done,
                                                                 ServerControl* __restrict__ ctl, uint64_t start_seq,
                                                                 uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                                                uint64_t* __restrict__ stamps) {
+                                                                uint64_t* __restrict__ stamps, uint32_t epoch) {
   __shared__ uint64_t s_next;
   __shared__ uint32_t s_n, s_exit, s_stop, s_ack;
   __shared__ uint32_t s_first[kServerPoll + 1];  // work items before slot i of the run
@@ -1797,9 +1858,12 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
   __shared__ u32x4 s_pre[kServerThreads];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   uint64_t t0 = 0, t_last = 0;  // thread 0 only
+  uint64_t n_bad = 0, n_scrub = 0;  // thread 0 only: the diagnostic counters, continued from the last instance's
   if (tid == 0) {
     s_next = start_seq;
     t0 = t_last = static_cast<uint64_t>(wall_clock64());
+    n_bad = *reinterpret_cast<const volatile uint64_t*>(&ctl->bad_slots);
+    n_scrub = *reinterpret_cast<const volatile uint64_t*>(&ctl->scrubs);
   }
   lds_barrier();
   // Diagnostic stamps (stamps != nullptr, QUICFEC_RESIDENT_STAMPS): thread 0's wall clock at the
@@ -1830,7 +1894,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
     lds_barrier();
     if (tid < 64) {
       const uint64_t seq = next + lane;
-      const uint64_t tag = (seq / kServerSlots) & 0xFFu;
+      const uint64_t tag = server_tag(seq, epoch);
       bool ok = lane < kServerPoll;
       bool inline_slot = false;
       if (ok) {
@@ -1911,11 +1975,12 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
 #pragma unroll
             for (uint32_t j = 0; j < kServerPackets; ++j) __asm__ volatile("" : "+v"(v[j]));
           }
-          const uint32_t lap1 = static_cast<uint32_t>(seq / kServerSlots) + 1u;
+          // both 8-B halves of every chunk carry this lap's tag in their top two bytes
+          const uint32_t tag = server_tag(seq, epoch);
           bool fresh = true;
           u32x4 acc = v[0];
 #pragma unroll
-          for (uint32_t j = 0; j < kServerPackets; ++j) fresh = fresh && v[j].w == lap1;
+          for (uint32_t j = 0; j < kServerPackets; ++j) fresh = fresh && (v[j].y >> 16) == tag && (v[j].w >> 16) == tag;
 #pragma unroll
           for (uint32_t j = 1; j < kServerPackets; ++j) acc ^= v[j];
           if (!fresh) {
@@ -1929,7 +1994,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
           // word from host memory -- the partial-line writes and the done word behind them left
           // the device only when a read to the host pushed them; profiles/r04_vram_store_forms.txt)
           sys_store_16b(reinterpret_cast<uint8_t*>(s_head[i][0] & kServerAddrMask) + (static_cast<uint64_t>(g) * cpp + col) * 16u,
-                        u32x4{acc.x, acc.y, acc.z, lap1});
+                        u32x4{acc.x, (acc.y & 0xFFFFu) | (tag << 16), acc.z, (acc.w & 0xFFFFu) | (tag << 16)});
           continue;
         }
         const uint32_t coff = col * 16u + 16u <= P ? col * 16u : P - 16u;
@@ -1949,7 +2014,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           // tagged like the header: in a VRAM ring the host's stores through the BAR carry no
           // order, and a word of the previous lap marks the slot bad (served by a later poll)
-          const uint64_t tag = ((next + i) / kServerSlots) & 0xFFu;
+          const uint64_t tag = server_tag(next + i, epoch);
           bool fresh = true;
 #pragma unroll
           for (uint32_t j = 0; j < kServerPackets; ++j) fresh = fresh && (ad[j] >> kServerTagShift) == tag;
@@ -1989,14 +2054,35 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(const ServerSlot
       if (s_ack != 0) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       if (stamps != nullptr && tid == 0) st_t[4] = static_cast<uint64_t>(wall_clock64());
       lds_barrier();
-      // the run up to its first slot with a chunk not yet landed (VRAM ring; n in any other case)
+      // the run up to its first slot with a word not yet landed (n when every word had)
       uint32_t n_ok = n;
-      if (tid < 64) {
-        for (uint32_t k = 0; k < n; ++k)
-          if (s_bad[k] != 0) {
-            n_ok = k;
-            break;
-          }
+      bool scrub = false;
+      for (uint32_t k = 0; k < n; ++k) {
+        if (s_bad[k] != 0) {
+          n_ok = k;
+          break;
+        }
+        scrub = scrub || server_scrub_after(next + k, epoch);
+      }
+      if (tid == 0 && n_ok < n) sys_store_relaxed(&ctl->bad_slots, ++n_bad);
+      if (scrub) {
+        // The last lap of an epoch (fec_kernels.hpp server_tag): zero the served slot's words and
+        // inline data area before its done word, so no word of this epoch can match a tag of the
+        // next.  Its next occupant writes only after it has seen the done word.
+        constexpr uint32_t kSlotPieces = sizeof(ServerSlot) / 16u;
+        const uint32_t pieces = kSlotPieces + (inl != nullptr ? kInlineSlotBytes / 16u : 0u);
+        for (uint32_t k = 0; k < n_ok; ++k) {
+          const uint64_t seq = next + k;
+          if (!server_scrub_after(seq, epoch)) continue;
+          uint8_t* slot = reinterpret_cast<uint8_t*>(ring + seq % kServerSlots);
+          uint8_t* area = inl != nullptr ? inl + (seq % kServerSlots) * kInlineSlotBytes : nullptr;
+          for (uint32_t c = tid; c < pieces; c += kServerThreads)
+            sys_store_16b(c < kSlotPieces ? slot + c * 16u : area + (c - kSlotPieces) * 16u, u32x4{0u, 0u, 0u, 0u});
+          if (tid == 0) ++n_scrub;
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every zero in place before the done words
+        lds_barrier();
+        if (tid == 0) sys_store_relaxed(&ctl->scrubs, n_scrub);
       }
       if (tid < n_ok) sys_store_relaxed(&done[(next + tid) % kServerSlots], next + tid + 1);
       if (tid == 0) {
@@ -2116,7 +2202,8 @@ hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
       const int waves = a.waves_per_cu ? a.waves_per_cu
                                        : env_waves("QUICFEC_ENCODE_WAVES", xor_waves ? kEncodeXorWavesPerCU
                                                                                      : blocks_per_cu * static_cast<int>(bs / 64));
-      const uint32_t smem = occupancy_cap_lds(waves, bs / 64);
+      uint32_t smem = occupancy_cap_lds(waves, bs / 64);
+      if constexpr ((POL & kStageRows) != 0) smem = std::max<uint32_t>(smem, tile * R * a.P);
       hipLaunchKernelGGL((encode_v16<K, R, OFF, FIRST, POL>), dim3(blocks), dim3(bs), smem, s, a.data,
                          a.offsets, a.parity, g0, n, cpp, a.P, a.k, a.r, row0,
                          static_cast<const Tab*>(a.tables), tile, gn, 0u);
@@ -2144,7 +2231,8 @@ hipError_t run_encode_bits(const EncodeLaunch& a, hipStream_t s) {
     const uint32_t blocks = static_cast<uint32_t>((gn + 2 * tile - 1) / (2 * tile));
     // uncapped: k=20 r=5 at 12 / 18 / 24 waves per CU within 0.2% (3 waves per SIMD by VGPRs)
     const int waves = a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_ENCODE_WAVES", 0);
-    const uint32_t smem = occupancy_cap_lds(waves, bs / 64);
+    uint32_t smem = occupancy_cap_lds(waves, bs / 64);
+    if constexpr ((POL & kStageRows) != 0) smem = std::max<uint32_t>(smem, 2 * tile * R * a.P);
     hipLaunchKernelGGL((encode_bits<K, R, W, POL>), dim3(blocks), dim3(bs), smem, s, a.data, a.parity, g0, cpp, a.P,
                        tile, gn, 0u);
     const hipError_t e = hipGetLastError();
@@ -2159,6 +2247,13 @@ hipError_t run_encode_bits(const EncodeLaunch& a, hipStream_t s) {
 bool use_encode_bits(uint32_t r) {
   const int mode = env_waves("QUICFEC_ENCODE_BITS", -1);
   return mode == 1 || (mode < 0 && r >= 4);
+}
+
+// kStageRows for a launch whose workgroup window (groups_per_block * r * P bytes) fits the LDS a
+// workgroup may take: QUICFEC_ENCODE_STAGE=1 on, 0 off (read per launch: A/B in one process).
+bool use_stage_rows(const EncodeLaunch& a, uint32_t groups_per_block) {
+  const int mode = env_waves("QUICFEC_ENCODE_STAGE", kEncodeStageDefault);
+  return mode == 1 && a.P % 16 == 0 && uint64_t(groups_per_block) * a.r * a.P <= 64u * 1024u;
 }
 
 template <int OFF>
@@ -2218,11 +2313,19 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
       // QUICFEC_ENCODE_BITS_WINDOW: packets in flight per lane (4; 2: 5.70 ms, 8: 5.28, 20: 5.91-6.03).
       if (a.P <= 8192 && use_encode_bits(a.r)) {
         const int w = env_waves("QUICFEC_ENCODE_BITS_WINDOW", 4);
-        if (a.k == 20 && a.r == 5) return w >= 8 ? run_encode_bits<20, 5, 8>(a, s) : run_encode_bits<20, 5, 4>(a, s);
-        if (a.k == 10 && a.r == 3) return run_encode_bits<10, 3, 4>(a, s);
+        const uint32_t cpp = (a.P + 15u) / 16u;
+        const bool stg = use_stage_rows(a, 2 * pick_tile(cpp, a.k, a.P));
+        if (a.k == 20 && a.r == 5) {
+          if (stg) return run_encode_bits<20, 5, 4, kNtStore | kStageRows>(a, s);
+          return w >= 8 ? run_encode_bits<20, 5, 8>(a, s) : run_encode_bits<20, 5, 4>(a, s);
+        }
+        if (a.k == 10 && a.r == 3) return stg ? run_encode_bits<10, 3, 4, kNtStore | kStageRows>(a, s) : run_encode_bits<10, 3, 4>(a, s);
       }
-      if (a.k == 10 && a.r == 3)
+      if (a.k == 10 && a.r == 3) {
+        if (pair && use_stage_rows(a, pick_tile((a.P + 15u) / 16u, a.k, a.P)))
+          return run_encode_v16<10, 3, 0, true, kNtStore | kPairMac | kStageRows>(a, 0, s);
         return pair ? run_encode_v16<10, 3, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<10, 3, 0, true>(a, 0, s);
+      }
       if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 0, true>(a, 0, s);
       if (a.k == 20 && a.r == 5)
         return pair ? run_encode_v16<20, 5, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<20, 5, 0, true>(a, 0, s);
@@ -2700,11 +2803,12 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
   return hipSuccess;
 }
 
-hipError_t launch_legacy_server(const ServerSlot* ring, const uint8_t* inl, uint64_t* done, ServerControl* ctl,
+hipError_t launch_legacy_server(ServerSlot* ring, uint8_t* inl, uint64_t* done, ServerControl* ctl,
                                 uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                uint64_t* stamps, hipStream_t s) {
+                                uint64_t* stamps, uint32_t epoch, hipStream_t s) {
+  if (epoch < 1u || epoch > kServerEpoch) return hipErrorInvalidValue;
   hipLaunchKernelGGL(legacy_server, dim3(1), dim3(kServerThreads), 0, s, ring, inl, done, ctl, start_seq, gen,
-                     idle_ticks, life_ticks, stamps);
+                     idle_ticks, life_ticks, stamps, epoch);
   return hipGetLastError();
 }
 

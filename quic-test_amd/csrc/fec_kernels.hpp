@@ -153,18 +153,38 @@ bool decode_needs_rec_off(const DecodeLaunch& a);
 // Whether launch_decode(a) runs a form that reads a compact codebook (coefficient bytes).
 bool decode_compact_tables(const DecodeLaunch& a);
 // ---- resident legacy encoder (fec_coalesce.cpp "resident server") ----
-// A ring of submission slots in page-locked, coherent host memory.  The host fills slot
-// seq % kServerSlots with a legacy call's groups: every word of a slot carries the slot's lap,
-// (seq / kServerSlots) & 0xFF, in its top byte, so the device recognises a complete slot by
-// the tags alone, whatever order its reads of the host's stores land in (the host writes the
-// groups after the first before the first group and the header, and the device reads those
-// only after it has seen the rest).  One resident workgroup serves the slots in seq order and
-// stores done[seq % kServerSlots] = seq + 1.  Calls are served without a kernel launch each.
+// A ring of submission slots (page-locked coherent host memory, or VRAM written through the BAR).
+// The host fills slot seq % kServerSlots with a legacy call's groups: every 8-B word of a slot
+// carries the slot's tag, server_tag(seq), in its top 16 bits, so the device recognises a
+// complete slot by the tags alone, whatever order its reads of the host's stores land in.  An
+// aligned 8-B store is the unit the host's stores are assumed to arrive in (x86 quadword
+// atomicity); nothing larger is assumed to arrive in one piece, so every 8-B word is
+// self-validating.  One resident workgroup serves the slots in seq order and stores
+// done[seq % kServerSlots] = seq + 1.  Calls are served without a kernel launch each.
+//
+// Tags and the epoch.  A slot's tag is (lap % epoch) + 1 with lap = seq / kServerSlots, so the
+// tags of one slot repeat every `epoch` laps (65535 by default; QUICFEC_RESIDENT_TEST_EPOCH for
+// tests).  A word left from the previous epoch could carry the current tag (a word written
+// exactly `epoch` laps ago and not since, e.g. a later group's address word under inline-only
+// calls), so the slot is scrubbed at every epoch boundary: the server zeroes the slot's words
+// and its inline data area after serving the last lap of an epoch, before that slot's done word
+// (its next occupant writes only after it has seen the done word, so the zeroes are in place
+// first), and the host zeroes the slot's inline output staging before publishing the first lap
+// of an epoch.  Within an epoch every tag of a slot is used once, so no stale word matches;
+// tag 0 (the zeroed state) never matches.
 constexpr uint32_t kServerSlots = 1024;
 constexpr uint32_t kServerMaxGroups = 8;  // groups per slot (legacy calls of 1..8 groups)
 constexpr uint32_t kServerPackets = 10;   // the legacy call's packets per group
-constexpr uint64_t kServerTagShift = 56;  // addresses below 2^56 (user virtual addresses)
+constexpr uint64_t kServerTagShift = 48;  // addresses below 2^48 (x86-64 user virtual addresses)
 constexpr uint64_t kServerAddrMask = (1ull << kServerTagShift) - 1;
+constexpr uint32_t kServerEpoch = 65535;  // laps per tag epoch (tags 1 .. epoch fit 16 bits)
+__host__ __device__ inline uint32_t server_tag(uint64_t seq, uint32_t epoch) {
+  return static_cast<uint32_t>((seq / kServerSlots) % epoch) + 1u;
+}
+// Whether the server scrubs the slot of seq after serving it (the last lap of an epoch).
+__host__ __device__ inline bool server_scrub_after(uint64_t seq, uint32_t epoch) {
+  return (seq / kServerSlots) % epoch == epoch - 1u;
+}
 struct alignas(64) ServerSlot {
   uint64_t out;             // tag | device address of the repair rows, row g at out + g * P
   uint64_t shape;           // tag | P (bits 0..15) | groups (bits 16..23; 0 = nothing to do) | kServerInline
@@ -174,24 +194,28 @@ struct alignas(64) ServerSlot {
 // calls live in uncached device memory that the host writes through the BAR, so the server's
 // poll and packet loads stay on the device.  An inline slot (shape bit kServerInline) carries
 // no addresses: its packets are copied by the host into the slot's data area, packet (g, j) as
-// chunks of 16 B -- 12 payload bytes (payload bytes [12c, 12c + 12) at chunk c, zero past P)
-// and, in the fourth 32-bit word, the slot's lap + 1 -- at chunk (g * 10 + j) * nch + c,
-// nch = ceil(P / 12).  Every chunk is self-validating like the header words: no ordering of the
-// host's stores through the BAR is assumed.  The rows come back the same way: an inline slot's
-// `out` is its output staging in page-locked host memory, repair chunk (g, c) -- payload bytes
-// [12c, 12c + 12) of row g and the lap + 1 word -- at out + (g * nch + c) * 16, and the host
-// takes the rows once every chunk carries the lap (the done word then only says "consumed").
+// 16-B chunks at chunk (g * 10 + j) * nch + c, nch = ceil(P / 12).  A chunk is two 8-B halves,
+// each 6 payload bytes and the slot's 16-bit tag in its top two bytes:
+//   bytes 0..5 = payload [12c, 12c + 6), bytes 6..7 = tag, bytes 8..13 = payload [12c + 6,
+//   12c + 12), bytes 14..15 = tag (payload zero past P),
+// so each half validates itself (a 16-B write-combined store may reach the device as two 8-B
+// pieces) and no ordering of the host's stores through the BAR is assumed.  The rows come back
+// the same way: an inline slot's `out` is its output staging in page-locked host memory, repair
+// chunk (g, c) in the same two-half form at out + (g * nch + c) * 16, and the host takes the rows
+// once both halves of every chunk carry the tag (the done word then only says "consumed").
 constexpr uint64_t kServerInline = 1ull << 24;
 constexpr uint32_t kInlineMaxGroups = 4;
 constexpr uint32_t kInlineMaxP = 1536;
-constexpr uint32_t kInlinePayload = 12;  // payload bytes of a 16-B chunk
+constexpr uint32_t kInlinePayload = 12;  // payload bytes of a 16-B chunk (6 per 8-B half)
 constexpr uint32_t kInlineSlotBytes = kInlineMaxGroups * kServerPackets * (kInlineMaxP / kInlinePayload) * 16;
 struct alignas(64) ServerControl {
   uint64_t stop;            // host -> device: leave at the next poll
   uint64_t pad0[7];
   uint64_t progress;        // device -> host: every seq below this has been served
   uint64_t exited;          // device -> host: generation of the last instance that left
-  uint64_t pad1[6];
+  uint64_t bad_slots;       // device -> host: polls that found a slot with a word not yet landed (diagnostic)
+  uint64_t scrubs;          // device -> host: slots scrubbed at an epoch boundary (diagnostic)
+  uint64_t pad1[4];
 };
 // One resident workgroup serving the ring from start_seq until it has found nothing to do for
 // idle_ticks, or lived life_ticks (wall-clock ticks, hipDeviceAttributeWallClockRate), or the
@@ -199,9 +223,10 @@ struct alignas(64) ServerControl {
 // stamps: nullptr, or 256 x 8 words of host memory for the diagnostic phase stamps (QUICFEC_RESIDENT_STAMPS).
 // inl: the inline data areas (kInlineSlotBytes per slot) when the ring is in VRAM, else nullptr;
 // then the host's stop word (host memory) is read by every 16th poll only, not every poll.
-hipError_t launch_legacy_server(const ServerSlot* ring, const uint8_t* inl, uint64_t* done, ServerControl* ctl,
+// epoch: laps per tag epoch (server_tag), 1 .. kServerEpoch.
+hipError_t launch_legacy_server(ServerSlot* ring, uint8_t* inl, uint64_t* done, ServerControl* ctl,
                                 uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                uint64_t* stamps, hipStream_t s);
+                                uint64_t* stamps, uint32_t epoch, hipStream_t s);
 
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);

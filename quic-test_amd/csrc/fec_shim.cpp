@@ -1321,7 +1321,12 @@ QFEC_EXPORT FECEncoderCtx* fec_encoder_new_device(double redundancy, uint32_t ma
 
 QFEC_EXPORT int fec_encoder_device(const FECEncoderCtx* ctx) { return ctx ? ctx->device : -1; }
 
-QFEC_EXPORT const char* fec_hip_version(void) { return "libfec_hip 0.1 gfx950"; }
+extern "C" const char qfec_src_hash[];  // src_hash.o, generated by src_hash.py at build time
+
+QFEC_EXPORT const char* fec_hip_version(void) {
+  static const std::string v = std::string("libfec_hip 0.2 gfx950 src=") + qfec_src_hash;
+  return v.c_str();
+}
 
 QFEC_EXPORT int fec_parity_matrix(uint32_t k, uint32_t r, uint8_t* out) {
   if (!out) return FEC_ERR_NULL;

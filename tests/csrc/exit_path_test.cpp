@@ -16,9 +16,26 @@
 // buffers; the *hostring modes keep the resident ring in page-locked host memory
 // (QUICFEC_RESIDENT_VRAM=0: the ring kind is fixed per process).
 //
-//   exit_path_test [resident|hostring|coalescer|pageable|nolaunch|mixed|mixed_hostring] [calls]
+// The ring's tag checks (fec_kernels.hpp server_tag):
+//  * tear: QUICFEC_RESIDENT_TEST_TEAR -- every inline call stores one chunk's tagged high half
+//    first and its low half ~100 us after the slot's header (a write-combined 16-B store evicted
+//    in two pieces), and every addressed call of several groups stores its later groups' address
+//    words ~100 us after the header.  The server must retry such a slot (resident_bad_slots > 0)
+//    and never serve it from the stale half or word.
+//  * epoch / epoch_hostring: a tag epoch of 2 laps (QUICFEC_RESIDENT_TEST_EPOCH) with the tear
+//    hook: slots 0, 5, 10, ... take 8-group addressed calls on even laps and one-group inline
+//    calls on odd laps, so an 8-group call's later address words from two laps back carry the
+//    current tag unless the epoch scrub zeroed them -- and the late stores make the server read
+//    those words before the new ones land.
+//  * poison_mt: 8 threads with a context each make one-group calls; the call of seq 600 fails as
+//    if its deadline had passed (QUICFEC_RESIDENT_TEST_FAIL_AT).  Every call of every thread --
+//    that one and the ones in flight when the Resident went out of service included -- must
+//    return 0 with the right row (served, or run on the coalescer path).
+//
+//   exit_path_test [resident|hostring|coalescer|pageable|nolaunch|mixed|mixed_hostring|tear|
+//                   epoch|epoch_hostring|poison_mt] [calls]
 //   -> one JSON line at exit: {"mode", "calls", "repairs_ok", "first_rc", "calls_after_exit", "names",
-//                              "resident_calls", "resident_inline", "resident_vram"}
+//                              "resident_calls", "resident_inline", "resident_vram", "bad_slots", "scrubs"}
 // Built by quic-test_amd/csrc/Makefile (target tests); run by tests/test_gpu_coalesce.py.
 #include <dlfcn.h>
 
@@ -29,6 +46,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <hip/hip_runtime_api.h>
@@ -43,7 +61,7 @@ std::mutex g_mu;
 std::string g_names;
 std::string g_mode = "resident";
 int g_calls = 0, g_first_rc = 0;
-unsigned long long g_resident_calls = 0, g_resident_inline = 0, g_resident_vram = 0;
+unsigned long long g_resident_calls = 0, g_resident_inline = 0, g_resident_vram = 0, g_bad = 0, g_scrubs = 0;
 bool g_ok = true;
 
 bool from_library(void* ret) {
@@ -67,10 +85,38 @@ void mark_exit() { g_exiting.store(true, std::memory_order_release); }
 
 void report() {
   std::printf("{\"mode\": \"%s\", \"calls\": %d, \"repairs_ok\": %s, \"first_rc\": %d, \"calls_after_exit\": %d, "
-              "\"names\": \"%s\", \"resident_calls\": %llu, \"resident_inline\": %llu, \"resident_vram\": %llu}\n",
+              "\"names\": \"%s\", \"resident_calls\": %llu, \"resident_inline\": %llu, \"resident_vram\": %llu, "
+              "\"bad_slots\": %llu, \"scrubs\": %llu}\n",
               g_mode.c_str(), g_calls, g_ok ? "true" : "false", g_first_rc, g_after.load(), g_names.c_str(), g_resident_calls,
-              g_resident_inline, g_resident_vram);
+              g_resident_inline, g_resident_vram, g_bad, g_scrubs);
   std::fflush(stdout);
+}
+
+// One thread of poison_mt: `calls` one-group calls of 10 x 1200 B on a context of its own,
+// every row checked against the XOR.  Returns false on any failure.
+bool poison_thread(int t, int calls) {
+  constexpr uint32_t K = 10, P = 1200;
+  FECEncoderCtx* ctx = fec_encoder_new(0.10, 1024);
+  if (!ctx) return false;
+  uint8_t* slab = static_cast<uint8_t*>(fec_alloc_slab(K * P));
+  uint8_t* rep = static_cast<uint8_t*>(fec_alloc_repair_buffer(P));
+  uint32_t offsets[K];
+  for (uint32_t j = 0; j < K; ++j) offsets[j] = j * P;
+  uint64_t x = 0x5EED0100u + uint64_t(t);
+  std::vector<uint8_t> want(P);
+  bool ok = true;
+  for (int c = 0; c < calls; ++c) {
+    for (uint32_t i = 0; i < K * P; i += 8) {
+      x = x * 6364136223846793005ull + 1442695040888963407ull;
+      std::memcpy(slab + i, &x, 8);
+    }
+    std::fill(want.begin(), want.end(), 0);
+    for (uint32_t j = 0; j < K; ++j)
+      for (uint32_t i = 0; i < P; ++i) want[i] ^= slab[j * P + i];
+    const int rc = fec_encode_batch(ctx, slab, offsets, 1, P, rep);
+    if (rc != 0 || std::memcmp(rep, want.data(), P) != 0) ok = false;
+  }
+  return ok;  // the context and buffers stay alive (a Go process exiting)
 }
 
 }  // namespace
@@ -108,6 +154,26 @@ int main(int argc, char** argv) {
     setenv("QUICFEC_RESIDENT_TEST_NOLAUNCH", "1", 1);
     setenv("QUICFEC_RESIDENT_DEADLINE_MS", "200", 1);
   }
+  const bool tear = g_mode == "tear", epoch = g_mode.rfind("epoch", 0) == 0;
+  if (tear || epoch) setenv("QUICFEC_RESIDENT_TEST_TEAR", "1", 1);
+  if (epoch) setenv("QUICFEC_RESIDENT_TEST_EPOCH", "2", 1);
+  if (g_mode == "epoch_hostring") setenv("QUICFEC_RESIDENT_VRAM", "0", 1);
+  if (g_mode == "poison_mt") {
+    setenv("QUICFEC_RESIDENT_TEST_FAIL_AT", "600", 1);
+    constexpr int kThreads = 8;
+    std::vector<std::thread> th;
+    std::vector<char> ok(kThreads, 0);
+    for (int t = 0; t < kThreads; ++t) th.emplace_back([t, calls, &ok] { ok[t] = poison_thread(t, calls / kThreads) ? 1 : 0; });
+    for (auto& x : th) x.join();
+    for (int t = 0; t < kThreads; ++t) g_ok = g_ok && ok[t] != 0;
+    g_calls = calls / kThreads * kThreads;
+    FECCoalesceStats st{};
+    fec_coalesce_stats(&st, 0);
+    g_resident_calls = st.resident_calls;
+    g_resident_vram = st.resident_vram;
+    std::atexit(mark_exit);
+    return 0;
+  }
   FECEncoderCtx* ctx = fec_encoder_new(0.10, 1024);
   if (!ctx) {
     std::printf("{\"skip\": \"no GPU\"}\n");
@@ -117,6 +183,9 @@ int main(int argc, char** argv) {
   // mixed: shapes on both sides of the inline bounds (<= 4 groups, P % 4 == 0, P <= 1536)
   static const uint32_t kShapes[][2] = {{1, 1200}, {4, 1536}, {2, 16}, {3, 100}, {1, 1201}, {5, 1200},
                                         {8, 1500}, {1, 2048}, {4, 20}, {2, 1538}, {1, 1500}, {6, 333}};
+  // tear: every inline shape, plus addressed calls of several groups from the page-locked slab
+  static const uint32_t kTearShapes[][2] = {{1, 1200}, {4, 1536}, {2, 16}, {3, 100}, {1, 1500}, {4, 20},
+                                            {2, 1224}, {5, 1200}, {8, 1500}, {3, 1201}};
   const bool pageable = g_mode == "pageable";
   uint8_t* slab_pin = static_cast<uint8_t*>(fec_alloc_slab(kSlab));
   uint8_t* rep_pin = static_cast<uint8_t*>(fec_alloc_repair_buffer(kMaxG * kMaxP));
@@ -130,13 +199,26 @@ int main(int argc, char** argv) {
   };
   std::vector<uint8_t> want(kMaxG * kMaxP);
   for (int c = 0; c < calls; ++c) {
-    const uint32_t G = mixed ? kShapes[c % 12][0] : 1, P = mixed ? kShapes[c % 12][1] : 1200;
-    uint8_t* slab = (mixed ? (c / 12) % 2 == 1 : pageable) ? slab_pg : slab_pin;
-    uint8_t* repair = (mixed ? (c / 24) % 2 == 1 : pageable) ? rep_pg : rep_pin;
-    for (uint32_t i = 0; i < G * K; ++i) offsets[i] = mixed ? rnd() % (kSlab - P + 1) : i * P;
-    for (uint32_t i = 0; i < kSlab; i += 4) {
-      const uint32_t v = rnd();
-      std::memcpy(slab + i, &v, 4);
+    uint32_t G = mixed ? kShapes[c % 12][0] : 1, P = mixed ? kShapes[c % 12][1] : 1200;
+    if (tear) G = kTearShapes[c % 10][0], P = kTearShapes[c % 10][1];
+    // epoch: call c goes to slot c % 1024 on lap c / 1024 (one thread, one Resident)
+    if (epoch) G = ((c % 1024) % 5 == 0 && (c / 1024) % 2 == 0) ? 8 : 1, P = 1200;
+    const bool scattered = mixed || tear || epoch;
+    uint8_t* slab = (mixed ? (c / 12) % 2 == 1 : tear ? (G <= 4 && P % 4 == 0 && P <= 1536 && (c / 10) % 2 == 1) : pageable) ? slab_pg : slab_pin;
+    uint8_t* repair = (mixed ? (c / 24) % 2 == 1 : tear ? (c / 20) % 2 == 1 : pageable) ? rep_pg : rep_pin;
+    for (uint32_t i = 0; i < G * K; ++i) offsets[i] = scattered ? rnd() % (kSlab - P + 1) : i * P;
+    if (epoch || tear) {
+      // fresh bytes where this call's packets are (a stale address or half reads other bytes)
+      for (uint32_t i = 0; i < G * K; ++i)
+        for (uint32_t b = 0; b < P; b += 4) {
+          const uint32_t v = rnd();
+          std::memcpy(slab + offsets[i] + b, &v, std::min<uint32_t>(4, P - b));
+        }
+    } else {
+      for (uint32_t i = 0; i < kSlab; i += 4) {
+        const uint32_t v = rnd();
+        std::memcpy(slab + i, &v, 4);
+      }
     }
     std::fill(want.begin(), want.end(), 0);
     for (uint32_t g = 0; g < G; ++g)
@@ -159,6 +241,8 @@ int main(int argc, char** argv) {
   g_resident_calls = st.resident_calls;
   g_resident_inline = st.resident_inline;
   g_resident_vram = st.resident_vram;
+  g_bad = st.resident_bad_slots;
+  g_scrubs = st.resident_scrubs;
   std::atexit(mark_exit);  // registered after the library's shutdown_all: runs before it
   return 0;               // encoders, slabs and repair buffers stay alive (a Go process exiting)
 }

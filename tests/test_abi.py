@@ -49,6 +49,20 @@ def test_library_exports_every_declared_symbol(quicfec_mod):
     assert set(quicfec_mod.REFERENCE_SYMBOLS) | set(quicfec_mod.HIP_SYMBOLS) <= exported
 
 
+def test_library_is_built_from_this_tree(quicfec_mod):
+    """The loaded libfec_hip.so embeds the hash of the sources it was built from
+    (quic-test_amd/csrc/src_hash.py, compiled in by the Makefile); it must equal the hash of the
+    tree this test runs from -- on the GPU box too, so a stale prebuilt library is caught
+    (VERDICT r04 item 5)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("src_hash", REPO / "quic-test_amd" / "csrc" / "src_hash.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    version = quicfec_mod.load_library().fec_hip_version().decode()
+    assert re.fullmatch(r"libfec_hip \S+ gfx950 src=[0-9a-f]{64}", version), version
+    assert version.endswith("src=" + mod.source_hash()), (version, mod.source_hash())
+
+
 def test_library_is_gfx950_code_object(quicfec_mod):
     blob = quicfec_mod.LIB_PATH.read_bytes()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob

@@ -66,3 +66,28 @@ def test_bits_is_the_default_for_c4(gpu_ctx, oracle_mod, torch_cuda, monkeypatch
         data = oracle_mod.splitmix_bytes(G * k * P, 0xDEF0 + k)
         got = _encode(gpu_ctx, torch_cuda, data, G, k, r, P)
         assert np.array_equal(got, oracle_mod.rs_encode(data, G, k, r, P, nthreads=8).reshape(-1))
+
+
+@pytest.mark.parametrize("form", ["tables", "bits"])
+@pytest.mark.parametrize("k,r", [(10, 3), (20, 5)])
+@pytest.mark.parametrize("P,G", [(1200, 1), (1200, 3), (1200, 4), (1200, 9), (1200, 1_001), (1024, 77), (64, 301),
+                                 (1216, 50), (1500, 33), (1201, 21)])
+def test_staged_rows_equal_oracle(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, form, k, r, P, G):
+    """QUICFEC_ENCODE_STAGE=1 (kStageRows): the workgroup's parity rows go
+    through LDS and leave as one run of whole 16-B pieces.  Exact for partial last tiles (G not
+    a multiple of the tile, a lane's second group past the end), small and large tiles, packet
+    sizes that are not a multiple of 16 (the staged form then stands aside), and chunked
+    launches, at an odd parity address; the bytes outside the parity are untouched (guard bytes)."""
+    monkeypatch.setenv("QUICFEC_ENCODE_STAGE", "1")
+    monkeypatch.setenv("QUICFEC_ENCODE_BITS", "1" if form == "bits" else "0")
+    monkeypatch.setenv("QUICFEC_MAX_WAVE_BLOCKS", "37")
+    data = oracle_mod.splitmix_bytes(G * k * P, 0x57A6E + 7 * P + G + k)
+    exp = oracle_mod.rs_encode(data, G, k, r, P, nthreads=8).reshape(-1)
+    dd = _dev(torch_cuda, data)
+    guard = 67  # an odd parity address: the staged run's 16-B stores are unaligned
+    dp = torch_cuda.full((G * r * P + 2 * guard,), 0xA5, dtype=torch_cuda.uint8, device="cuda")
+    gpu_ctx.encode_dev(dd, G, k, r, P, dp[guard:guard + G * r * P])
+    gpu_ctx.synchronize()
+    got = dp.cpu().numpy()
+    assert np.array_equal(got[guard:guard + G * r * P], exp)
+    assert (got[:guard] == 0xA5).all() and (got[guard + G * r * P:] == 0xA5).all()

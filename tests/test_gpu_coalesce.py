@@ -429,3 +429,56 @@ def test_resident_ring_kinds_mixed_shapes(mode):
         # whatever the slab; page-locked slabs add the rest of the <= 8-group shapes
         assert rec["resident_inline"] == 180, rec
         assert rec["resident_calls"] > rec["resident_inline"], rec
+
+
+def test_resident_serves_no_torn_chunk_or_late_address_word():
+    """The VRAM ring's tags are per 8-B word (fec_kernels.hpp server_tag):
+    with QUICFEC_RESIDENT_TEST_TEAR every inline call stores one chunk's tagged high half first
+    and its low half ~100 us after the slot's header -- a 16-B write-combined store reaching the
+    device as two pieces -- and every addressed call of several groups stores its later groups'
+    address words ~100 us after the header.  The server must see those slots as not yet landed
+    (resident_bad_slots > 0: it retried them) and serve every one only once both halves / every
+    word arrived: each repair row equals the XOR of its ten packets (the reference's
+    xor_packets_scalar, fec_xor_simd.cpp:411-427), computed on the CPU."""
+    rec = _exit_path_run("tear", calls=300)
+    if "skip" in rec:
+        pytest.skip(rec["skip"])
+    assert rec["repairs_ok"] is True and rec["calls"] == 300, rec
+    assert rec["calls_after_exit"] == 0, rec["names"]
+    if rec["resident_vram"]:  # pageable slabs take the resident path only inline (VRAM ring)
+        assert rec["resident_calls"] == 300, rec
+    assert rec["bad_slots"] > 0, rec
+
+
+@pytest.mark.parametrize("mode", ["epoch", "epoch_hostring"])
+def test_resident_tag_epoch_scrub_under_mixed_calls(mode):
+    """a later group's address word written by an 8-group call and not since
+    (one-group inline calls write none) carries the same tag again one tag epoch later.  With an
+    epoch of 2 laps, slots 0, 5, 10, ... take 8-group addressed calls on even laps and one-group
+    inline calls on odd laps over 6 laps (6,144 calls), and the tear hook stores the later groups'
+    words ~100 us late, so the server reads the words two laps old first.  The server zeroes each
+    slot after the last lap of an epoch (scrubs > 0), so those words never match: every row
+    equals the CPU XOR.  Both ring kinds (VRAM; page-locked host memory, where no call is inline)."""
+    rec = _exit_path_run(mode, calls=6 * 1024)
+    if "skip" in rec:
+        pytest.skip(rec["skip"])
+    assert rec["repairs_ok"] is True and rec["calls"] == 6 * 1024, rec
+    assert rec["calls_after_exit"] == 0, rec["names"]
+    assert rec["resident_calls"] == 6 * 1024, rec
+    # epochs end after laps 1 and 3 (and 5, if the last lap's calls were served before the read)
+    assert rec["scrubs"] >= 2 * 1024, rec
+    assert rec["bad_slots"] > 0, rec
+
+
+def test_poisoned_resident_fails_no_in_flight_call():
+    """when one call poisons the Resident (its deadline passed), the calls
+    other threads have in flight must not fail with it.  8 threads with a context each make
+    one-group calls; seq 600 fails at once (QUICFEC_RESIDENT_TEST_FAIL_AT).  Its slot and every
+    other published slot are either served before the instance leaves or, once it has left
+    without serving them, run on the coalescer path: all 2,400 calls return 0 with the right row."""
+    rec = _exit_path_run("poison_mt", calls=2_400)
+    if "skip" in rec:
+        pytest.skip(rec["skip"])
+    assert rec["repairs_ok"] is True and rec["calls"] == 2_400, rec
+    assert rec["calls_after_exit"] == 0, rec["names"]
+    assert 600 <= rec["resident_calls"] < 2_400, rec
