@@ -33,6 +33,8 @@ import sys
 import time
 from pathlib import Path
 
+T_START = time.monotonic()  # this process's start: the line's wall_s phases are measured from it
+
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "quic-test_amd"))
 
@@ -981,9 +983,12 @@ def main() -> int:
     if args.groups:
         cfg["workload"] += f" (groups override: {G}/GPU)"
 
+    wall = {"setup": round(time.monotonic() - T_START, 2)}  # rank 0's wall-clock seconds per phase
     bench = Bench(args, rank, world, local)
+    t = time.monotonic()
     head = bench.measure(args.config, cfg, G, args.steps, args.warmup, args.decode_api, not args.no_verify,
                          not args.no_other_api, args.e2e)
+    wall["headline"] = round(time.monotonic() - t, 2)
 
     legs = None
     if legs_enabled(args, world):
@@ -992,16 +997,24 @@ def main() -> int:
             lg = args.leg_groups or lc["groups"]
             if args.leg_groups:
                 lc["workload"] += f" (groups override: {lg}/GPU)"
-            return bench.measure(config, lc, lg, min(args.steps, 20), min(args.warmup, 2), "auto",
-                                 not args.no_verify, False, e2e)
+            t0 = time.monotonic()
+            res = bench.measure(config, lc, lg, min(args.steps, 20), min(args.warmup, 2), "auto",
+                                not args.no_verify, False, e2e)
+            wall["leg_" + config] = round(time.monotonic() - t0, 2)
+            return res
         legs = run_legs(measure_leg)
 
     cpu = None
+    t = time.monotonic()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg)
+        wall["cpu_baseline"] = round(time.monotonic() - t, 2)
     site = None  # beside the headline like cpu_baseline, and skipped with it (profiled and A/B runs)
+    t = time.monotonic()
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_call_site:
         site = call_site()
+        wall["call_site"] = round(time.monotonic() - t, 2)
+    wall["total"] = round(time.monotonic() - T_START, 2)
 
     if rank == 0:
         k, r, P = cfg["k"], cfg["r"], cfg["P"]
@@ -1029,6 +1042,7 @@ def main() -> int:
             out["buffers"] = head["buffers"]
         if legs:
             out.update(legs)
+        out["wall_s"] = wall
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

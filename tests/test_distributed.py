@@ -108,23 +108,29 @@ def test_bench_gpus_n_spawns_n_ranks(world):
     assert ("c4" in rec) == (world > 1) and ("c5_e2e" in rec) == (world > 1)
 
 
-def test_bench_gpus_2_carries_every_multi_gpu_config():
-    """One `bench.py --gpus 2` invocation reports the C4 and C5 lines beside the headline, each
-    reduced over both ranks (barrier, MAX time, SUM of payload) like the headline."""
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_gpus_n_carries_every_multi_gpu_config(world):
+    """One `bench.py --gpus N` invocation reports the C4 and C5 lines beside the headline, each
+    reduced over all N ranks (barrier, MAX time, SUM of payload) like the headline.  N = 8 is the
+    driver's scaling run: eight gloo ranks spawned by the GPU-free parent."""
     import json
     import subprocess
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["QUICFEC_DIST_BACKEND"] = "gloo"
-    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--launch-selftest"],
-                         env=env, capture_output=True, text=True, timeout=180)
+    out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", str(world), "--launch-selftest"],
+                         env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
-    assert rec["n_gpus"] == 2
+    assert rec["n_gpus"] == world and rec["gpus_arg"] == world
+    assert rec["max_elapsed"] == pytest.approx(0.25 * world)          # MAX over ranks
+    assert rec["total_groups"] == pytest.approx(1000 * world)         # SUM over ranks
     for sec in ("c4", "c5_e2e"):
-        assert rec[sec]["ranks"] == 2, sec
-        assert rec[sec]["ms_per_step"] == pytest.approx(20.0)     # MAX over ranks (rank 1: 0.02 s)
+        assert rec[sec]["ranks"] == world, sec
+        assert rec[sec]["ms_per_step"] == pytest.approx(10.0 * world)  # MAX over ranks (rank i: 0.01 (i + 1) s)
         assert rec[sec]["verified"] is True
-    assert rec["c5_e2e"]["e2e_pinned"]["ranks"] == 2
+    assert rec["c5_e2e"]["e2e_pinned"]["ranks"] == world
+    if world != 2:
+        return
     assert "C4" in rec["c4"]["workload"] and "C5" in rec["c5_e2e"]["workload"]
     # --legs off drops them
     out = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--legs", "off", "--launch-selftest"],
