@@ -451,7 +451,9 @@ class Resident {
     r->no_launch = env_long("QUICFEC_RESIDENT_TEST_NOLAUNCH", 0) != 0;
     // tests: a short tag epoch (fec_kernels.hpp server_tag), so the scrubs at its boundaries run
     // within a few thousand calls
-    r->epoch = static_cast<uint32_t>(std::min<long>(kServerEpoch, std::max(1L, env_long("QUICFEC_RESIDENT_TEST_EPOCH", kServerEpoch))));
+    const long ep = std::min<long>(kServerEpoch, std::max(1L, env_long("QUICFEC_RESIDENT_TEST_EPOCH", kServerEpoch)));
+    r->epoch = 1u;
+    while (r->epoch * 2 <= static_cast<uint32_t>(ep)) r->epoch *= 2;  // a power of two (server_tag)
     // tests: every inline call lands one chunk in two 8-B pieces, the half with the tag first and
     // the other ~100 us after the slot's header (a write-combined store evicted in pieces)
     r->tear = env_long("QUICFEC_RESIDENT_TEST_TEAR", 0) != 0;
@@ -533,7 +535,7 @@ class Resident {
     // the previous epoch may carry a tag of this one (the server zeroed the slot's own words and
     // data area after serving its last lap; fec_kernels.hpp server_tag).  The previous occupant's
     // rows were all collected, so the device writes nothing here until this slot is published.
-    if (vinl && seq >= kServerSlots && (seq / kServerSlots) % epoch == 0) {
+    if (vinl && seq >= kServerSlots && server_tag(seq, epoch) == 1u) {
       std::memset(iouts.host + size_t(si) * kInlineOutBytes, 0, kInlineOutBytes);
       std::atomic_thread_fence(std::memory_order_seq_cst);
     }
@@ -630,14 +632,24 @@ class Resident {
       }
     }
     if (rc == FEC_OK && inline_pk) {
-      for (uint32_t g = 0; g < G; ++g)
-        for (uint32_t c = 0; c < nch; ++c) {
-          const uint8_t* ch = stg + (size_t(g) * nch + c) * 16;
-          uint8_t* dst = repair_out + size_t(g) * P + c * kInlinePayload;
-          const uint32_t n = std::min(kInlinePayload, P - c * kInlinePayload);
-          std::memcpy(dst, ch, std::min(6u, n));
-          if (n > 6) std::memcpy(dst + 6, ch + 8, n - 6);
+      // chunk c's 12 payload bytes to repair bytes [12c, 12c + 12): two 8-B copies per chunk,
+      // in increasing order, each overwriting the previous one's two tag bytes, while the copy
+      // stays inside the row (12c + 14 <= P); the last chunks byte-exact
+      const uint32_t nfast = P >= 14 ? (P - 14) / kInlinePayload + 1 : 0;
+      for (uint32_t g = 0; g < G; ++g) {
+        const uint8_t* ch = stg + size_t(g) * nch * 16;
+        uint8_t* dst = repair_out + size_t(g) * P;
+        uint32_t c = 0;
+        for (; c < nfast; ++c) {
+          std::memcpy(dst + c * kInlinePayload, ch + c * 16, 8);
+          std::memcpy(dst + c * kInlinePayload + 6, ch + c * 16 + 8, 8);
         }
+        for (; c < nch; ++c) {
+          const uint32_t n = std::min(kInlinePayload, P - c * kInlinePayload);
+          std::memcpy(dst + c * kInlinePayload, ch + c * 16, std::min(6u, n));
+          if (n > 6) std::memcpy(dst + c * kInlinePayload + 6, ch + c * 16 + 8, n - 6);
+        }
+      }
     } else if (rc == FEC_OK && !repair_dev) {
       std::memcpy(repair_out, outs.host + size_t(si) * kResidentOutBytes, size_t(G) * P);
     }

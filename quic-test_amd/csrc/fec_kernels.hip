@@ -2806,7 +2806,7 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
 hipError_t launch_legacy_server(ServerSlot* ring, uint8_t* inl, uint64_t* done, ServerControl* ctl,
                                 uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
                                 uint64_t* stamps, uint32_t epoch, hipStream_t s) {
-  if (epoch < 1u || epoch > kServerEpoch) return hipErrorInvalidValue;
+  if (epoch < 1u || epoch > kServerEpoch || (epoch & (epoch - 1u)) != 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(legacy_server, dim3(1), dim3(kServerThreads), 0, s, ring, inl, done, ctl, start_seq, gen,
                      idle_ticks, life_ticks, stamps, epoch);
   return hipGetLastError();

@@ -162,9 +162,9 @@ bool decode_compact_tables(const DecodeLaunch& a);
 // self-validating.  One resident workgroup serves the slots in seq order and stores
 // done[seq % kServerSlots] = seq + 1.  Calls are served without a kernel launch each.
 //
-// Tags and the epoch.  A slot's tag is (lap % epoch) + 1 with lap = seq / kServerSlots, so the
-// tags of one slot repeat every `epoch` laps (65535 by default; QUICFEC_RESIDENT_TEST_EPOCH for
-// tests).  A word left from the previous epoch could carry the current tag (a word written
+// Tags and the epoch.  A slot's tag is (lap & (epoch - 1)) + 1 with lap = seq / kServerSlots and
+// epoch a power of two (no division on the server's critical path), so the tags of one slot
+// repeat every `epoch` laps (32768 by default; QUICFEC_RESIDENT_TEST_EPOCH for tests).  A word left from the previous epoch could carry the current tag (a word written
 // exactly `epoch` laps ago and not since, e.g. a later group's address word under inline-only
 // calls), so the slot is scrubbed at every epoch boundary: the server zeroes the slot's words
 // and its inline data area after serving the last lap of an epoch, before that slot's done word
@@ -177,13 +177,13 @@ constexpr uint32_t kServerMaxGroups = 8;  // groups per slot (legacy calls of 1.
 constexpr uint32_t kServerPackets = 10;   // the legacy call's packets per group
 constexpr uint64_t kServerTagShift = 48;  // addresses below 2^48 (x86-64 user virtual addresses)
 constexpr uint64_t kServerAddrMask = (1ull << kServerTagShift) - 1;
-constexpr uint32_t kServerEpoch = 65535;  // laps per tag epoch (tags 1 .. epoch fit 16 bits)
+constexpr uint32_t kServerEpoch = 32768;  // laps per tag epoch, a power of two (tags 1 .. epoch fit 16 bits)
 __host__ __device__ inline uint32_t server_tag(uint64_t seq, uint32_t epoch) {
-  return static_cast<uint32_t>((seq / kServerSlots) % epoch) + 1u;
+  return (static_cast<uint32_t>(seq / kServerSlots) & (epoch - 1u)) + 1u;
 }
 // Whether the server scrubs the slot of seq after serving it (the last lap of an epoch).
 __host__ __device__ inline bool server_scrub_after(uint64_t seq, uint32_t epoch) {
-  return (seq / kServerSlots) % epoch == epoch - 1u;
+  return (static_cast<uint32_t>(seq / kServerSlots) & (epoch - 1u)) == epoch - 1u;
 }
 struct alignas(64) ServerSlot {
   uint64_t out;             // tag | device address of the repair rows, row g at out + g * P
@@ -223,7 +223,7 @@ struct alignas(64) ServerControl {
 // stamps: nullptr, or 256 x 8 words of host memory for the diagnostic phase stamps (QUICFEC_RESIDENT_STAMPS).
 // inl: the inline data areas (kInlineSlotBytes per slot) when the ring is in VRAM, else nullptr;
 // then the host's stop word (host memory) is read by every 16th poll only, not every poll.
-// epoch: laps per tag epoch (server_tag), 1 .. kServerEpoch.
+// epoch: laps per tag epoch (server_tag), a power of two, 1 .. kServerEpoch.
 hipError_t launch_legacy_server(ServerSlot* ring, uint8_t* inl, uint64_t* done, ServerControl* ctl,
                                 uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
                                 uint64_t* stamps, uint32_t epoch, hipStream_t s);

@@ -543,18 +543,24 @@ int legacy_raw(int calls) {
   }
   const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
   fec_coalesce_stats(&cs, 0);
+  // where the slowest calls are (the first call pays any lazily created state)
+  const size_t imax = us.empty() ? 0 : size_t(std::max_element(us.begin(), us.end()) - us.begin());
+  std::vector<double> rest(us.begin() + (us.empty() ? 0 : 1), us.end());
+  const double first_us = us.empty() ? 0.0 : us[0], rest_max = rest.empty() ? 0.0 : *std::max_element(rest.begin(), rest.end());
   const char* co = std::getenv("QUICFEC_COALESCE");
   const char* res = std::getenv("QUICFEC_RESIDENT");
-  char cfg[512];
+  char cfg[768];
   std::snprintf(cfg, sizeof(cfg),
                 "\"streams\": 1, \"coalesce\": %d, \"resident\": %d, \"errors\": %ld, \"resident_calls\": %llu, "
                 "\"resident_inline\": %llu, \"resident_vram\": %llu, "
-                "\"resident_us_per_call\": {\"pre\": %.2f, \"wait\": %.2f, \"post\": %.2f}",
+                "\"resident_us_per_call\": {\"pre\": %.2f, \"wait\": %.2f, \"post\": %.2f}, "
+                "\"max_at_call\": %zu, \"first_call_us\": %.1f, \"max_after_first_us\": %.1f, \"batches\": %llu",
                 co && co[0] == '0' ? 0 : 1, res && res[0] == '0' ? 0 : 1, errors, (unsigned long long)cs.resident_calls,
                 (unsigned long long)cs.resident_inline, (unsigned long long)cs.resident_vram,
                 cs.resident_calls ? cs.resident_pre_ns / 1e3 / cs.resident_calls : 0.0,
                 cs.resident_calls ? cs.resident_wait_ns / 1e3 / cs.resident_calls : 0.0,
-                cs.resident_calls ? cs.resident_post_ns / 1e3 / cs.resident_calls : 0.0);
+                cs.resident_calls ? cs.resident_post_ns / 1e3 / cs.resident_calls : 0.0, imax, first_us, rest_max,
+                (unsigned long long)cs.batches);
   print_lat("legacy_raw", cfg, us, calls, wall, 0.0, nullptr);
   fec_free_slab(slab);
   fec_free_repair_buffer(rep);
