@@ -1074,17 +1074,22 @@ constexpr uint64_t kRunAgg = 1ull << 32;
 constexpr uint64_t kRunIncl = 2ull << 32;
 constexpr uint32_t kRunEpochShift = 34;
 
-// One group's rebuilt rows into acc (rows 0..e-1), returns e.  Same survivor choice, record
-// and arithmetic as fused_group's DIRECT + INLINE path (survivors: the surviving data shards
-// ascending, then the e lowest surviving parity rows; record from the colex ranks).
+// One group's rebuild in two stages, so a wave can have the next group's survivor loads in flight
+// while it computes and stores this one (kRunPipe): runs_load issues the survivor loads and finds
+// the record, runs_compute forms the rows.  Same survivor choice, record and arithmetic as
+// fused_group's DIRECT + INLINE path (survivors: the surviving data shards ascending, then the e
+// lowest surviving parity rows; record from the colex ranks).
+struct RunMeta {
+  const Tab* tabs;
+  uint32_t e;
+  bool xor_only;
+};
+
 template <int K, int R, int NM, int NT, int POL>
-__device__ __forceinline__ uint32_t runs_rebuild(uint64_t g, uint64_t m, uint32_t lane,
-                                                 const uint8_t* __restrict__ data,
-                                                 const uint8_t* __restrict__ parity,
-                                                 const uint8_t* __restrict__ codebook, const RankMeta& rm,
-                                                 uint32_t P, const uint32_t (&toff)[NT > 0 ? NT : 1],
-                                                 uint32_t (&acc)[R][4 * NM + NT]) {
-  constexpr int NW = 4 * NM + NT;
+__device__ __forceinline__ RunMeta runs_load(uint64_t g, uint64_t m, uint32_t lane, const uint8_t* __restrict__ data,
+                                             const uint8_t* __restrict__ parity, const uint8_t* __restrict__ codebook,
+                                             const RankMeta& rm, uint32_t P, const uint32_t (&toff)[NT > 0 ? NT : 1],
+                                             uint32_t (&x)[K][4 * NM + NT]) {
   constexpr uint64_t kmask = (1ull << K) - 1;
   constexpr uint64_t rmask = (1ull << R) - 1;
   const uint64_t lost = m & kmask;
@@ -1105,12 +1110,13 @@ __device__ __forceinline__ uint32_t runs_rebuild(uint64_t g, uint64_t m, uint32_
       sp &= sp - 1;
     }
   }
-  const bool xor_only = e == 1 && (pm & 1u) == 0;
-  const Tab* tabs = reinterpret_cast<const Tab*>(codebook + rm.base[e] + (rank_e * rm.count_r[e] + rank_r) * rm.stride[e] + 128);
+  RunMeta mt;
+  mt.e = e;
+  mt.xor_only = e == 1 && (pm & 1u) == 0;
+  mt.tabs = reinterpret_cast<const Tab*>(codebook + rm.base[e] + (rank_e * rm.count_r[e] + rank_r) * rm.stride[e] + 128);
   uint64_t surv = (~lost & kmask) | (rsel << K);
   const uint8_t* dg = data + g * K * static_cast<uint64_t>(P);
   const uint8_t* pg = parity + g * R * static_cast<uint64_t>(P);
-  uint32_t x[K][NW];
 #pragma unroll
   for (int s = 0; s < K; ++s) {
     const uint32_t sid = static_cast<uint32_t>(__builtin_ctzll(surv));
@@ -1130,16 +1136,22 @@ __device__ __forceinline__ uint32_t runs_rebuild(uint64_t g, uint64_t m, uint32_
       else x[s][4 * NM + t] = *reinterpret_cast<const u32u*>(src + toff[t]);
     }
   }
+  return mt;
+}
+
+template <int K, int R, int NM, int NT>
+__device__ __forceinline__ void runs_compute(const RunMeta& mt, uint32_t (&x)[K][4 * NM + NT], uint32_t (&acc)[R][4 * NM + NT]) {
+  constexpr int NW = 4 * NM + NT;
 #pragma unroll
   for (int mm = 0; mm < R; ++mm)
 #pragma unroll
     for (int q = 0; q < NW; ++q) acc[mm][q] = 0;
-  if (xor_only) {  // single data loss rebuilt from parity row 0: the reference XOR
+  if (mt.xor_only) {  // single data loss rebuilt from parity row 0: the reference XOR
 #pragma unroll
     for (int s = 0; s < K; ++s)
 #pragma unroll
       for (int q = 0; q < NW; ++q) acc[0][q] ^= x[s][q];
-    return 1;
+    return;
   }
 #pragma unroll
   for (int s = 0; s < K; ++s) {
@@ -1156,8 +1168,8 @@ __device__ __forceinline__ uint32_t runs_rebuild(uint64_t g, uint64_t m, uint32_
     }
 #pragma unroll
     for (int mm = 0; mm < R; ++mm) {
-      if (static_cast<uint32_t>(mm) < e) {
-        const Tab& t = tabs[mm * K + s];
+      if (static_cast<uint32_t>(mm) < mt.e) {
+        const Tab& t = mt.tabs[mm * K + s];
         if (t.coef == 1u) {
 #pragma unroll
           for (int q = 0; q < NW; ++q) acc[mm][q] ^= x[s][q];
@@ -1168,8 +1180,11 @@ __device__ __forceinline__ uint32_t runs_rebuild(uint64_t g, uint64_t m, uint32_
       }
     }
   }
-  return e;
 }
+
+// recover_runs: the wave's groups one after another (default), or with the next group's survivor
+// loads issued before this group's arithmetic and stores (probe form).
+constexpr int kRunPipe = 16384;
 
 // stage_bytes: dynamic LDS of the run image (0: every row straight to HBM).  The image is used
 // only when P % 16 == 0 and `out` is 16-B aligned (the launcher passes 0 otherwise), so row
@@ -1308,15 +1323,52 @@ __global__ __launch_bounds__(64 * WAVES) void recover_runs(const uint8_t* __rest
     toff[t] = NM * 1024u + t * 256u + lane * 4u;
     if (toff[t] + 4u > P) toff[t] = P - 4u;
   }
-  for (uint32_t i = wave; i < nwork; i += WAVES) {
+  auto item_of = [&](uint32_t i, uint64_t& gi, uint64_t& mw, uint32_t& r0) {
     const uint64_t mi = s_mask[i];
-    const uint64_t mw = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(mi >> 32))) << 32) |
-                        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(mi));
+    mw = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(mi >> 32))) << 32) |
+         __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(mi));
     const uint32_t item = __builtin_amdgcn_readfirstlane(s_item[i]);
-    const uint64_t gi = static_cast<uint64_t>(tile) * kTile + (item >> 16);
-    const uint32_t r0 = item & 0xFFFFu;
+    gi = static_cast<uint64_t>(tile) * kTile + (item >> 16);
+    r0 = item & 0xFFFFu;
+  };
+  constexpr bool kPipe = (POL & kRunPipe) != 0;
+  uint32_t xn[kPipe ? K : 1][kPipe ? NW : 1];  // kRunPipe: the next group's survivors, loads in flight
+  RunMeta mn{};
+  if constexpr (kPipe) {
+    if (wave < nwork) {
+      uint64_t gi, mw;
+      uint32_t r0;
+      item_of(wave, gi, mw, r0);
+      mn = runs_load<K, R, NM, NT, POL>(gi, mw, lane, data, parity, codebook, rm, P, toff, xn);
+    }
+  }
+  for (uint32_t i = wave; i < nwork; i += WAVES) {
+    uint64_t gi, mw;
+    uint32_t r0;
+    item_of(i, gi, mw, r0);
     uint32_t acc[R][NW];
-    const uint32_t e = runs_rebuild<K, R, NM, NT, POL>(gi, mw, lane, data, parity, codebook, rm, P, toff, acc);
+    uint32_t e;
+    if constexpr (kPipe) {
+      uint32_t x[K][NW];
+#pragma unroll
+      for (int s2 = 0; s2 < K; ++s2)
+#pragma unroll
+        for (int q = 0; q < NW; ++q) x[s2][q] = xn[s2][q];
+      const RunMeta mt = mn;
+      if (i + WAVES < nwork) {
+        uint64_t gn, mwn;
+        uint32_t rn;
+        item_of(i + WAVES, gn, mwn, rn);
+        mn = runs_load<K, R, NM, NT, POL>(gn, mwn, lane, data, parity, codebook, rm, P, toff, xn);
+      }
+      runs_compute<K, R, NM, NT>(mt, x, acc);
+      e = mt.e;
+    } else {
+      uint32_t x[K][NW];
+      const RunMeta mt = runs_load<K, R, NM, NT, POL>(gi, mw, lane, data, parity, codebook, rm, P, toff, x);
+      runs_compute<K, R, NM, NT>(mt, x, acc);
+      e = mt.xor_only ? 1u : mt.e;
+    }
     if (flags & 1u) continue;  // probe: reads and arithmetic only
 #pragma unroll
     for (int mm = 0; mm < R; ++mm) {

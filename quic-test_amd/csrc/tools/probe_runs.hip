@@ -240,12 +240,18 @@ int main(int argc, char** argv) {
       RF("runs w8 tg16 nl+ns st58K" + at, NL | NS, 8, 16, 57600, 0, chk, outs[i])
       RF("runs w4 tg8 nl+ns st29K" + at, NL | NS, 4, 8, 28800, 0, chk, outs[i])
       RF("runs w8 tg8 nostore" + at, NL, 8, 8, 28800, 1, false, outs[i])
+      // several groups per wave, the next group's loads in flight during this one's rows (kRunPipe)
+      RF("runs w4 tg16 nl+ns st58K" + at, NL | NS, 4, 16, 59392, 0, chk, outs[i])
+      RF("runs w4 tg16 pipe nl+ns st58K" + at, NL | NS | kRunPipe, 4, 16, 59392, 0, chk, outs[i])
+      RF("runs w8 tg32 pipe nl+ns st60K" + at, NL | NS | kRunPipe, 8, 32, 61440, 0, chk, outs[i])
     }
     if (loss > 0) {
       RF("runs w8 nl+ns st32K" + at, NL | NS, 8, 512, 32768, 0, chk, outs[i])
       RF("runs w4 nl+ns st24K" + at, NL | NS, 4, 256, 24576, 0, chk, outs[i])
       RF("runs w4 nl st24K" + at, NL, 4, 256, 24576, 0, chk, outs[i])
       RF("runs w8 nostore" + at, NL, 8, 512, 0, 1, false, outs[i])
+      RF("runs w8 pipe nl+ns st48K" + at, NL | NS | kRunPipe, 8, 512, 49152, 0, chk, outs[i])
+      RF("runs w4 tg256 pipe nl+ns st24K" + at, NL | NS | kRunPipe, 4, 256, 24576, 0, chk, outs[i])
     }
   }
   // reference output: the two-step packed recover

@@ -38,3 +38,9 @@ timeout -k 10 400 python -u scripts/probe_recover_delta.py --alloc contiguous > 
 cat "$E/delta_contiguous.jsonl"
 timeout -k 10 400 python -u scripts/probe_recover_delta.py --alloc torch > "$E/delta_torch.jsonl"
 cat "$E/delta_torch.jsonl"
+# the one-launch tile recover with the next group's loads in flight
+# (kRunPipe), dense (C3: several groups per wave) and sparse (C5), against the library's forms
+timeout -k 10 300 ./quic-test_amd/lib/probe_runs 1000000 7 0 > "$E/probe_runs_c3.txt" 2>&1
+tail -25 "$E/probe_runs_c3.txt"
+timeout -k 10 300 ./quic-test_amd/lib/probe_runs 1000000 9 0.01 > "$E/probe_runs_c5.txt" 2>&1
+tail -25 "$E/probe_runs_c5.txt"
