@@ -162,6 +162,9 @@ class Coalescer {
  public:
   // NULL when the device or page-locked memory cannot be set up (the call then runs alone).
   static Coalescer* create(int device, uint32_t P) {
+    // QUICFEC_COALESCE_STAMPS: the creation's phase times to stderr (diagnostic)
+    const bool stamps = env_long("QUICFEC_COALESCE_STAMPS", 0) != 0;
+    uint64_t t[5] = {now_ns(), 0, 0, 0, 0};
     std::unique_ptr<Coalescer> c(new Coalescer());
     c->device = device;
     c->P = P;
@@ -170,11 +173,13 @@ class Coalescer {
     c->max_inflight = static_cast<int>(std::max(1L, std::min(8L, env_long("QUICFEC_COALESCE_INFLIGHT", 2))));
     c->ctx = fec_encoder_new_device(0.10, c->cap, device);
     if (!c->ctx) return nullptr;
+    t[1] = now_ns();
     BindDevice bd(device);
     if (!bd.ok || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
       (void)hipGetLastError();
       return nullptr;
     }
+    t[2] = now_ns();
     // in flight + the open one + one whose callers are still copying out
     for (int i = 0; i < c->max_inflight + 2; ++i) {
       auto b = std::make_unique<Batch>();
@@ -185,8 +190,13 @@ class Coalescer {
       }
       c->batches.push_back(std::move(b));
     }
+    t[3] = now_ns();
     std::lock_guard<std::mutex> lk(c->mu);
     c->open_free();
+    t[4] = now_ns();
+    if (stamps)
+      std::fprintf(stderr, "{\"coalescer_create_us\": {\"context\": %.1f, \"stream\": %.1f, \"batches\": %.1f, \"open\": %.1f}}\n",
+                   (t[1] - t[0]) / 1e3, (t[2] - t[1]) / 1e3, (t[3] - t[2]) / 1e3, (t[4] - t[3]) / 1e3);
     return c.release();
   }
 

@@ -182,6 +182,61 @@ __global__ __launch_bounds__(WAVES * 64) void rw2_glds(const uint8_t* __restrict
   }
 }
 
+// C4-shaped traffic (k=20 r=5, 80/20 read/write): a wave streams units of
+// KP pieces by LDS-DMA into a 2-unit ring (unit u+1 in flight while u is folded) and stores RP
+// pieces per unit (nt).  One wave per workgroup so the ring (2 * KP KiB) fits beside others.
+template <int KP, int RP, int NTL>
+__global__ __launch_bounds__(64) void rw2_glds_kr(const uint8_t* __restrict__ in, uint8_t* __restrict__ outp,
+                                                  uint64_t units) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[2 * KP][1024];
+  const int lane = threadIdx.x;
+  const uint64_t step = uint64_t(gridDim.x);
+  uint64_t u = blockIdx.x;
+  if (u >= units) return;
+#pragma unroll
+  for (int i = 0; i < KP; ++i) glds16(in + (u * KP + i) * 1024 + lane * 16, &ring[i][0], NTL);
+  int cur = 0;
+  for (; u < units; u += step) {
+    const uint64_t nu = u + step;
+    if (nu < units) {
+#pragma unroll
+      for (int i = 0; i < KP; ++i) glds16(in + (nu * KP + i) * 1024 + lane * 16, &ring[(1 - cur) * KP + i][0], NTL);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KP) : "memory");
+    } else {
+      wait_vm<0>();
+    }
+    u32x4 acc[RP];
+#pragma unroll
+    for (int i = 0; i < RP; ++i) acc[i] = *reinterpret_cast<const u32x4*>(&ring[cur * KP + i][lane * 16]);
+#pragma unroll
+    for (int j = RP; j < KP; ++j) acc[j % RP] ^= *reinterpret_cast<const u32x4*>(&ring[cur * KP + j][lane * 16]);
+#pragma unroll
+    for (int i = 0; i < RP; ++i)
+      __builtin_nontemporal_store(acc[i], reinterpret_cast<u32x4*>(outp + (u * RP + i) * 1024 + lane * 16));
+    cur = 1 - cur;
+  }
+}
+
+// The same C4-shaped traffic with register loads (KP pieces in flight per wave, then RP stores).
+template <int KP, int RP>
+__global__ __launch_bounds__(256) void rw_reg_kr(const uint8_t* __restrict__ in, uint8_t* __restrict__ outp, uint64_t units) {
+  const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+  const uint64_t step = uint64_t(gridDim.x) * 4;
+  for (uint64_t u = uint64_t(blockIdx.x) * 4 + wave; u < units; u += step) {
+    u32x4 v[KP];
+#pragma unroll
+    for (int j = 0; j < KP; ++j) v[j] = *reinterpret_cast<const u32x4*>(in + (u * KP + j) * 1024 + lane * 16);
+    u32x4 acc[RP];
+#pragma unroll
+    for (int i = 0; i < RP; ++i) acc[i] = v[i];
+#pragma unroll
+    for (int j = RP; j < KP; ++j) acc[j % RP] ^= v[j];
+#pragma unroll
+    for (int i = 0; i < RP; ++i)
+      __builtin_nontemporal_store(acc[i], reinterpret_cast<u32x4*>(outp + (u * RP + i) * 1024 + lane * 16));
+  }
+}
+
 // The same traffic with register loads: a wave loads a unit's 10 pieces, folds, stores 3.
 template <int WAVES, bool NTL>
 __global__ __launch_bounds__(WAVES * 64) void rw_reg(const uint8_t* __restrict__ in, uint8_t* __restrict__ outp,
@@ -263,6 +318,20 @@ int main(int argc, char** argv) {
   time("rw reg nt 4w x8", [&] { rw_reg<4, true><<<cus * 8, 256>>>(buf, outp, units); });
   time("rw reg 4w x16", [&] { rw_reg<4, false><<<cus * 16, 256>>>(buf, outp, units); });
   CHECK(hipFree(outp));
+  // C4's mix (k=20 r=5): 24 GB read, 6 GB written when the buffer is 24 GB (argv[1] = 24000000000)
+  {
+    const uint64_t u20 = pieces / 20;
+    CHECK(hipMalloc(&outp, u20 * 5 * 1024));
+    std::printf("-- C4 mix: %.1f GB read + %.1f GB written; GB/s column = read bytes / t\n", u20 * 20 * 1024 / 1e9,
+                u20 * 5 * 1024 / 1e9);
+    time("c4 glds 1w x4/CU nt", [&] { rw2_glds_kr<20, 5, 1><<<cus * 4, 64>>>(buf, outp, u20); });
+    time("c4 glds 1w x3/CU nt", [&] { rw2_glds_kr<20, 5, 1><<<cus * 3, 64>>>(buf, outp, u20); });
+    time("c4 glds 1w x4/CU", [&] { rw2_glds_kr<20, 5, 0><<<cus * 4, 64>>>(buf, outp, u20); });
+    time("c4 reg 4w x2", [&] { rw_reg_kr<20, 5><<<cus * 2, 256>>>(buf, outp, u20); });
+    time("c4 reg 4w x3", [&] { rw_reg_kr<20, 5><<<cus * 3, 256>>>(buf, outp, u20); });
+    time("c4 reg 4w x4", [&] { rw_reg_kr<20, 5><<<cus * 4, 256>>>(buf, outp, u20); });
+    CHECK(hipFree(outp));
+  }
   CHECK(hipFree(buf));
   CHECK(hipFree(out));
   return 0;
