@@ -161,59 +161,42 @@ void atomic_max(std::atomic<uint64_t>& a, uint64_t v) {
 class Coalescer {
  public:
   // NULL when the device or page-locked memory cannot be set up (the call then runs alone).
+  // Nothing but the first batch's page-locked buffers and event is made here: no context and no
+  // stream (the leader launches on its caller's context stream), further batches when concurrent
+  // callers need them.  A context and a stream of its own each cost ~9 ms here (a stream that
+  // needs a new hardware queue), and the first shared-launch call of a process paid both: 18-22 ms
+  // against a p99 of 21-35 us (QUICFEC_COALESCE_STAMPS, profiles/r05e/legacy_coalescer_*.err).
   static Coalescer* create(int device, uint32_t P) {
-    // QUICFEC_COALESCE_STAMPS: the creation's phase times to stderr (diagnostic)
-    const bool stamps = env_long("QUICFEC_COALESCE_STAMPS", 0) != 0;
-    uint64_t t[5] = {now_ns(), 0, 0, 0, 0};
+    // QUICFEC_COALESCE_STAMPS: the creation's time to stderr (diagnostic)
+    const uint64_t t0 = now_ns();
     std::unique_ptr<Coalescer> c(new Coalescer());
     c->device = device;
     c->P = P;
     const uint64_t fit = kStageBudget / (uint64_t(kPackets) * P);
     c->cap = static_cast<uint32_t>(std::max<uint64_t>(8, std::min<uint64_t>(kMaxBatchGroups, fit)));
     c->max_inflight = static_cast<int>(std::max(1L, std::min(8L, env_long("QUICFEC_COALESCE_INFLIGHT", 2))));
-    c->ctx = fec_encoder_new_device(0.10, c->cap, device);
-    if (!c->ctx) return nullptr;
-    t[1] = now_ns();
     BindDevice bd(device);
-    if (!bd.ok || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    t[2] = now_ns();
-    // in flight + the open one + one whose callers are still copying out
-    for (int i = 0; i < c->max_inflight + 2; ++i) {
-      auto b = std::make_unique<Batch>();
-      if (!b->addr.alloc(size_t(c->cap) * kPackets * sizeof(uint64_t)) || !b->out.alloc(size_t(c->cap) * P) ||
-          hipEventCreateWithFlags(&b->done, hipEventDisableTiming) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
-      }
-      c->batches.push_back(std::move(b));
-    }
-    t[3] = now_ns();
+    if (!bd.ok || !c->add_batch()) return nullptr;
     std::lock_guard<std::mutex> lk(c->mu);
     c->open_free();
-    t[4] = now_ns();
-    if (stamps)
-      std::fprintf(stderr, "{\"coalescer_create_us\": {\"context\": %.1f, \"stream\": %.1f, \"batches\": %.1f, \"open\": %.1f}}\n",
-                   (t[1] - t[0]) / 1e3, (t[2] - t[1]) / 1e3, (t[3] - t[2]) / 1e3, (t[4] - t[3]) / 1e3);
+    if (env_long("QUICFEC_COALESCE_STAMPS", 0) != 0)
+      std::fprintf(stderr, "{\"coalescer_create_us\": %.1f}\n", (now_ns() - t0) / 1e3);
     return c.release();
   }
 
   uint32_t capacity() const { return cap; }
 
-  ~Coalescer() {  // process exit, no caller left (shutdown_all)
+  ~Coalescer() {  // only a Coalescer whose create() failed; never at exit (shutdown_all)
     BindDevice bd(device);
-    if (stream) (void)hipStreamSynchronize(stream);
     for (auto& b : batches)
       if (b->done) (void)hipEventDestroy(b->done);
     batches.clear();
-    if (stream) (void)hipStreamDestroy(stream);
-    if (ctx) fec_encoder_free(ctx);
   }
 
-  // The legacy call's body; slab_dev is the slab's device address when it is page-locked.
-  int encode(const uint8_t* slab, const uint8_t* slab_dev, const uint32_t* offsets, uint32_t G, uint8_t* repair_out) {
+  // The legacy call's body; slab_dev is the slab's device address when it is page-locked; stream:
+  // the caller's context stream (a leader launches its batch there).
+  int encode(const uint8_t* slab, const uint8_t* slab_dev, const uint32_t* offsets, uint32_t G, uint8_t* repair_out,
+             hipStream_t stream) {
     std::unique_lock<std::mutex> lk(mu);
     if (!slab_dev && !staging_ready) {
       for (auto& b : batches)
@@ -261,7 +244,7 @@ class Coalescer {
         lk.lock();
         if (b.state.load(std::memory_order_relaxed) == Batch::kOpen &&
             inflight.load(std::memory_order_relaxed) < max_inflight)
-          lead(b, lk);  // returns with the lock released
+          lead(b, lk, stream);  // returns with the lock released
         else
           lk.unlock();
         spins = 0;
@@ -292,8 +275,6 @@ class Coalescer {
   int device = 0;
   uint32_t P = 0, cap = 0;
   int max_inflight = 2;
-  FECEncoderCtx* ctx = nullptr;  // the coalescer's own (plans, device binding)
-  hipStream_t stream = nullptr;
   std::mutex mu;
   std::condition_variable cv_room;  // callers waiting for an open batch with room
   std::vector<std::unique_ptr<Batch>> batches;
@@ -304,9 +285,28 @@ class Coalescer {
   uint32_t spin_pause = static_cast<uint32_t>(env_long("QUICFEC_COALESCE_SPIN_PAUSE", 256));
   uint32_t spin_yield = static_cast<uint32_t>(env_long("QUICFEC_COALESCE_SPIN_YIELD", 3840));
 
-  // Opens a free batch for new callers, if there is one.  Caller holds mu.
+  // One more batch (its page-locked address list and output, its event, and staging when pageable
+  // callers have needed it).  Caller holds mu, or owns the coalescer alone (create).
+  bool add_batch() {
+    auto b = std::make_unique<Batch>();
+    if (!b->addr.alloc(size_t(cap) * kPackets * sizeof(uint64_t)) || !b->out.alloc(size_t(cap) * P) ||
+        (staging_ready && !b->stage.alloc(size_t(cap) * kPackets * P)) ||
+        hipEventCreateWithFlags(&b->done, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    batches.push_back(std::move(b));
+    return true;
+  }
+
+  // Opens a free batch for new callers, if there is one -- a new one while fewer than the in-flight
+  // batches + the open one + one still being copied out exist.  Caller holds mu.
   void open_free() {
-    for (size_t i = 0; i < batches.size(); ++i) {
+    for (size_t i = 0;; ++i) {
+      if (i == batches.size()) {
+        BindDevice bd(device);
+        if (batches.size() >= size_t(max_inflight) + 2 || !bd.ok || !add_batch()) return;
+      }
       Batch& b = *batches[i];
       if (b.state.load(std::memory_order_relaxed) != Batch::kFree) continue;
       b.used = b.calls = b.readers = 0;
@@ -322,7 +322,7 @@ class Coalescer {
 
   // Closes, launches and completes batch b.  Called with mu held through `lk`; returns with it
   // released.
-  void lead(Batch& b, std::unique_lock<std::mutex>& lk) {
+  void lead(Batch& b, std::unique_lock<std::mutex>& lk, hipStream_t stream) {
     b.state.store(Batch::kClosed, std::memory_order_relaxed);
     open = -1;
     open_free();
@@ -333,12 +333,18 @@ class Coalescer {
     while (b.copying.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
     b.state.store(Batch::kLaunched, std::memory_order_relaxed);
     const uint64_t t1 = now_ns();
-    int rc = encode_addr_batch(ctx, reinterpret_cast<const uint64_t*>(b.addr.dev), n, kPackets, 1, P, b.out.dev, stream);
+    // the gather encode of the batch's groups, row 0 = XOR as the reference (no coefficient table)
+    BindDevice bd(device);
+    const EncodeLaunch a{nullptr, b.addr.dev, OffsetKind::kAddr, b.out.dev, n, kPackets, 1, P, nullptr};
+    hipError_t le = bd.ok ? launch_encode(a, stream) : hipErrorInvalidDevice;
+    int rc = le == hipSuccess ? FEC_OK : FEC_ERR_HIP;
     std::string err;
     uint64_t t2 = t1;
-    if (rc == FEC_OK) {
-      BindDevice bd(device);
-      hipError_t e = bd.ok ? hipEventRecord(b.done, stream) : hipErrorInvalidDevice;
+    if (rc != FEC_OK) {
+      (void)hipGetLastError();
+      err = std::string("fec_encode_batch (coalesced): ") + hipGetErrorString(le);
+    } else {
+      hipError_t e = hipEventRecord(b.done, stream);
       t2 = now_ns();
       // poll (a blocking wait adds its wake-up to every batch); yield once it takes a while
       for (uint32_t i = 0; e == hipSuccess; ++i) {
@@ -356,8 +362,6 @@ class Coalescer {
         rc = FEC_ERR_HIP;
         err = std::string("fec_encode_batch (coalesced): ") + hipGetErrorString(e);
       }
-    } else {
-      err = fec_hip_last_error();
     }
     const uint64_t t3 = now_ns();
     g_close_ns.fetch_add(t1 - t0, std::memory_order_relaxed);
@@ -968,7 +972,7 @@ void coalesce_prepare(int device) {
 }
 
 bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* offsets, uint32_t num_groups,
-                            uint32_t packet_size, uint8_t* repair_out, int* rc) {
+                            uint32_t packet_size, uint8_t* repair_out, int* rc, hipStream_t stream) {
   const uint64_t t_enter = now_ns();
   if (env_long("QUICFEC_COALESCE", 1) == 0 || g_shut.load(std::memory_order_acquire)) return false;
   if (num_groups > static_cast<uint64_t>(std::max(0L, env_long("QUICFEC_COALESCE_MAX_GROUPS", 64)))) return false;
@@ -1000,7 +1004,7 @@ bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* off
   Coalescer* c = coalescer_for(device, packet_size);
   if (!c || num_groups > c->capacity() / 2) return false;
   *rc = c->encode(slab, sm == HostMem::kPinned ? static_cast<const uint8_t*>(sdev) : nullptr, offsets, num_groups,
-                  repair_out);
+                  repair_out, stream);
   return true;
 }
 

@@ -27,9 +27,10 @@ void set_last_error(const char* msg);
 // The legacy fec_encode_batch call (10 packets per group at slab + offsets[i], packet_size
 // bytes each, repair row g at repair_out + g * packet_size) joined into a shared launch on
 // `device`.  Returns false when the call is not one the coalescer takes (device-resident
-// buffers, too large, switched off); else true with the call's return code in *rc.
+// buffers, too large, switched off); else true with the call's return code in *rc.  stream: the
+// caller's context stream (a shared launch led by this caller goes there).
 bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* offsets, uint32_t num_groups,
-                            uint32_t packet_size, uint8_t* repair_out, int* rc);
+                            uint32_t packet_size, uint8_t* repair_out, int* rc, hipStream_t stream);
 
 // Sets up the resident encoder's page-locked ring for `device` ahead of the first legacy call
 // (no kernel launch; that happens on the first call).

@@ -1167,7 +1167,8 @@ static int fec_encode_batch_impl(FECEncoderCtx* ctx, const uint8_t* slab, const 
   // Small host-resident calls -- the reference's one group per call from each stream's own
   // context -- share launches with every other context's (fec_coalesce.cpp).
   int crc = 0;
-  if (qfec::coalesce_legacy_encode(ctx->device, slab, offsets, num_groups, packet_size, repair_out, &crc)) return crc;
+  if (qfec::coalesce_legacy_encode(ctx->device, slab, offsets, num_groups, packet_size, repair_out, &crc, ctx->stream))
+    return crc;
   constexpr uint32_t kPackets = 10;  // fec_xor_simd.cpp:580
   std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard dg(ctx->device);
