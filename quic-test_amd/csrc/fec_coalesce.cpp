@@ -143,6 +143,39 @@ struct Batch {
   std::condition_variable cv;  // callers that stopped spinning: done, or a launch slot came free
 };
 
+// A batch large enough for any packet size the coalescer takes: cap * P <= kStageBudget / 10
+// (cap = max(8, min(kMaxBatchGroups, kStageBudget / (10 P))), P <= kCoalesceMaxP).
+constexpr size_t kBatchOutMax = std::max<size_t>(kStageBudget / kPackets, size_t(8) * kCoalesceMaxP);
+
+// The first batch of the device's first coalescer, made with the device's first context
+// (coalesce_prepare) so that the first shared-launch call of a process pays no page-locked
+// allocation (~0.35 ms; profiles/r05g): sized for any packet size.
+std::mutex g_spare_mu;
+std::map<int, std::unique_ptr<Batch>> g_spare;
+
+bool alloc_batch(Batch& b, size_t groups, size_t out_bytes) {
+  if (!b.addr.alloc(groups * kPackets * sizeof(uint64_t)) || !b.out.alloc(out_bytes) ||
+      hipEventCreateWithFlags(&b.done, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return true;
+}
+
+void prepare_spare_batch(int device) {
+  std::lock_guard<std::mutex> lk(g_spare_mu);
+  if (g_spare.count(device)) return;
+  auto b = std::make_unique<Batch>();
+  g_spare.emplace(device, alloc_batch(*b, kMaxBatchGroups, kBatchOutMax) ? std::move(b) : nullptr);
+}
+
+std::unique_ptr<Batch> take_spare_batch(int device) {
+  std::lock_guard<std::mutex> lk(g_spare_mu);
+  auto it = g_spare.find(device);
+  if (it == g_spare.end()) return nullptr;
+  return std::move(it->second);
+}
+
 std::atomic<uint64_t> g_calls{0}, g_groups{0}, g_batches{0}, g_max_batch{0}, g_max_calls{0};
 std::atomic<uint64_t> g_close_ns{0}, g_launch_ns{0}, g_done_ns{0};
 
@@ -207,7 +240,7 @@ class Coalescer {
       staging_ready = true;
     }
     for (;;) {
-      if (open < 0) open_free();
+      if (open < 0) open_free(true);
       if (open >= 0 && batches[open]->used + G <= cap) break;
       cv_room.wait(lk);
     }
@@ -275,6 +308,7 @@ class Coalescer {
   int device = 0;
   uint32_t P = 0, cap = 0;
   int max_inflight = 2;
+  int stamps_left = env_long("QUICFEC_COALESCE_STAMPS", 0) != 0 ? 3 : 0;  // leaders only, under no lock: diagnostic
   std::mutex mu;
   std::condition_variable cv_room;  // callers waiting for an open batch with room
   std::vector<std::unique_ptr<Batch>> batches;
@@ -288,24 +322,30 @@ class Coalescer {
   // One more batch (its page-locked address list and output, its event, and staging when pageable
   // callers have needed it).  Caller holds mu, or owns the coalescer alone (create).
   bool add_batch() {
-    auto b = std::make_unique<Batch>();
-    if (!b->addr.alloc(size_t(cap) * kPackets * sizeof(uint64_t)) || !b->out.alloc(size_t(cap) * P) ||
-        (staging_ready && !b->stage.alloc(size_t(cap) * kPackets * P)) ||
-        hipEventCreateWithFlags(&b->done, hipEventDisableTiming) != hipSuccess) {
+    std::unique_ptr<Batch> b = batches.empty() ? take_spare_batch(device) : nullptr;  // made at the first context
+    if (!b) {
+      b = std::make_unique<Batch>();
+      if (!alloc_batch(*b, cap, size_t(cap) * P)) return false;
+    }
+    if (staging_ready && !b->stage.alloc(size_t(cap) * kPackets * P)) {
       (void)hipGetLastError();
+      if (b->done) (void)hipEventDestroy(b->done);
       return false;
     }
     batches.push_back(std::move(b));
     return true;
   }
 
-  // Opens a free batch for new callers, if there is one -- a new one while fewer than the in-flight
-  // batches + the open one + one still being copied out exist.  Caller holds mu.
-  void open_free() {
+  // Opens a free batch for new callers, if there is one -- with grow, a new one while fewer than
+  // the in-flight batches + the open one + one still being copied out exist (only callers that
+  // need room grow the set: a leader closing its batch does not pay an allocation).  Caller holds
+  // mu.
+  void open_free(bool grow = false) {
     for (size_t i = 0;; ++i) {
       if (i == batches.size()) {
+        if (!grow || batches.size() >= size_t(max_inflight) + 2) return;
         BindDevice bd(device);
-        if (batches.size() >= size_t(max_inflight) + 2 || !bd.ok || !add_batch()) return;
+        if (!bd.ok || !add_batch()) return;
       }
       Batch& b = *batches[i];
       if (b.state.load(std::memory_order_relaxed) != Batch::kFree) continue;
@@ -364,6 +404,11 @@ class Coalescer {
       }
     }
     const uint64_t t3 = now_ns();
+    if (stamps_left > 0) {  // QUICFEC_COALESCE_STAMPS: the first batches' phases (diagnostic)
+      --stamps_left;
+      std::fprintf(stderr, "{\"coalescer_batch_us\": {\"close\": %.1f, \"launch\": %.1f, \"done\": %.1f}}\n", (t1 - t0) / 1e3,
+                   (t2 - t1) / 1e3, (t3 - t2) / 1e3);
+    }
     g_close_ns.fetch_add(t1 - t0, std::memory_order_relaxed);
     g_launch_ns.fetch_add(t2 - t1, std::memory_order_relaxed);
     g_done_ns.fetch_add(t3 - t2, std::memory_order_relaxed);
@@ -967,7 +1012,9 @@ Coalescer* coalescer_for(int device, uint32_t P) {
 }  // namespace
 
 void coalesce_prepare(int device) {
-  if (t_holds_reg || env_long("QUICFEC_COALESCE", 1) == 0 || env_long("QUICFEC_RESIDENT", 1) == 0) return;
+  if (t_holds_reg || env_long("QUICFEC_COALESCE", 1) == 0) return;
+  prepare_spare_batch(device);
+  if (env_long("QUICFEC_RESIDENT", 1) == 0) return;
   (void)resident_for(device);
 }
 
@@ -1001,10 +1048,16 @@ bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* off
   // Pageable packets are staged per batch at cap * 10 * P bytes (cap >= 8): past this size the
   // legacy call runs alone on its context (QUIC datagrams are <= 1500 B).
   if (packet_size > kCoalesceMaxP) return false;
+  const uint64_t t_cls = now_ns();
   Coalescer* c = coalescer_for(device, packet_size);
   if (!c || num_groups > c->capacity() / 2) return false;
+  const uint64_t t_for = now_ns();
   *rc = c->encode(slab, sm == HostMem::kPinned ? static_cast<const uint8_t*>(sdev) : nullptr, offsets, num_groups,
                   repair_out, stream);
+  static std::atomic<int> stamps_left{env_long("QUICFEC_COALESCE_STAMPS", 0) != 0 ? 3 : 0};
+  if (stamps_left.load(std::memory_order_relaxed) > 0 && stamps_left.fetch_sub(1) > 0)  // diagnostic
+    std::fprintf(stderr, "{\"coalesced_call_us\": {\"classify\": %.1f, \"coalescer_for\": %.1f, \"encode\": %.1f}}\n",
+                 (t_cls - t_enter) / 1e3, (t_for - t_cls) / 1e3, (now_ns() - t_for) / 1e3);
   return true;
 }
 

@@ -2224,14 +2224,20 @@ uint32_t pick_tile(uint32_t cpp, uint32_t k, uint32_t P) {
   return best;
 }
 
+// Groups per workgroup of the tiled encodes (encode_bits: per half): QUICFEC_ENCODE_TILE (tuning
+// A/B; must fit 512 lanes), else pick_tile.
+uint32_t encode_tile(const EncodeLaunch& a) {
+  const uint32_t cpp = (a.P + 15u) / 16u;
+  const int tile_env = env_waves("QUICFEC_ENCODE_TILE", 0);
+  return tile_env > 0 && cpp > 0 && uint32_t(tile_env) * cpp <= 512 ? uint32_t(tile_env) : pick_tile(cpp, a.k, a.P);
+}
+
 // POL: parity is written once and not re-read by this kernel (non-temporal stores).
 template <int K, int R, int OFF, bool FIRST, int POL = kNtStore>
 hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
   const uint32_t cpp = (a.P + 15u) / 16u;
   // QUICFEC_ENCODE_TILE: groups per workgroup override (tuning A/B; must fit 512 lanes)
-  const int tile_env = env_waves("QUICFEC_ENCODE_TILE", 0);
-  const uint32_t tile = tile_env > 0 && cpp > 0 && uint32_t(tile_env) * cpp <= 512 ? uint32_t(tile_env)
-                                                                                    : pick_tile(cpp, a.k, a.P);
+  const uint32_t tile = encode_tile(a);
   const uint64_t gchunk = kMaxThreadsPerLaunch / cpp;
   for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
     const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
@@ -2273,8 +2279,7 @@ hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
 template <int K, int R, int W, int POL = kNtStore>
 hipError_t run_encode_bits(const EncodeLaunch& a, hipStream_t s) {
   const uint32_t cpp = (a.P + 15u) / 16u;
-  const int tile_env = env_waves("QUICFEC_ENCODE_TILE", 0);
-  const uint32_t tile = tile_env > 0 && uint32_t(tile_env) * cpp <= 512 ? uint32_t(tile_env) : pick_tile(cpp, a.k, a.P);
+  const uint32_t tile = encode_tile(a);
   if (tile == 0) return hipErrorInvalidValue;  // callers route P > 8,192 elsewhere
   const uint32_t bs = (tile * cpp + 63) / 64 * 64;
   const uint64_t gchunk = max_wave_blocks() * 2 * tile;
@@ -2365,8 +2370,7 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
       // QUICFEC_ENCODE_BITS_WINDOW: packets in flight per lane (4; 2: 5.70 ms, 8: 5.28, 20: 5.91-6.03).
       if (a.P <= 8192 && use_encode_bits(a.r)) {
         const int w = env_waves("QUICFEC_ENCODE_BITS_WINDOW", 4);
-        const uint32_t cpp = (a.P + 15u) / 16u;
-        const bool stg = use_stage_rows(a, 2 * pick_tile(cpp, a.k, a.P));
+        const bool stg = use_stage_rows(a, 2 * encode_tile(a));
         if (a.k == 20 && a.r == 5) {
           if (stg) return run_encode_bits<20, 5, 4, kNtStore | kStageRows>(a, s);
           return w >= 8 ? run_encode_bits<20, 5, 8>(a, s) : run_encode_bits<20, 5, 4>(a, s);
@@ -2374,7 +2378,7 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
         if (a.k == 10 && a.r == 3) return stg ? run_encode_bits<10, 3, 4, kNtStore | kStageRows>(a, s) : run_encode_bits<10, 3, 4>(a, s);
       }
       if (a.k == 10 && a.r == 3) {
-        if (pair && use_stage_rows(a, pick_tile((a.P + 15u) / 16u, a.k, a.P)))
+        if (pair && use_stage_rows(a, encode_tile(a)))
           return run_encode_v16<10, 3, 0, true, kNtStore | kPairMac | kStageRows>(a, 0, s);
         return pair ? run_encode_v16<10, 3, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<10, 3, 0, true>(a, 0, s);
       }
