@@ -1185,6 +1185,9 @@ __device__ __forceinline__ void runs_compute(const RunMeta& mt, uint32_t (&x)[K]
 // recover_runs: the wave's groups one after another (default), or with the next group's survivor
 // loads issued before this group's arithmetic and stores (probe form).
 constexpr int kRunPipe = 16384;
+// recover_runs (probe form): the run image leaves by plain stores while rows past the image keep
+// the POL's store policy.
+constexpr int kRunImgPlain = 32768;
 
 // stage_bytes: dynamic LDS of the run image (0: every row straight to HBM).  The image is used
 // only when P % 16 == 0 and `out` is 16-B aligned (the launcher passes 0 otherwise), so row
@@ -1409,8 +1412,9 @@ __global__ __launch_bounds__(64 * WAVES) void recover_runs(const uint8_t* __rest
   // the image leaves in 16-B pieces by consecutive threads: whole lines but at the run's ends
   uint8_t* run = out + static_cast<uint64_t>(first) * P;
   const uint32_t n16 = staged * P / 16u;
+  constexpr int kImgPol = (POL & kRunImgPlain) != 0 ? (POL & ~kNtStore) : POL;
   for (uint32_t c = tid; c < n16; c += 64u * WAVES)
-    st16<POL>(run + c * 16u, *reinterpret_cast<const u32x4*>(run_image + c * 16u));
+    st16<kImgPol>(run + c * 16u, *reinterpret_cast<const u32x4*>(run_image + c * 16u));
 }
 
 // Packed recover rows: row_start[g] = exclusive prefix sum over groups of the number of rows a

@@ -251,6 +251,11 @@ int main(int argc, char** argv) {
       RF("runs w4 nl st24K" + at, NL, 4, 256, 24576, 0, chk, outs[i])
       RF("runs w8 nostore" + at, NL, 8, 512, 0, 1, false, outs[i])
       RF("runs w8 pipe nl+ns st48K" + at, NL | NS | kRunPipe, 8, 512, 49152, 0, chk, outs[i])
+      // the store policy by path: the run image's copy-out plain, rows past it nt; a larger image
+      RF("runs w8 nl+ns img-plain st48K" + at, NL | NS | kRunImgPlain, 8, 512, 49152, 0, chk, outs[i])
+      RF("runs w8 nl+ns st64K" + at, NL | NS, 8, 512, 65536, 0, chk, outs[i])
+      RF("runs w8 nl st64K" + at, NL, 8, 512, 65536, 0, chk, outs[i])
+      RF("runs w8 nl+ns img-plain st64K" + at, NL | NS | kRunImgPlain, 8, 512, 65536, 0, chk, outs[i])
       RF("runs w4 tg256 pipe nl+ns st24K" + at, NL | NS | kRunPipe, 4, 256, 24576, 0, chk, outs[i])
     }
   }

@@ -28,7 +28,9 @@ SHAPES = {
            (6, "QUICFEC_ENCODE_BLOCKS", 2), (6, "QUICFEC_ENCODE_BLOCKS", 1), (3, "QUICFEC_ENCODE_BLOCKS", 3),
            (2, "QUICFEC_ENCODE_BLOCKS", 4), (3, "QUICFEC_ENCODE_BLOCKS", 2)],
     "c4": [(None, None, None), (2, "QUICFEC_ENCODE_WAVES", 0), (3, "QUICFEC_ENCODE_WAVES", 0), (5, "QUICFEC_ENCODE_WAVES", 0),
-           (6, "QUICFEC_ENCODE_WAVES", 0), (4, "QUICFEC_ENCODE_WAVES", 10), (4, "QUICFEC_ENCODE_WAVES", 15)],
+           (6, "QUICFEC_ENCODE_WAVES", 0), (4, "QUICFEC_ENCODE_WAVES", 10), (4, "QUICFEC_ENCODE_WAVES", 15),
+           (4, "QUICFEC_ENCODE_WAVES", 8), (4, "QUICFEC_ENCODE_WAVES", 12), (5, "QUICFEC_ENCODE_WAVES", 10),
+           (3, "QUICFEC_ENCODE_WAVES", 9), (5, "QUICFEC_ENCODE_WAVES", 12)],
 }
 KNOBS = ("QUICFEC_ENCODE_TILE", "QUICFEC_ENCODE_BLOCKS", "QUICFEC_ENCODE_WAVES")
 
