@@ -2290,8 +2290,11 @@ hipError_t run_encode_bits(const EncodeLaunch& a, hipStream_t s) {
   for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
     const uint64_t gn = (a.groups - g0 < gchunk) ? a.groups - g0 : gchunk;
     const uint32_t blocks = static_cast<uint32_t>((gn + 2 * tile - 1) / (2 * tile));
-    // uncapped: k=20 r=5 at 12 / 18 / 24 waves per CU within 0.2% (3 waves per SIMD by VGPRs)
-    const int waves = a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_ENCODE_WAVES", 0);
+    // Unstaged: uncapped (k=20 r=5 at 12 / 18 / 24 waves per CU within 0.2%, 3 waves per SIMD by
+    // VGPRs).  Staged rows (kStageRows): 2 workgroups per CU, 5.163 vs 5.246 ms uncapped on two
+    // boxes (scripts/sweep_encode_tiles.py, profiles/r05h, r05i).
+    constexpr int kDefWaves = (POL & kStageRows) != 0 ? 10 : 0;
+    const int waves = a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_ENCODE_WAVES", kDefWaves);
     uint32_t smem = occupancy_cap_lds(waves, bs / 64);
     if constexpr ((POL & kStageRows) != 0) smem = std::max<uint32_t>(smem, 2 * tile * R * a.P);
     hipLaunchKernelGGL((encode_bits<K, R, W, POL>), dim3(blocks), dim3(bs), smem, s, a.data, a.parity, g0, cpp, a.P,
@@ -2659,8 +2662,21 @@ uint64_t runs_blocks_per_launch(uint64_t groups) {
   return nb < mb ? nb : mb;
 }
 
+// The tile recover's row stores: plain (default) or non-temporal (QUICFEC_RUNS_NT_STORE=1, read
+// per launch).  At C5 (1% loss) plain stores were 10-15% faster on all three boxes measured in
+// round 5 (profiles/r05c, r05e, r05i probe_runs_c5.txt: 0.2246-0.2256 vs 0.2460-0.2647 ms at a
+// 48-KB image); round 4's boxes had the other order by 2-6%.
+template <int K, int R, int NM, int NT, int POL>
+hipError_t run_recover_runs_pol(const RunsLaunch& a, uint32_t stage, hipStream_t s);
+
 template <int K, int R, int NM, int NT>
 hipError_t run_recover_runs(const RunsLaunch& a, uint32_t stage, hipStream_t s) {
+  return env_waves("QUICFEC_RUNS_NT_STORE", 0) == 1 ? run_recover_runs_pol<K, R, NM, NT, kNtLoad | kNtStore>(a, stage, s)
+                                                    : run_recover_runs_pol<K, R, NM, NT, kNtLoad>(a, stage, s);
+}
+
+template <int K, int R, int NM, int NT, int POL>
+hipError_t run_recover_runs_pol(const RunsLaunch& a, uint32_t stage, hipStream_t s) {
   RankMeta rm{};
   for (int e = 1; e <= 3; ++e) {
     rm.base[e] = a.meta.base[e];
@@ -2677,7 +2693,7 @@ hipError_t run_recover_runs(const RunsLaunch& a, uint32_t stage, hipStream_t s) 
     const uint64_t g0 = c * per;
     const uint64_t gn = a.groups - g0 < per ? a.groups - g0 : per;
     const uint32_t nb = static_cast<uint32_t>((gn + kRunGroups - 1) / kRunGroups);
-    hipLaunchKernelGGL((recover_runs<K, R, NM, NT, kNtLoad | kNtStore, kRunWaves>), dim3(nb), dim3(64 * kRunWaves), stage, s, a.data + g0 * K * static_cast<uint64_t>(a.P),
+    hipLaunchKernelGGL((recover_runs<K, R, NM, NT, POL, kRunWaves>), dim3(nb), dim3(64 * kRunWaves), stage, s, a.data + g0 * K * static_cast<uint64_t>(a.P),
                        a.parity + g0 * R * static_cast<uint64_t>(a.P), a.masks + g0, gn, a.P, a.codebook, rm, a.out,
                        a.row_start + g0, a.status ? a.status + g0 : nullptr, lb, ticket, a.epoch + c, stage,
                        c > 0 ? totals + (c - 1) : nullptr, totals + c, c + 1 == launches ? a.total : nullptr, 0u);
