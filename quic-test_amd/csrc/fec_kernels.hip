@@ -2662,16 +2662,18 @@ uint64_t runs_blocks_per_launch(uint64_t groups) {
   return nb < mb ? nb : mb;
 }
 
-// The tile recover's row stores: plain (default) or non-temporal (QUICFEC_RUNS_NT_STORE=1, read
-// per launch).  At C5 (1% loss) plain stores were 10-15% faster on all three boxes measured in
-// round 5 (profiles/r05c, r05e, r05i probe_runs_c5.txt: 0.2246-0.2256 vs 0.2460-0.2647 ms at a
-// 48-KB image); round 4's boxes had the other order by 2-6%.
+// The tile recover's row stores: non-temporal (default) or plain (QUICFEC_RUNS_NT_STORE=0, read
+// per launch).  Back-to-back recovers alone favour plain stores by 10-15% on this round's boxes
+// (profiles/r05c, r05e, r05i probe_runs_c5.txt), but there the 0.13 GB of rows stay in the
+// Infinity Cache from one launch to the next (the form's time equals its no-store floor); in the
+// bench's step, after the encode's 15.6 GB, the two policies recover in the same 0.254 ms and the
+// plain rows' write-back lands in the next encode (+0.01 ms; profiles/r05j/ab_legs.jsonl).
 template <int K, int R, int NM, int NT, int POL>
 hipError_t run_recover_runs_pol(const RunsLaunch& a, uint32_t stage, hipStream_t s);
 
 template <int K, int R, int NM, int NT>
 hipError_t run_recover_runs(const RunsLaunch& a, uint32_t stage, hipStream_t s) {
-  return env_waves("QUICFEC_RUNS_NT_STORE", 0) == 1 ? run_recover_runs_pol<K, R, NM, NT, kNtLoad | kNtStore>(a, stage, s)
+  return env_waves("QUICFEC_RUNS_NT_STORE", 1) == 1 ? run_recover_runs_pol<K, R, NM, NT, kNtLoad | kNtStore>(a, stage, s)
                                                     : run_recover_runs_pol<K, R, NM, NT, kNtLoad>(a, stage, s);
 }
 

@@ -141,10 +141,8 @@ struct RunsLaunch {
 };
 // LDS run image per workgroup of 512 groups (tools/probe_runs.hip): C5's
 // ~59 rows per tile fit 48 KB (40 rows) mostly; two workgroups per CU.
-// recover_runs' run image per workgroup (QUICFEC_RUNS_STAGE).  64 KB with plain row stores: C5
-// 0.2172 vs 0.2256 ms at 48 KB on one box (profiles/r05i/probe_runs_c5.txt); two workgroups a CU
-// still fit (2 x 70 KB of 160 KB).
-constexpr int kRunsStageBytes = 64 * 1024;
+// recover_runs' run image per workgroup (QUICFEC_RUNS_STAGE).
+constexpr int kRunsStageBytes = 48 * 1024;
 bool runs_supported(uint32_t k, uint32_t r, uint32_t P);
 uint32_t runs_launches(uint64_t groups);
 uint64_t runs_workspace_bytes(uint64_t groups);

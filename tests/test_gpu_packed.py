@@ -280,16 +280,16 @@ def _check_packed(gpu_ctx, torch, oracle_mod, k, r, P, G, masks, out_offset=0):
 @pytest.mark.parametrize("k,r,P", [(10, 3, 1200), (10, 3, 700), (10, 3, 1400), (10, 3, 2000), (10, 3, 300),
                                    (10, 3, 1024), (10, 3, 1040), (10, 3, 1201), (10, 1, 1200), (10, 2, 1200),
                                    (10, 2, 700), (4, 2, 513), (4, 2, 1200)])
-@pytest.mark.parametrize("stage", ["default", "0", "16384", "49152", "nt"])
+@pytest.mark.parametrize("stage", ["default", "0", "16384", "65536", "plain"])
 def test_packed_runs_one_launch(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, k, r, P, stage):
     """The one-launch packed recover (recover_runs: decoupled look-back row starts, rows staged
     per workgroup in an LDS image and written as one run) on every mask-addressed piece layout,
     forced for mixed loss (QUICFEC_PACKED_RUNS=1), with the image off, small (most rows past it go
-    straight to HBM), round 4's 48 KB and the default 64 KB, and with non-temporal row stores
-    (QUICFEC_RUNS_NT_STORE=1, round 4's policy); bit-exact against the oracle."""
+    straight to HBM), the default 48 KB and 64 KB, and with plain row stores
+    (QUICFEC_RUNS_NT_STORE=0); bit-exact against the oracle."""
     monkeypatch.setenv("QUICFEC_PACKED_RUNS", "1")
-    if stage == "nt":
-        monkeypatch.setenv("QUICFEC_RUNS_NT_STORE", "1")
+    if stage == "plain":
+        monkeypatch.setenv("QUICFEC_RUNS_NT_STORE", "0")
     elif stage != "default":
         monkeypatch.setenv("QUICFEC_RUNS_STAGE", stage)
     G = 3_001
