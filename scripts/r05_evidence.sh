@@ -1,5 +1,6 @@
 #!/usr/bin/env bash
-# Round 5 evidence on the current build, in one gpurun call (everything in gpurun_out/${EVID}/):
+# Round 5 evidence on the current build, in two gpurun calls (PART=1: A-C, PART=2: D; everything
+# in gpurun_out/${EVID}/):
 #  A. the GPU suite and smoke (prints the library's source hash against the tree's);
 #  B. the legacy call site and the exit-path program under rocprofv3 (each must exit 0);
 #  C. a soak of the resident ring with the round-5 tags (16 and 100 streams, every repair
@@ -14,6 +15,7 @@ ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
 E="$ROOT/gpurun_out/${EVID:-r05}"
 mkdir -p "$E"
 cd "$ROOT"
+if [ "${PART:-1}" = 1 ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$E/pytest_gpu.log" 2>&1 || { tail -40 "$E/pytest_gpu.log"; exit 1; }
 tail -1 "$E/pytest_gpu.log"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$E/smoke.log" 2>&1
@@ -33,6 +35,8 @@ timeout -k 10 90 $B legacy 100 0 20 >> "$E/soak.jsonl" 2>&1
 grep '^{' "$E/soak.jsonl" | cut -c1-200
 QUICFEC_FUZZ_SEED=0x5EED5000 QUICFEC_FUZZ_BLOCKS=300 timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > "$E/fuzz_3000.log" 2>&1 || { tail -20 "$E/fuzz_3000.log"; exit 1; }
 tail -1 "$E/fuzz_3000.log"
+exit 0
+fi
 CFGS="${PMC_CFGS:-c2c3 c5 c4}" bash scripts/gpu_pmc.sh > "$E/pmc.log" 2>&1
 for c in ${PMC_CFGS:-c2c3 c5 c4}; do cp "$ROOT/gpurun_out/pmc_$c.json" "$ROOT/profiles/pmc_$c.json"; cp "$ROOT/gpurun_out/pmc_$c.json" "$E/pmc_$c.json"; done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$E/prof" -o run --output-format csv -- \
