@@ -2379,14 +2379,27 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
         const int w = env_waves("QUICFEC_ENCODE_BITS_WINDOW", 4);
         const bool stg = use_stage_rows(a, 2 * encode_tile(a));
         if (a.k == 20 && a.r == 5) {
-          if (stg) return run_encode_bits<20, 5, 4, kNtStore | kStageRows>(a, s);
+          if (stg) {
+            switch (env_waves("QUICFEC_ENCODE_MEMPOL", 0)) {  // as for k=10 r=3 below
+              case 1: return run_encode_bits<20, 5, 4, kStageRows>(a, s);
+              case 2: return run_encode_bits<20, 5, 4, kNtLoad | kNtStore | kStageRows>(a, s);
+              case 3: return run_encode_bits<20, 5, 4, kNtLoad | kStageRows>(a, s);
+              default: return run_encode_bits<20, 5, 4, kNtStore | kStageRows>(a, s);
+            }
+          }
           return w >= 8 ? run_encode_bits<20, 5, 8>(a, s) : run_encode_bits<20, 5, 4>(a, s);
         }
         if (a.k == 10 && a.r == 3) return stg ? run_encode_bits<10, 3, 4, kNtStore | kStageRows>(a, s) : run_encode_bits<10, 3, 4>(a, s);
       }
       if (a.k == 10 && a.r == 3) {
-        if (pair && use_stage_rows(a, encode_tile(a)))
-          return run_encode_v16<10, 3, 0, true, kNtStore | kPairMac | kStageRows>(a, 0, s);
+        if (pair && use_stage_rows(a, encode_tile(a))) {
+          switch (env_waves("QUICFEC_ENCODE_MEMPOL", 0)) {  // tuning A/B of the staged form's cache policy
+            case 1: return run_encode_v16<10, 3, 0, true, kPairMac | kStageRows>(a, 0, s);
+            case 2: return run_encode_v16<10, 3, 0, true, kNtLoad | kNtStore | kPairMac | kStageRows>(a, 0, s);
+            case 3: return run_encode_v16<10, 3, 0, true, kNtLoad | kPairMac | kStageRows>(a, 0, s);
+            default: return run_encode_v16<10, 3, 0, true, kNtStore | kPairMac | kStageRows>(a, 0, s);
+          }
+        }
         return pair ? run_encode_v16<10, 3, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<10, 3, 0, true>(a, 0, s);
       }
       if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 0, true>(a, 0, s);

@@ -23,7 +23,7 @@ case "${1:-run}" in
     $H -x hip -c -o $A/fec_coalesce.o quic-test_amd/csrc/fec_coalesce.cpp $SANF
     RT=$([ "$SANK" = thread ] && echo "" || echo -shared-libasan)
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -fsanitize=$SANK $RT -o $A/libfec_hip.so \
-      quic-test_amd/lib/fec_kernels.o $A/fec_shim.o $A/fec_batcher.o $A/fec_coalesce.o
+      quic-test_amd/lib/fec_kernels.o quic-test_amd/lib/src_hash.o $A/fec_shim.o $A/fec_batcher.o $A/fec_coalesce.o
     C="/opt/rocm/llvm/bin/clang++ -O1 -g -std=c++17 -fsanitize=$SANK $RT -fno-omit-frame-pointer -Iinclude -Iquic-test_amd/host"
     $C -fPIC -shared -o $A/libquicfec_host.so quic-test_amd/host/fec.cpp -L$A -lfec_hip -Wl,-rpath,'$ORIGIN'
     $C -o $A/host_mirror_test tests/csrc/host_mirror_test.cpp -L$A -lquicfec_host -lfec_hip oracle/liboracle.so \
@@ -50,5 +50,10 @@ case "${1:-run}" in
     QUICFEC_RESIDENT_VRAM=0 timeout -k 10 120 $A/batcher_latency legacy 16 0 2
     timeout -k 10 120 $A/exit_path_test mixed 360
     timeout -k 10 120 $A/exit_path_test mixed_hostring 360
+    # round 5: the ring's tag hooks (torn chunks, late address words, epoch scrubs) and poisoning
+    # under 8 threads, through the same host code
+    timeout -k 10 120 $A/exit_path_test tear 300
+    timeout -k 10 300 $A/exit_path_test epoch 6144
+    timeout -k 10 300 $A/exit_path_test poison_mt 2400
     ;;
 esac

@@ -21,9 +21,14 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO / "quic-test_amd"))
 import quicfec  # noqa: E402
 
-CONFIGS = {"c2": (10, 3, 1200, 1_000_000), "c4": (20, 5, 1200, 1_000_000)}
+CONFIGS = {"c2": (10, 3, 1200, 1_000_000), "c4": (20, 5, 1200, 1_000_000),
+           "c2pol": (10, 3, 1200, 1_000_000), "c4pol": (20, 5, 1200, 1_000_000)}
 # (tile, env var for occupancy, value); None = the library's default
 SHAPES = {
+    "c2pol": [(None, None, None), (None, "QUICFEC_ENCODE_MEMPOL", 1), (None, "QUICFEC_ENCODE_MEMPOL", 2),
+              (None, "QUICFEC_ENCODE_MEMPOL", 3)],
+    "c4pol": [(None, None, None), (None, "QUICFEC_ENCODE_MEMPOL", 1), (None, "QUICFEC_ENCODE_MEMPOL", 2),
+              (None, "QUICFEC_ENCODE_MEMPOL", 3)],
     "c2": [(None, None, None), (4, "QUICFEC_ENCODE_BLOCKS", 2), (4, "QUICFEC_ENCODE_BLOCKS", 3), (5, "QUICFEC_ENCODE_BLOCKS", 2),
            (6, "QUICFEC_ENCODE_BLOCKS", 2), (6, "QUICFEC_ENCODE_BLOCKS", 1), (3, "QUICFEC_ENCODE_BLOCKS", 3),
            (2, "QUICFEC_ENCODE_BLOCKS", 4), (3, "QUICFEC_ENCODE_BLOCKS", 2)],
@@ -32,18 +37,19 @@ SHAPES = {
            (4, "QUICFEC_ENCODE_WAVES", 8), (4, "QUICFEC_ENCODE_WAVES", 12), (5, "QUICFEC_ENCODE_WAVES", 10),
            (3, "QUICFEC_ENCODE_WAVES", 9), (5, "QUICFEC_ENCODE_WAVES", 12)],
 }
-KNOBS = ("QUICFEC_ENCODE_TILE", "QUICFEC_ENCODE_BLOCKS", "QUICFEC_ENCODE_WAVES")
+KNOBS = ("QUICFEC_ENCODE_TILE", "QUICFEC_ENCODE_BLOCKS", "QUICFEC_ENCODE_WAVES", "QUICFEC_ENCODE_MEMPOL")
 
 
 def set_shape(shape) -> str:
     for k in KNOBS:
         os.environ.pop(k, None)
     tile, var, val = shape
-    if tile is None:
+    if var is None:
         return "default"
-    os.environ["QUICFEC_ENCODE_TILE"] = str(tile)
+    if tile is not None:
+        os.environ["QUICFEC_ENCODE_TILE"] = str(tile)
     os.environ[var] = str(val)
-    return f"tile {tile} {var.split('_')[-1].lower()} {val}"
+    return (f"tile {tile} " if tile is not None else "") + f"{var.split('_')[-1].lower()} {val}"
 
 
 def main() -> None:
