@@ -2361,6 +2361,14 @@ hipError_t run_encode_generic(const EncodeLaunch& a, hipStream_t s) {
   return hipSuccess;
 }
 
+// A compile-time encode in its staged form (kStageRows) where the workgroup's window fits
+// (use_stage_rows), else with POL's direct stores.
+template <int K, int R, int OFF, int POL = kNtStore>
+hipError_t run_encode_v16_staged(const EncodeLaunch& a, hipStream_t s) {
+  if (use_stage_rows(a, encode_tile(a))) return run_encode_v16<K, R, OFF, true, POL | kStageRows>(a, 0, s);
+  return run_encode_v16<K, R, OFF, true, POL>(a, 0, s);
+}
+
 }  // namespace
 
 hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
@@ -2402,18 +2410,18 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
         }
         return pair ? run_encode_v16<10, 3, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<10, 3, 0, true>(a, 0, s);
       }
-      if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 0, true>(a, 0, s);
+      if (a.k == 10 && a.r == 1) return run_encode_v16_staged<10, 1, 0>(a, s);
       if (a.k == 20 && a.r == 5)
         return pair ? run_encode_v16<20, 5, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<20, 5, 0, true>(a, 0, s);
-      if (a.k == 4 && a.r == 2) return run_encode_v16<4, 2, 0, true>(a, 0, s);
+      if (a.k == 4 && a.r == 2) return run_encode_v16_staged<4, 2, 0>(a, s);
       // k=10 r=2 (the campaign's 20% FEC rate): compile-time k unless QUICFEC_ENCODE_RUNTIME_K=1
       // (A/B against the runtime-k loop)
       static const bool rt_k = env_waves("QUICFEC_ENCODE_RUNTIME_K", 0) == 1;
-      if (a.k == 10 && a.r == 2 && !rt_k) return run_encode_v16<10, 2, 0, true, kNtStore | kPairMac>(a, 0, s);
+      if (a.k == 10 && a.r == 2 && !rt_k) return run_encode_v16_staged<10, 2, 0, kNtStore | kPairMac>(a, s);
     } else if (a.off_kind == OffsetKind::kU32) {
-      if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 1, true>(a, 0, s);
+      if (a.k == 10 && a.r == 1) return run_encode_v16_staged<10, 1, 1>(a, s);
     } else if (a.off_kind == OffsetKind::kAddr) {
-      if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 3, true>(a, 0, s);
+      if (a.k == 10 && a.r == 1) return run_encode_v16_staged<10, 1, 3>(a, s);
     }
   }
   switch (a.off_kind) {

@@ -22,7 +22,8 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO / "quic-test_amd"))
 import quicfec  # noqa: E402
 
-CONFIGS = {"c2": (10, 3, 1200, 1 << 20), "c4": (20, 5, 1200, 1 << 20)}
+CONFIGS = {"c2": (10, 3, 1200, 1 << 20), "c4": (20, 5, 1200, 1 << 20), "k10r1": (10, 1, 1200, 1 << 20),
+           "k10r2": (10, 2, 1200, 1 << 20), "k4r2": (4, 2, 1200, 1 << 20)}
 
 
 def main() -> None:
