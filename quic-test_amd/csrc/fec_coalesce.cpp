@@ -308,7 +308,7 @@ class Coalescer {
   int device = 0;
   uint32_t P = 0, cap = 0;
   int max_inflight = 2;
-  int stamps_left = env_long("QUICFEC_COALESCE_STAMPS", 0) != 0 ? 3 : 0;  // leaders only, under no lock: diagnostic
+  std::atomic<int> stamps_left{env_long("QUICFEC_COALESCE_STAMPS", 0) != 0 ? 3 : 0};  // diagnostic: the first batches
   std::mutex mu;
   std::condition_variable cv_room;  // callers waiting for an open batch with room
   std::vector<std::unique_ptr<Batch>> batches;
@@ -404,8 +404,7 @@ class Coalescer {
       }
     }
     const uint64_t t3 = now_ns();
-    if (stamps_left > 0) {  // QUICFEC_COALESCE_STAMPS: the first batches' phases (diagnostic)
-      --stamps_left;
+    if (stamps_left.load(std::memory_order_relaxed) > 0 && stamps_left.fetch_sub(1) > 0) {  // QUICFEC_COALESCE_STAMPS
       std::fprintf(stderr, "{\"coalescer_batch_us\": {\"close\": %.1f, \"launch\": %.1f, \"done\": %.1f}}\n", (t1 - t0) / 1e3,
                    (t2 - t1) / 1e3, (t3 - t2) / 1e3);
     }
