@@ -99,7 +99,7 @@ int fec_decode_batch_rs_dev(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* 
 /* Recover: decode without touching d_data.  The rebuilt data shards of group g go to
  * d_rebuilt + (g*r + m)*P, m = 0..e-1 over the group's lost data shards in ascending shard
  * order -- the reference decoder hands recovered packets back as separate buffers
- * (decoder.go:29-34 Recovered{PacketID, Data}, :170-178), and a device-resident receiver
+ * (decoder.go:16-22 Recovered{PacketID, Data}, the list built at :195-207), and a device-resident receiver
  * consumes them the same way.  d_rebuilt holds num_groups*r*P bytes; slots m >= e of a
  * group, and all slots of an unrecoverable group, are left unwritten.  Writing the rebuilt
  * packets back to back (the write pattern of encode's parity rows) instead of scattered

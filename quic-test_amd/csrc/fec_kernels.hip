@@ -1049,7 +1049,7 @@ __global__ __launch_bounds__(256) void decode_fused(const uint8_t* __restrict__ 
 // ---------------------------------------------------------------------------------
 // Packed recover in one launch: recover_runs (fec_recover_batch_rs_dev_packed; DESIGN.md §5,
 // round 4).  The reference decoder hands rebuilt packets back as separate buffers
-// (decoder.go:29-34 `Recovered`); the packed list puts all of a batch's rebuilt packets back
+// (decoder.go:16-22 `Recovered`, listed at :195-207); the packed list puts all of a batch's rebuilt packets back
 // to back, group g's from row row_start[g] (exclusive prefix sum of the rows every group
 // rebuilds: its lost data shards when recoverable, else 0).
 //
@@ -2410,18 +2410,21 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
         }
         return pair ? run_encode_v16<10, 3, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<10, 3, 0, true>(a, 0, s);
       }
-      if (a.k == 10 && a.r == 1) return run_encode_v16_staged<10, 1, 0>(a, s);
+      // staged rows measured per shape (scripts/ab_stage_rows.py, profiles/r05k): k=10 r=1 level
+      // (2.383 vs 2.378 ms), k=10 r=2 -1.5% (2.537 vs 2.575), k=4 r=2 +8.9% (1.351 vs 1.241): the
+      // XOR row and k=4 keep their direct stores
+      if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 0, true>(a, 0, s);
       if (a.k == 20 && a.r == 5)
         return pair ? run_encode_v16<20, 5, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<20, 5, 0, true>(a, 0, s);
-      if (a.k == 4 && a.r == 2) return run_encode_v16_staged<4, 2, 0>(a, s);
+      if (a.k == 4 && a.r == 2) return run_encode_v16<4, 2, 0, true>(a, 0, s);
       // k=10 r=2 (the campaign's 20% FEC rate): compile-time k unless QUICFEC_ENCODE_RUNTIME_K=1
       // (A/B against the runtime-k loop)
       static const bool rt_k = env_waves("QUICFEC_ENCODE_RUNTIME_K", 0) == 1;
       if (a.k == 10 && a.r == 2 && !rt_k) return run_encode_v16_staged<10, 2, 0, kNtStore | kPairMac>(a, s);
     } else if (a.off_kind == OffsetKind::kU32) {
-      if (a.k == 10 && a.r == 1) return run_encode_v16_staged<10, 1, 1>(a, s);
+      if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 1, true>(a, 0, s);
     } else if (a.off_kind == OffsetKind::kAddr) {
-      if (a.k == 10 && a.r == 1) return run_encode_v16_staged<10, 1, 3>(a, s);
+      if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 3, true>(a, 0, s);
     }
   }
   switch (a.off_kind) {
