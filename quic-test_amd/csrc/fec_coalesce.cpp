@@ -447,7 +447,7 @@ bool alloc_coherent(Pinned& m, size_t bytes) {
 
 constexpr uint32_t kResidentOutBytes = 16u << 10;  // per slot: repair rows of callers whose buffer is pageable
 // per slot of the VRAM ring: an inline call's tagged repair chunks (kInlineMaxGroups x 128 x 16 B)
-constexpr uint32_t kInlineOutBytes = kInlineMaxGroups * kInlineChunksMax * 16;
+constexpr uint32_t kInlineOutBytes = kInlineMaxGroups * (kInlineMaxP / kInlinePayload) * 16;
 
 std::atomic<uint64_t> g_res_calls{0}, g_res_launches{0}, g_res_pre_ns{0}, g_res_wait_ns{0}, g_res_post_ns{0};
 std::atomic<uint64_t> g_res_inline{0}, g_res_vram{0};
@@ -563,8 +563,8 @@ class Resident {
     const uint64_t base = reinterpret_cast<uint64_t>(slab_dev);
     const uint64_t seq = next_seq.fetch_add(1, std::memory_order_relaxed);
     const uint32_t si = static_cast<uint32_t>(seq % kServerSlots);
-    const uint32_t tagv = server_tag(seq, epoch);
-    const uint64_t tag = uint64_t(tagv) << kServerTagShift;
+    const uint32_t tag16 = server_tag(seq, epoch);
+    const uint64_t tag = uint64_t(tag16) << kServerTagShift;
     // the slot's previous occupant (seq - kServerSlots) has been served and collected; if that
     // does not happen within the deadline, or no instance can be launched to serve it, the
     // Resident is poisoned and this call is not taken (its slot stays untouched: overwriting it
@@ -602,7 +602,7 @@ class Resident {
       // the packets into the slot's data area (both halves of each chunk carry the tag), then the header
       uint8_t* const area = vinl + size_t(si) * kInlineSlotBytes;
       if (tear) torn = (seq * 7919u) % (uint64_t(G) * kServerPackets * nch);
-      pack_inline(area, slab, offsets, G, P, tagv, torn);
+      pack_inline(area, slab, offsets, G, P, tag16, torn);
       __atomic_store_n(&sl->out, reinterpret_cast<uint64_t>(out_dev) | tag, __ATOMIC_RELAXED);
       __atomic_store_n(&sl->shape, uint64_t(P) | (uint64_t(G) << 16) | kServerInline | tag, __ATOMIC_RELAXED);
       if (torn != ~0ull) {
@@ -610,7 +610,7 @@ class Resident {
         std::atomic_thread_fence(std::memory_order_seq_cst);
         const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(100);
         while (std::chrono::steady_clock::now() < until) __builtin_ia32_pause();
-        store_half(area + torn * 16, chunk_half(slab + offsets[torn / nch], P, uint32_t(torn % nch) * kInlinePayload, tagv));
+        store_half(area + torn * 16, chunk_half(slab + offsets[torn / nch], P, uint32_t(torn % nch) * kInlinePayload, tag16));
       }
     } else {
       // groups after the first, then the first group and the header (every word tagged: the
@@ -643,7 +643,7 @@ class Resident {
     const uint8_t* const stg = inline_pk ? iouts.host + size_t(si) * kInlineOutBytes : nullptr;
     uint32_t landed = 0;
     auto half_ok = [&](uint32_t h) {  // 8-B half h of the staging carries this lap's tag
-      return (__atomic_load_n(reinterpret_cast<const uint64_t*>(stg) + h, __ATOMIC_ACQUIRE) >> 56) == tagv;
+      return (__atomic_load_n(reinterpret_cast<const uint64_t*>(stg) + h, __ATOMIC_ACQUIRE) >> 48) == tag16;
     };
     auto rows_landed = [&]() {
       if (!half_ok(2 * (G * nch - 1) + 1)) return false;
@@ -690,22 +690,22 @@ class Resident {
       }
     }
     if (rc == FEC_OK && inline_pk) {
-      // chunk c's 14 payload bytes to repair bytes [14c, 14c + 14): two 8-B copies per chunk,
-      // in increasing order, each overwriting the previous one's tag byte, while the copy stays
-      // inside the row (14c + 15 <= P); the last chunks byte-exact
-      const uint32_t nfast = P >= 15 ? (P - 15) / kInlinePayload + 1 : 0;
+      // chunk c's 12 payload bytes to repair bytes [12c, 12c + 12): two 8-B copies per chunk,
+      // in increasing order, each overwriting the previous one's two tag bytes, while the copy
+      // stays inside the row (12c + 14 <= P); the last chunks byte-exact
+      const uint32_t nfast = P >= 14 ? (P - 14) / kInlinePayload + 1 : 0;
       for (uint32_t g = 0; g < G; ++g) {
         const uint8_t* ch = stg + size_t(g) * nch * 16;
         uint8_t* dst = repair_out + size_t(g) * P;
         uint32_t c = 0;
         for (; c < nfast; ++c) {
           std::memcpy(dst + c * kInlinePayload, ch + c * 16, 8);
-          std::memcpy(dst + c * kInlinePayload + kInlineHalf, ch + c * 16 + 8, 8);
+          std::memcpy(dst + c * kInlinePayload + 6, ch + c * 16 + 8, 8);
         }
         for (; c < nch; ++c) {
           const uint32_t n = std::min(kInlinePayload, P - c * kInlinePayload);
-          std::memcpy(dst + c * kInlinePayload, ch + c * 16, std::min(kInlineHalf, n));
-          if (n > kInlineHalf) std::memcpy(dst + c * kInlinePayload + kInlineHalf, ch + c * 16 + 8, n - kInlineHalf);
+          std::memcpy(dst + c * kInlinePayload, ch + c * 16, std::min(6u, n));
+          if (n > 6) std::memcpy(dst + c * kInlinePayload + 6, ch + c * 16 + 8, n - 6);
         }
       }
     } else if (rc == FEC_OK && !repair_dev) {
@@ -840,31 +840,31 @@ class Resident {
     return found;
   }
 
-  // One 8-B half of an inline chunk: payload bytes [off, off + 7) of a packet of P bytes (zero
-  // past P) and the tag in the top byte (fec_kernels.hpp kServerInline).
-  static uint64_t chunk_half(const uint8_t* src, uint32_t P, uint32_t off, uint32_t tag) {
+  // One 8-B half of an inline chunk: payload bytes [off, off + 6) of a packet of P bytes (zero
+  // past P) and the tag in the top two bytes (fec_kernels.hpp kServerInline).
+  static uint64_t chunk_half(const uint8_t* src, uint32_t P, uint32_t off, uint32_t tag16) {
     uint64_t w = 0;
     if (off + 8 <= P) {
       std::memcpy(&w, src + off, 8);
-      w &= 0x00FFFFFFFFFFFFFFull;
+      w &= 0x0000FFFFFFFFFFFFull;
     } else if (off < P) {
-      std::memcpy(&w, src + off, std::min(kInlineHalf, P - off));
+      std::memcpy(&w, src + off, std::min(6u, P - off));
     }
-    return w | (uint64_t(tag) << 56);
+    return w | (uint64_t(tag16) << 48);
   }
 
   static void store_half(uint8_t* p, uint64_t w) { *reinterpret_cast<volatile uint64_t*>(p) = w; }
 
   // An inline slot's packets into its data area through the BAR (fec_kernels.hpp kServerInline):
-  // packet p = g * 10 + j as nch 16-B chunks, each two 8-B halves of 7 payload bytes and the tag;
+  // packet p = g * 10 + j as nch 16-B chunks, each two 8-B halves of 6 payload bytes and the tag;
   // each chunk one 16-B store (write-combined).  torn (tests, QUICFEC_RESIDENT_TEST_TEAR): that
   // chunk gets only its high half here; the caller stores the low half after the header.
   static void pack_inline(uint8_t* area, const uint8_t* slab, const uint32_t* offsets, uint32_t G, uint32_t P,
-                          uint32_t tagv, uint64_t torn) {
+                          uint32_t tag16, uint64_t torn) {
     typedef uint64_t v2u __attribute__((vector_size(16)));
     const uint32_t nch = (P + kInlinePayload - 1) / kInlinePayload;
-    const uint32_t nfast = P >= 15 ? (P - 15) / kInlinePayload + 1 : 0;  // chunks whose two 8-B reads stay in the packet
-    const uint64_t tg = uint64_t(tagv) << 56, lo56 = 0x00FFFFFFFFFFFFFFull;
+    const uint32_t nfast = P >= 14 ? (P - 14) / kInlinePayload + 1 : 0;  // chunks whose two 8-B reads stay in the packet
+    const uint64_t tg = uint64_t(tag16) << 48, lo48 = 0x0000FFFFFFFFFFFFull;
     for (uint32_t p = 0; p < G * kServerPackets; ++p) {
       const uint8_t* src = slab + offsets[p];
       volatile v2u* dst = reinterpret_cast<volatile v2u*>(area + size_t(p) * nch * 16);
@@ -874,20 +874,19 @@ class Resident {
         const uint32_t ct = static_cast<uint32_t>(torn % nch);
         for (uint32_t c = 0; c < nch; ++c)
           if (c != ct)
-            dst[c] = v2u{chunk_half(src, P, c * kInlinePayload, tagv),
-                         chunk_half(src, P, c * kInlinePayload + kInlineHalf, tagv)};
-        store_half(area + (size_t(p) * nch + ct) * 16 + 8, chunk_half(src, P, ct * kInlinePayload + kInlineHalf, tagv));
+            dst[c] = v2u{chunk_half(src, P, c * kInlinePayload, tag16), chunk_half(src, P, c * kInlinePayload + 6, tag16)};
+        store_half(area + (size_t(p) * nch + ct) * 16 + 8, chunk_half(src, P, ct * kInlinePayload + 6, tag16));
         continue;
       }
       uint32_t c = 0;
       for (; c < nfast; ++c) {
         uint64_t a, b;
         std::memcpy(&a, src + size_t(c) * kInlinePayload, 8);
-        std::memcpy(&b, src + size_t(c) * kInlinePayload + kInlineHalf, 8);
-        dst[c] = v2u{(a & lo56) | tg, (b & lo56) | tg};
+        std::memcpy(&b, src + size_t(c) * kInlinePayload + 6, 8);
+        dst[c] = v2u{(a & lo48) | tg, (b & lo48) | tg};
       }
       for (; c < nch; ++c)
-        dst[c] = v2u{chunk_half(src, P, c * kInlinePayload, tagv), chunk_half(src, P, c * kInlinePayload + kInlineHalf, tagv)};
+        dst[c] = v2u{chunk_half(src, P, c * kInlinePayload, tag16), chunk_half(src, P, c * kInlinePayload + 6, tag16)};
     }
   }
 

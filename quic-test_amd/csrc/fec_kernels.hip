@@ -2031,12 +2031,12 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
 #pragma unroll
             for (uint32_t j = 0; j < kServerPackets; ++j) __asm__ volatile("" : "+v"(v[j]));
           }
-          // both 8-B halves of every chunk carry this lap's tag in their top byte
+          // both 8-B halves of every chunk carry this lap's tag in their top two bytes
           const uint32_t tag = server_tag(seq, epoch);
           bool fresh = true;
           u32x4 acc = v[0];
 #pragma unroll
-          for (uint32_t j = 0; j < kServerPackets; ++j) fresh = fresh && (v[j].y >> 24) == tag && (v[j].w >> 24) == tag;
+          for (uint32_t j = 0; j < kServerPackets; ++j) fresh = fresh && (v[j].y >> 16) == tag && (v[j].w >> 16) == tag;
 #pragma unroll
           for (uint32_t j = 1; j < kServerPackets; ++j) acc ^= v[j];
           if (!fresh) {
@@ -2050,7 +2050,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
           // word from host memory -- the partial-line writes and the done word behind them left
           // the device only when a read to the host pushed them; profiles/r04_vram_store_forms.txt)
           sys_store_16b(reinterpret_cast<uint8_t*>(s_head[i][0] & kServerAddrMask) + (static_cast<uint64_t>(g) * cpp + col) * 16u,
-                        u32x4{acc.x, (acc.y & 0x00FFFFFFu) | (tag << 24), acc.z, (acc.w & 0x00FFFFFFu) | (tag << 24)});
+                        u32x4{acc.x, (acc.y & 0xFFFFu) | (tag << 16), acc.z, (acc.w & 0xFFFFu) | (tag << 16)});
           continue;
         }
         const uint32_t coff = col * 16u + 16u <= P ? col * 16u : P - 16u;

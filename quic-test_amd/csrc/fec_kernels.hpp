@@ -165,8 +165,7 @@ bool decode_compact_tables(const DecodeLaunch& a);
 //
 // Tags and the epoch.  A slot's tag is (lap & (epoch - 1)) + 1 with lap = seq / kServerSlots and
 // epoch a power of two (no division on the server's critical path), so the tags of one slot
-// repeat every `epoch` laps (128 by default, so a tag fits the one tag byte of an inline chunk's
-// 8-B half; QUICFEC_RESIDENT_TEST_EPOCH for tests).  A word left from the previous epoch could carry the current tag (a word written
+// repeat every `epoch` laps (32768 by default; QUICFEC_RESIDENT_TEST_EPOCH for tests).  A word left from the previous epoch could carry the current tag (a word written
 // exactly `epoch` laps ago and not since, e.g. a later group's address word under inline-only
 // calls), so the slot is scrubbed at every epoch boundary: the server zeroes the slot's words
 // and its inline data area after serving the last lap of an epoch, before that slot's done word
@@ -179,7 +178,7 @@ constexpr uint32_t kServerMaxGroups = 8;  // groups per slot (legacy calls of 1.
 constexpr uint32_t kServerPackets = 10;   // the legacy call's packets per group
 constexpr uint64_t kServerTagShift = 48;  // addresses below 2^48 (x86-64 user virtual addresses)
 constexpr uint64_t kServerAddrMask = (1ull << kServerTagShift) - 1;
-constexpr uint32_t kServerEpoch = 128;  // laps per tag epoch, a power of two (tags 1 .. epoch fit a byte)
+constexpr uint32_t kServerEpoch = 32768;  // laps per tag epoch, a power of two (tags 1 .. epoch fit 16 bits)
 __host__ __device__ inline uint32_t server_tag(uint64_t seq, uint32_t epoch) {
   return (static_cast<uint32_t>(seq / kServerSlots) & (epoch - 1u)) + 1u;
 }
@@ -196,24 +195,20 @@ struct alignas(64) ServerSlot {
 // calls live in uncached device memory that the host writes through the BAR, so the server's
 // poll and packet loads stay on the device.  An inline slot (shape bit kServerInline) carries
 // no addresses: its packets are copied by the host into the slot's data area, packet (g, j) as
-// 16-B chunks at chunk (g * 10 + j) * nch + c, nch = ceil(P / 14).  A chunk is two 8-B halves,
-// each 7 payload bytes and the slot's tag in its top byte:
-//   bytes 0..6 = payload [14c, 14c + 7), byte 7 = tag, bytes 8..14 = payload [14c + 7,
-//   14c + 14), byte 15 = tag (payload zero past P),
+// 16-B chunks at chunk (g * 10 + j) * nch + c, nch = ceil(P / 12).  A chunk is two 8-B halves,
+// each 6 payload bytes and the slot's 16-bit tag in its top two bytes:
+//   bytes 0..5 = payload [12c, 12c + 6), bytes 6..7 = tag, bytes 8..13 = payload [12c + 6,
+//   12c + 12), bytes 14..15 = tag (payload zero past P),
 // so each half validates itself (a 16-B write-combined store may reach the device as two 8-B
-// pieces) and no ordering of the host's stores through the BAR is assumed; 14 payload bytes per
-// 16 B crossing the BAR (round 5's first form carried 12, a 16-bit tag per half).  The rows come back
+// pieces) and no ordering of the host's stores through the BAR is assumed.  The rows come back
 // the same way: an inline slot's `out` is its output staging in page-locked host memory, repair
 // chunk (g, c) in the same two-half form at out + (g * nch + c) * 16, and the host takes the rows
 // once both halves of every chunk carry the tag (the done word then only says "consumed").
 constexpr uint64_t kServerInline = 1ull << 24;
 constexpr uint32_t kInlineMaxGroups = 4;
 constexpr uint32_t kInlineMaxP = 1536;
-constexpr uint32_t kInlineHalf = 7;                   // payload bytes of an 8-B half (its 8th byte: the tag)
-constexpr uint32_t kInlinePayload = 2 * kInlineHalf;  // payload bytes of a 16-B chunk
-constexpr uint32_t kInlineChunksMax = (kInlineMaxP + kInlinePayload - 1) / kInlinePayload;  // per packet
-constexpr uint32_t kInlineSlotBytes = kInlineMaxGroups * kServerPackets * kInlineChunksMax * 16;
-static_assert(kServerEpoch <= 255, "a tag must fit an inline half's tag byte");
+constexpr uint32_t kInlinePayload = 12;  // payload bytes of a 16-B chunk (6 per 8-B half)
+constexpr uint32_t kInlineSlotBytes = kInlineMaxGroups * kServerPackets * (kInlineMaxP / kInlinePayload) * 16;
 struct alignas(64) ServerControl {
   uint64_t stop;            // host -> device: leave at the next poll
   uint64_t pad0[7];
