@@ -2574,6 +2574,16 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, b
 #define QFEC_FUSED_P(M, KK, RR)                                                               \
   M(KK, RR, 0, 1) M(KK, RR, 0, 2) M(KK, RR, 0, 3) M(KK, RR, 0, 4) M(KK, RR, 1, 0) M(KK, RR, 1, 1) \
   M(KK, RR, 1, 2) M(KK, RR, 1, 3) M(KK, RR, 1, 4)
+  // tuning A/B of the C3 slot recover's cache policy in the bench's step (QUICFEC_DECODE_MEMPOL,
+  // read per launch: 1 NT loads + plain stores, 2 plain loads + NT stores, 3 plain both)
+  if (!dry && direct && a.compact_out && a.scan != kDecodeScanGroups && a.k == 10 && a.r == 3 && nm == 1 && nt == 1) {
+    switch (env_waves("QUICFEC_DECODE_MEMPOL", 0)) {
+      case 1: return run_decode_fused<10, 3, kNtLoad | kCompactOut, 1, 1, true>(a, s);
+      case 2: return run_decode_fused<10, 3, kNtStore | kCompactOut, 1, 1, true>(a, s);
+      case 3: return run_decode_fused<10, 3, kCompactOut, 1, 1, true>(a, s);
+      default: break;
+    }
+  }
   QFEC_FUSED_P(QFEC_FUSED_DS, 10, 3)
   QFEC_FUSED_R(10, 3, 1, 1)
   QFEC_FUSED_P(QFEC_FUSED_L, 20, 5)
