@@ -51,3 +51,7 @@ $T python bench.py --config c5 --e2e --no-cpu-baseline > "$E/legs/c5_satellite.j
 for f in "$E"/legs/*.json; do
   python -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); k=d['kernels']; print('$f'.split('/')[-1], d['value'], d['verified'], {n: (v['ms'], v['achieved_GBps']) for n, v in k.items()}, d['roofline']['frac'], d['roofline']['traffic'])"
 done
+# the --gpus 2 rehearsal (two gloo ranks sharing the card) at the driver's default sizes: every
+# section verified, traffic from this build's PMC (1M groups per rank = the PMC workload), wall_s
+QUICFEC_DIST_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 > "$E/bench_gpus2_gloo_rehearsal.json" 2> "$E/bench_gpus2.err"
+python -c "import json; d=json.loads(open('$E/bench_gpus2_gloo_rehearsal.json').read().strip().splitlines()[-1]); print('gpus2', d['n_gpus'], d['value'], d['verified'], d['roofline']['traffic'], d.get('wall_s'), {s: (d[s]['ranks'], d[s]['value'], d[s]['verified'], d[s]['roofline']['traffic']) for s in ('c4', 'c5_e2e')})"
