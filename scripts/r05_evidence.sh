@@ -4,7 +4,7 @@
 #  A. the GPU suite and smoke (prints the library's source hash against the tree's);
 #  B. the legacy call site and the exit-path program under rocprofv3 (each must exit 0);
 #  C. a soak of the resident ring with the round-5 tags (16 and 100 streams, every repair
-#     checked) and a 3,000-case random sweep against the oracle;
+#     checked) and a 12,000-case random sweep against the oracle;
 #  D. PMC traffic per config on this build (copied into profiles/ so the benches read this
 #     build's bytes), rocprofv3 kernel statistics of the default bench, the default bench line as
 #     the driver runs it, and the other configs' legs.
@@ -33,8 +33,8 @@ B=./quic-test_amd/lib/batcher_latency
 timeout -k 10 90 $B legacy 16 0 30 > "$E/soak.jsonl" 2>&1
 timeout -k 10 90 $B legacy 100 0 20 >> "$E/soak.jsonl" 2>&1
 grep '^{' "$E/soak.jsonl" | cut -c1-200
-QUICFEC_FUZZ_SEED=0x5EED5000 QUICFEC_FUZZ_BLOCKS=300 timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > "$E/fuzz_3000.log" 2>&1 || { tail -20 "$E/fuzz_3000.log"; exit 1; }
-tail -1 "$E/fuzz_3000.log"
+QUICFEC_FUZZ_SEED=0x5EED5000 QUICFEC_FUZZ_BLOCKS=1200 timeout -k 10 900 python -u -m pytest tests/test_gpu_fuzz.py -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > "$E/fuzz_12000.log" 2>&1 || { tail -20 "$E/fuzz_12000.log"; exit 1; }
+tail -1 "$E/fuzz_12000.log"
 exit 0
 fi
 CFGS="${PMC_CFGS:-c2c3 c5 c4}" bash scripts/gpu_pmc.sh > "$E/pmc.log" 2>&1
