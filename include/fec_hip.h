@@ -301,6 +301,8 @@ typedef struct {
   uint64_t resident_vram;      /* devices whose resident ring is in device memory (not reset) */
   uint64_t resident_bad_slots; /* polls that found a published slot with a word not yet landed, retried (not reset) */
   uint64_t resident_scrubs;    /* slots the resident encoder zeroed at a tag-epoch boundary (not reset) */
+  uint64_t resident_servers;   /* serving workgroups per resident instance (QUICFEC_RESIDENT_SERVERS), the
+                                  largest over devices; 0 before any resident encoder exists (not reset) */
 } FECCoalesceStats;
 
 /* Process-wide totals over every device and packet size; reset = 1 zeroes them after the read. */

@@ -522,6 +522,23 @@ class Resident {
     // no word of a slot that was never written carries a tag (tags are 1 .. epoch; alloc_coherent zeroed it)
     std::memset(r->ring.host, 0, sizeof(ServerSlot) * kServerSlots);
     if (env_long("QUICFEC_RESIDENT_VRAM", 1) != 0) r->setup_vram();
+    // Serving classes (fec_kernels.hpp kServerMaxClasses): QUICFEC_RESIDENT_SERVERS workgroups, a
+    // power of two up to 8 (rounded down); more than one share a few words of uncached device
+    // memory, and without them the instance is one workgroup.
+    const long want = std::min<long>(kServerMaxClasses, std::max(1L, env_long("QUICFEC_RESIDENT_SERVERS", 1)));
+    while (r->classes * 2 <= static_cast<uint32_t>(want)) r->classes *= 2;
+    if (r->classes > 1) {
+      void* c = nullptr;
+      if (hipExtMallocWithFlags(&c, sizeof(ServerCoord), hipDeviceMallocUncached) != hipSuccess ||
+          hipMemsetAsync(c, 0, sizeof(ServerCoord), r->stream) != hipSuccess || hipStreamSynchronize(r->stream) != hipSuccess) {
+        (void)hipGetLastError();
+        if (c) (void)hipFree(c);
+        c = nullptr;
+        r->classes = 1;
+      }
+      r->coord = static_cast<ServerCoord*>(c);
+    }
+    r->poll_slots = static_cast<uint32_t>(std::min<long>(kServerPoll, std::max(1L, env_long("QUICFEC_RESIDENT_POLL", kServerPoll))));
     r->collected.reset(new std::atomic<uint64_t>[kServerSlots]);
     for (uint32_t i = 0; i < kServerSlots; ++i) r->collected[i].store(0, std::memory_order_relaxed);
     return r.release();
@@ -539,8 +556,9 @@ class Resident {
   bool usable() const { return !broken.load(std::memory_order_acquire); }
 
   // The server's diagnostic counters (ServerControl): retried slots and epoch scrubs.
-  uint64_t bad_slots() const { return __atomic_load_n(&reinterpret_cast<const ServerControl*>(ctl.host)->bad_slots, __ATOMIC_ACQUIRE); }
-  uint64_t scrubs() const { return __atomic_load_n(&reinterpret_cast<const ServerControl*>(ctl.host)->scrubs, __ATOMIC_ACQUIRE); }
+  uint64_t bad_slots() const { return sum_classes(&ServerControl::bad_slots); }
+  uint64_t scrubs() const { return sum_classes(&ServerControl::scrubs); }
+  uint32_t serving_classes() const { return classes; }
 
   // The call's result, or kNotTaken when the Resident is (or just became) unusable before the
   // call published its slot: nothing of the caller's was handed to the device, and the caller
@@ -774,6 +792,9 @@ class Resident {
   bool tear = false;                          // QUICFEC_RESIDENT_TEST_TEAR
   uint64_t fail_at = ~0ull;                   // QUICFEC_RESIDENT_TEST_FAIL_AT
   uint32_t epoch = kServerEpoch;              // QUICFEC_RESIDENT_TEST_EPOCH
+  uint32_t classes = 1;                       // QUICFEC_RESIDENT_SERVERS
+  uint32_t poll_slots = kServerPoll;          // QUICFEC_RESIDENT_POLL
+  ServerCoord* coord = nullptr;               // device memory shared by the classes' workgroups
   std::atomic<bool> outs_ready{false};
   // The slots as the host writes them and as the device reads them: the page-locked ring, or
   // (setup_vram) one address for both, uncached device memory the host writes through the BAR.
@@ -913,6 +934,13 @@ class Resident {
     }
   }
 
+  uint64_t sum_classes(uint64_t (ServerControl::*field)[kServerMaxClasses]) const {
+    const ServerControl* c = reinterpret_cast<const ServerControl*>(ctl.host);
+    uint64_t s = 0;
+    for (uint32_t i = 0; i < kServerMaxClasses; ++i) s += __atomic_load_n(&(c->*field)[i], __ATOMIC_ACQUIRE);
+    return s;
+  }
+
   bool instance_alive() const {
     const uint64_t g = gen.load(std::memory_order_acquire);
     return g != 0 && __atomic_load_n(&reinterpret_cast<const ServerControl*>(ctl.host)->exited, __ATOMIC_ACQUIRE) != g;
@@ -927,16 +955,17 @@ class Resident {
       set_last_error("fec_encode_batch: the resident encoder is shutting down or out of service");
       return FEC_ERR_HIP;
     }
-    const uint64_t start = __atomic_load_n(&c->progress, __ATOMIC_ACQUIRE);
     const uint64_t g = gen.load(std::memory_order_relaxed) + 1;
     if (no_launch) {  // tests: an instance that is "alive" and never serves
       gen.store(g, std::memory_order_release);
       return FEC_OK;
     }
+    // every class resumes from its own progress mark (ServerControl::progress, read by the instance)
     BindDevice bd(device);
     const hipError_t e = bd.ok ? launch_legacy_server(ring_d, vinl, reinterpret_cast<uint64_t*>(done.dev),
-                                                      reinterpret_cast<ServerControl*>(ctl.dev), start, g, idle_ticks,
-                                                      life_ticks, stamps.host ? reinterpret_cast<uint64_t*>(stamps.dev) : nullptr,
+                                                      reinterpret_cast<ServerControl*>(ctl.dev), coord, classes, poll_slots, g,
+                                                      idle_ticks, life_ticks,
+                                                      stamps.host ? reinterpret_cast<uint64_t*>(stamps.dev) : nullptr,
                                                       epoch, stream)
                                : hipErrorInvalidDevice;
     if (e != hipSuccess) {
@@ -1082,12 +1111,14 @@ QFEC_EXPORT int fec_coalesce_stats(FECCoalesceStats* out, int reset) {
   out->resident_vram = g_res_vram.load();
   out->resident_bad_slots = 0;
   out->resident_scrubs = 0;
+  out->resident_servers = 0;
   {
     std::lock_guard<std::mutex> lk(g_reg_mu);
     for (auto& kv : g_resident)
       if (kv.second) {
         out->resident_bad_slots += kv.second->bad_slots();
         out->resident_scrubs += kv.second->scrubs();
+        out->resident_servers = std::max<uint64_t>(out->resident_servers, kv.second->serving_classes());
       }
   }
   if (reset) {

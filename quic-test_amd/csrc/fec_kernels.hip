@@ -1836,7 +1836,6 @@ __global__ __launch_bounds__(256) void copy_words(const uint4* __restrict__ src,
 // after kServerMaxPolls polls.
 constexpr uint32_t kServerThreads = 1024;
 constexpr uint32_t kServerMaxPolls = 1u << 22;
-constexpr uint32_t kServerPoll = 16;      // slots read per poll
 constexpr uint32_t kServerHeadWords = 16;  // words of a slot read by the poll: out, shape, addr[0..13]
 
 __device__ __forceinline__ void sys_store_release(uint64_t* p, uint64_t v) {
@@ -1895,17 +1894,29 @@ __device__ __forceinline__ u64x2 sys_load_16(const uint64_t* p) {
 // slot's rows by their tags, so its done word needs no acknowledgement of the row stores: a
 // batch of inline slots only waits for them when it also holds an addressed slot (or scrubs a
 // slot at an epoch boundary, fec_kernels.hpp server_tag).
+//
+// Serving classes (fec_kernels.hpp kServerMaxClasses): workgroup c of `classes` serves the seqs
+// of class c (seq % classes == c) and steps through them `classes` apart; its poll, run, done
+// words and progress mark are its class's alone.  The workgroups share only the ServerCoord
+// words (uncached device memory, read with the poll): an idle flag each, and the leave word any
+// of them sets when it leaves on its own (the stop word, the life bound, its poll bound) or finds
+// every class idle -- so an instance leaves as a whole, and the last workgroup out stores the
+// exited word the host relaunches on.
 __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __restrict__ ring,
                                                                 uint8_t* __restrict__ inl,
                                                                 uint64_t* __restrict__ done,
-                                                                ServerControl* __restrict__ ctl, uint64_t start_seq,
-                                                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+                                                                ServerControl* __restrict__ ctl,
+                                                                ServerCoord* __restrict__ coord, uint32_t classes,
+                                                                uint32_t poll_slots, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
                                                                 uint64_t* __restrict__ stamps, uint32_t epoch) {
   __shared__ uint64_t s_next;
-  __shared__ uint32_t s_n, s_exit, s_stop, s_ack;
+  __shared__ uint32_t s_n, s_exit, s_stop, s_ack, s_told;
+  __shared__ uint64_t s_idle[kServerMaxClasses];
   __shared__ uint32_t s_first[kServerPoll + 1];  // work items before slot i of the run
   __shared__ uint32_t s_P[kServerPoll], s_cpp[kServerPoll], s_inl[kServerPoll], s_bad[kServerPoll];
   __shared__ uint64_t s_head[kServerPoll][kServerHeadWords];  // out, shape, addr[0..13] (tagged)
+  const uint32_t K = classes, cls = blockIdx.x;
+  if (cls != 0) stamps = nullptr;  // class 0's stamps only
   // VRAM ring: every poll also reads the first 16 KB of the next slot's inline data area, one
   // 16-B chunk a thread, in flight with the header loads -- an inline slot found complete at
   // the head of the run then takes its chunks from here instead of a second dependent round
@@ -1915,11 +1926,15 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   uint64_t t0 = 0, t_last = 0;  // thread 0 only
   uint64_t n_bad = 0, n_scrub = 0;  // thread 0 only: the diagnostic counters, continued from the last instance's
+  bool was_idle = false;            // thread 0 only: this class's idle flag as last published
   if (tid == 0) {
-    s_next = start_seq;
+    // the class's first unserved seq: its progress mark (the first instance's marks are 0, so
+    // rounded up into the class)
+    const uint64_t p = *reinterpret_cast<const volatile uint64_t*>(&ctl->progress[cls]);
+    s_next = p + (cls + K - static_cast<uint32_t>(p % K)) % K;
     t0 = t_last = static_cast<uint64_t>(wall_clock64());
-    n_bad = *reinterpret_cast<const volatile uint64_t*>(&ctl->bad_slots);
-    n_scrub = *reinterpret_cast<const volatile uint64_t*>(&ctl->scrubs);
+    n_bad = *reinterpret_cast<const volatile uint64_t*>(&ctl->bad_slots[cls]);
+    n_scrub = *reinterpret_cast<const volatile uint64_t*>(&ctl->scrubs[cls]);
   }
   lds_barrier();
   // Diagnostic stamps (stamps != nullptr, QUICFEC_RESIDENT_STAMPS): thread 0's wall clock at the
@@ -1935,23 +1950,31 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
     if (inl != nullptr)
       pre = __builtin_nontemporal_load(reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(
           reinterpret_cast<uintptr_t>(inl + static_cast<uint64_t>(next % kServerSlots) * kInlineSlotBytes) + tid * 16u));
-    if (tid < kServerPoll * kServerHeadWords / 2) {
+    constexpr uint32_t kPollLanes = kServerPoll * kServerHeadWords / 2;
+    if (tid < kPollLanes) {
       const uint32_t i = tid / (kServerHeadWords / 2), piece = tid % (kServerHeadWords / 2);
-      const u64x2 v = sys_load_16(reinterpret_cast<const uint64_t*>(ring + (next + i) % kServerSlots) + 2 * piece);
+      const u64x2 v = i >= poll_slots ? u64x2{0, 0} : sys_load_16(reinterpret_cast<const uint64_t*>(ring + (next + uint64_t(i) * K) % kServerSlots) + 2 * piece);
       s_head[i][2 * piece] = v.x;
       s_head[i][2 * piece + 1] = v.y;
-    } else if (tid == kServerPoll * kServerHeadWords / 2) {
+    } else if (tid == kPollLanes) {
       // with the ring in VRAM the stop word (host memory) would make every poll a PCIe round
       // trip again: every 16th poll reads it (the idle and life bounds hold regardless)
       s_stop = (inl == nullptr || (it & 15u) == 0) ? (*reinterpret_cast<const volatile uint64_t*>(&ctl->stop) != 0 ? 1u : 0u)
                                                    : 0u;
+    } else if (coord != nullptr && tid == kPollLanes + 1) {
+      s_told = sys_load_16(&coord->leave).x == gen ? 1u : 0u;
+    } else if (coord != nullptr && tid >= kPollLanes + 2 && tid < kPollLanes + 2 + kServerMaxClasses / 2) {
+      const uint32_t q = tid - (kPollLanes + 2);
+      const u64x2 v = sys_load_16(&coord->idle[2 * q]);
+      s_idle[2 * q] = v.x;
+      s_idle[2 * q + 1] = v.y;
     }
     s_pre[tid] = pre;
     lds_barrier();
     if (tid < 64) {
-      const uint64_t seq = next + lane;
+      const uint64_t seq = next + uint64_t(lane) * K;
       const uint64_t tag = server_tag(seq, epoch);
-      bool ok = lane < kServerPoll;
+      bool ok = lane < poll_slots;
       bool inline_slot = false;
       if (ok) {
         // out, shape and (unless the packets are inline) the first group's 10 addresses (words 0 .. 11)
@@ -1989,7 +2012,22 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
         const bool stop = s_stop != 0;
         s_n = n;
         s_ack = addressed != 0 ? 1u : 0u;
-        s_exit = (stop || now - t0 > life_ticks || (n == 0 && now - t_last > idle_ticks)) ? 1u : 0u;
+        const bool idle = n == 0 && now - t_last > idle_ticks;
+        bool leave = stop || now - t0 > life_ticks || it + 1 == kServerMaxPolls;
+        if (coord == nullptr) {
+          leave = leave || idle;
+        } else {
+          // every class idle (this one now, the others by their published flags), or told to leave
+          bool all_idle = idle;
+          for (uint32_t c = 0; c < K; ++c) all_idle = all_idle && (c == cls || s_idle[c] == gen);
+          if (idle != was_idle) {
+            sys_store_relaxed(&coord->idle[cls], idle ? gen : 0);
+            was_idle = idle;
+          }
+          if ((leave || all_idle) && s_told == 0) sys_store_relaxed(&coord->leave, gen);
+          leave = leave || all_idle || s_told != 0;
+        }
+        s_exit = leave ? 1u : 0u;
       }
     }
     lds_barrier();
@@ -2014,8 +2052,8 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
         const uint32_t local = w - s_first[i];
         const uint32_t cpp = s_cpp[i], P = s_P[i];
         const uint32_t g = local / cpp, col = local - g * cpp;
+        const uint64_t seq = next + uint64_t(i) * K;
         if (s_inl[i] != 0) {
-          const uint64_t seq = next + i;
           const uint32_t c0 = g * kServerPackets * cpp + col;  // chunk (g, 0, col)
           u32x4 v[kServerPackets];
           if (i == 0 && (g + 1) * kServerPackets * cpp <= kServerThreads) {
@@ -2062,7 +2100,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
           // written by the host before the slot's first group and header, seen complete above;
           // relaxed system-scope loads (uncached, all ten in flight: volatile loads were each
           // followed by a full wait, one PCIe round trip apiece)
-          const uint64_t* src = ring[(next + i) % kServerSlots].addr + g * kServerPackets;
+          const uint64_t* src = ring[seq % kServerSlots].addr + g * kServerPackets;
 #pragma unroll
           for (uint32_t j = 0; j < kServerPackets; ++j)
             ad[j] = __hip_atomic_load(reinterpret_cast<const __attribute__((address_space(1))) uint64_t*>(
@@ -2070,7 +2108,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           // tagged like the header: in a VRAM ring the host's stores through the BAR carry no
           // order, and a word of the previous lap marks the slot bad (served by a later poll)
-          const uint64_t tag = server_tag(next + i, epoch);
+          const uint64_t tag = server_tag(seq, epoch);
           bool fresh = true;
 #pragma unroll
           for (uint32_t j = 0; j < kServerPackets; ++j) fresh = fresh && (ad[j] >> kServerTagShift) == tag;
@@ -2118,9 +2156,9 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
           n_ok = k;
           break;
         }
-        scrub = scrub || server_scrub_after(next + k, epoch);
+        scrub = scrub || server_scrub_after(next + uint64_t(k) * K, epoch);
       }
-      if (tid == 0 && n_ok < n) sys_store_relaxed(&ctl->bad_slots, ++n_bad);
+      if (tid == 0 && n_ok < n) sys_store_relaxed(&ctl->bad_slots[cls], ++n_bad);
       if (scrub) {
         // The last lap of an epoch (fec_kernels.hpp server_tag): zero the served slot's words and
         // inline data area before its done word, so no word of this epoch can match a tag of the
@@ -2128,7 +2166,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
         constexpr uint32_t kSlotPieces = sizeof(ServerSlot) / 16u;
         const uint32_t pieces = kSlotPieces + (inl != nullptr ? kInlineSlotBytes / 16u : 0u);
         for (uint32_t k = 0; k < n_ok; ++k) {
-          const uint64_t seq = next + k;
+          const uint64_t seq = next + uint64_t(k) * K;
           if (!server_scrub_after(seq, epoch)) continue;
           uint8_t* slot = reinterpret_cast<uint8_t*>(ring + seq % kServerSlots);
           uint8_t* area = inl != nullptr ? inl + (seq % kServerSlots) * kInlineSlotBytes : nullptr;
@@ -2138,12 +2176,15 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
         }
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every zero in place before the done words
         lds_barrier();
-        if (tid == 0) sys_store_relaxed(&ctl->scrubs, n_scrub);
+        if (tid == 0) sys_store_relaxed(&ctl->scrubs[cls], n_scrub);
       }
-      if (tid < n_ok) sys_store_relaxed(&done[(next + tid) % kServerSlots], next + tid + 1);
+      if (tid < n_ok) {
+        const uint64_t seq = next + uint64_t(tid) * K;
+        sys_store_relaxed(&done[seq % kServerSlots], seq + 1);
+      }
       if (tid == 0) {
-        s_next = next + n_ok;
-        sys_store_relaxed(&ctl->progress, next + n_ok);
+        s_next = next + uint64_t(n_ok) * K;
+        sys_store_relaxed(&ctl->progress[cls], next + uint64_t(n_ok) * K);
       }
       if (stamps != nullptr && tid == 0) {
         st_t[5] = static_cast<uint64_t>(wall_clock64());
@@ -2166,8 +2207,19 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
     if (leave) break;
   }
   if (tid == 0) {
-    sys_store_release(&ctl->progress, s_next);
-    sys_store_release(&ctl->exited, gen);
+    sys_store_release(&ctl->progress[cls], s_next);
+    bool last = true;
+    if (coord != nullptr) {
+      // count this workgroup out of instance gen (the word still holds the previous instance's
+      // count until the first of this one's); at most `classes` contenders, so the loop ends
+      uint64_t v = __hip_atomic_load(&coord->exits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), nv = 0;
+      do {
+        nv = (v >> 8) == gen ? v + 1 : (gen << 8) | 1u;
+      } while (!__hip_atomic_compare_exchange_strong(&coord->exits, &v, nv, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM));
+      last = (nv & 0xFFu) == K;
+    }
+    if (last) sys_store_release(&ctl->exited, gen);
   }
 }
 
@@ -2916,11 +2968,17 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
 }
 
 hipError_t launch_legacy_server(ServerSlot* ring, uint8_t* inl, uint64_t* done, ServerControl* ctl,
-                                uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                uint64_t* stamps, uint32_t epoch, hipStream_t s) {
+                                ServerCoord* coord, uint32_t classes, uint32_t poll_slots, uint64_t gen,
+                                uint64_t idle_ticks, uint64_t life_ticks, uint64_t* stamps, uint32_t epoch,
+                                hipStream_t s) {
   if (epoch < 1u || epoch > kServerEpoch || (epoch & (epoch - 1u)) != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(legacy_server, dim3(1), dim3(kServerThreads), 0, s, ring, inl, done, ctl, start_seq, gen,
-                     idle_ticks, life_ticks, stamps, epoch);
+  // classes: a power of two (it divides kServerSlots), with the shared words when more than one;
+  // gen fits the exit count's 56 bits
+  if (classes < 1u || classes > kServerMaxClasses || (classes & (classes - 1u)) != 0 || (classes > 1u && !coord) ||
+      gen == 0 || gen >= (1ull << 56) || poll_slots < 1u || poll_slots > kServerPoll)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(legacy_server, dim3(classes), dim3(kServerThreads), 0, s, ring, inl, done, ctl,
+                     classes > 1u ? coord : nullptr, classes, poll_slots, gen, idle_ticks, life_ticks, stamps, epoch);
   return hipGetLastError();
 }
 

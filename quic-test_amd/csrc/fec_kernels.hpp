@@ -160,8 +160,9 @@ bool decode_compact_tables(const DecodeLaunch& a);
 // complete slot by the tags alone, whatever order its reads of the host's stores land in.  An
 // aligned 8-B store is the unit the host's stores are assumed to arrive in (x86 quadword
 // atomicity); nothing larger is assumed to arrive in one piece, so every 8-B word is
-// self-validating.  One resident workgroup serves the slots in seq order and stores
-// done[seq % kServerSlots] = seq + 1.  Calls are served without a kernel launch each.
+// self-validating.  Resident workgroups serve the slots in seq order (one per serving class,
+// below) and store done[seq % kServerSlots] = seq + 1.  Calls are served without a kernel launch
+// each.
 //
 // Tags and the epoch.  A slot's tag is (lap & (epoch - 1)) + 1 with lap = seq / kServerSlots and
 // epoch a power of two (no division on the server's critical path), so the tags of one slot
@@ -209,25 +210,44 @@ constexpr uint32_t kInlineMaxGroups = 4;
 constexpr uint32_t kInlineMaxP = 1536;
 constexpr uint32_t kInlinePayload = 12;  // payload bytes of a 16-B chunk (6 per 8-B half)
 constexpr uint32_t kInlineSlotBytes = kInlineMaxGroups * kServerPackets * (kInlineMaxP / kInlinePayload) * 16;
+// Serving classes.  An instance is `classes` workgroups (a power of two, 1 .. kServerMaxClasses,
+// so it divides kServerSlots): workgroup c serves the seqs with seq % classes == c, in order, so
+// concurrent callers are served by independent poll -> serve -> done cycles.
+constexpr uint32_t kServerMaxClasses = 8;
+constexpr uint32_t kServerPoll = 16;  // the most slots one poll reads (and one batch serves)
 struct alignas(64) ServerControl {
   uint64_t stop;            // host -> device: leave at the next poll
   uint64_t pad0[7];
-  uint64_t progress;        // device -> host: every seq below this has been served
-  uint64_t exited;          // device -> host: generation of the last instance that left
-  uint64_t bad_slots;       // device -> host: polls that found a slot with a word not yet landed (diagnostic)
-  uint64_t scrubs;          // device -> host: slots scrubbed at an epoch boundary (diagnostic)
-  uint64_t pad1[4];
+  uint64_t exited;          // device -> host: generation of the last instance that left (its last workgroup)
+  uint64_t pad1[7];
+  uint64_t progress[kServerMaxClasses];   // device -> host: every seq of class c below progress[c] was served
+  uint64_t bad_slots[kServerMaxClasses];  // device -> host: polls that found a slot with a word not yet landed (diagnostic)
+  uint64_t scrubs[kServerMaxClasses];     // device -> host: slots scrubbed at an epoch boundary (diagnostic)
 };
-// One resident workgroup serving the ring from start_seq until it has found nothing to do for
-// idle_ticks, or lived life_ticks (wall-clock ticks, hipDeviceAttributeWallClockRate), or the
-// host sets ctl->stop; on leaving it stores progress and then exited = gen.
-// stamps: nullptr, or 256 x 8 words of host memory for the diagnostic phase stamps (QUICFEC_RESIDENT_STAMPS).
+// Device memory the workgroups of one instance share (uncached: they run on different XCDs, each
+// with its own L2).  Words are tagged with the instance's generation, so nothing is reset
+// between instances.
+struct alignas(64) ServerCoord {
+  uint64_t leave;                      // gen: every workgroup of instance gen leaves at its next poll
+  uint64_t exits;                      // (gen << 8) | workgroups of instance gen that have left
+  uint64_t pad[6];
+  uint64_t idle[kServerMaxClasses];    // gen while class c's workgroup has been idle for idle_ticks, else 0
+};
+// One resident instance serving the ring, each class from its progress mark, until every class
+// has found nothing to do for idle_ticks, or it lived life_ticks (wall-clock ticks,
+// hipDeviceAttributeWallClockRate), or the host sets ctl->stop; on leaving a workgroup stores its
+// class's progress, and the last one to leave stores exited = gen.
+// coord: nullptr when classes == 1.  poll_slots: slots of its class a workgroup reads per poll
+// (1 .. kServerPoll), the longest run one batch serves.
+// stamps: nullptr, or 256 x 8 words of host memory for the diagnostic phase stamps of class 0
+// (QUICFEC_RESIDENT_STAMPS).
 // inl: the inline data areas (kInlineSlotBytes per slot) when the ring is in VRAM, else nullptr;
 // then the host's stop word (host memory) is read by every 16th poll only, not every poll.
 // epoch: laps per tag epoch (server_tag), a power of two, 1 .. kServerEpoch.
 hipError_t launch_legacy_server(ServerSlot* ring, uint8_t* inl, uint64_t* done, ServerControl* ctl,
-                                uint64_t start_seq, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                uint64_t* stamps, uint32_t epoch, hipStream_t s);
+                                ServerCoord* coord, uint32_t classes, uint32_t poll_slots, uint64_t gen,
+                                uint64_t idle_ticks, uint64_t life_ticks, uint64_t* stamps, uint32_t epoch,
+                                hipStream_t s);
 
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);

@@ -53,10 +53,10 @@ void report(const char* mode, int streams, std::vector<double>& us, double secon
   fec_coalesce_stats(&cs, 0);
   std::printf("{\"mode\": \"%s\", \"streams\": %d, \"groups\": %zu, \"seconds\": %.3f, \"groups_per_s\": %.1f, "
               "\"delay_us\": {\"p50\": %.2f, \"p99\": %.2f}, \"errors\": %ld, \"resident_calls\": %llu, "
-              "\"resident_inline\": %llu, \"resident_vram\": %llu}\n",
+              "\"resident_inline\": %llu, \"resident_vram\": %llu, \"resident_servers\": %llu}\n",
               mode, streams, us.size(), seconds, double(us.size()) / seconds, pct(0.5), pct(0.99), errors,
               (unsigned long long)cs.resident_calls, (unsigned long long)cs.resident_inline,
-              (unsigned long long)cs.resident_vram);
+              (unsigned long long)cs.resident_vram, (unsigned long long)cs.resident_servers);
   std::fflush(stdout);
 }
 

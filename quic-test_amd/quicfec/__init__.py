@@ -510,7 +510,7 @@ def xor_packets(packets, packet_size: int, repair, variant: str = "avx2") -> Non
 
 COALESCE_STATS = ("calls", "groups", "batches", "max_batch", "max_calls", "close_ns", "launch_ns", "done_ns", "resident_calls", "resident_launches",
                   "resident_pre_ns", "resident_wait_ns", "resident_post_ns", "resident_inline", "resident_vram",
-                  "resident_bad_slots", "resident_scrubs")
+                  "resident_bad_slots", "resident_scrubs", "resident_servers")
 
 
 def coalesce_stats(reset: bool = False) -> dict:

@@ -32,14 +32,23 @@
 //    that one and the ones in flight when the Resident went out of service included -- must
 //    return 0 with the right row (served, or run on the coalescer path).
 //
+//  * cycles_mt: 4 threads with a context each make one-group calls in bursts of 8 with a 2-ms
+//    pause after each (QUICFEC_RESIDENT_IDLE_US=300), so resident instances leave and are
+//    relaunched many times while other threads' calls are in flight -- with several serving
+//    classes (QUICFEC_RESIDENT_SERVERS) every class must resume from its own progress mark.
+//
+// Every mode honours QUICFEC_RESIDENT_SERVERS from the environment (serving workgroups).
+//
 //   exit_path_test [resident|hostring|coalescer|pageable|nolaunch|mixed|mixed_hostring|tear|
-//                   epoch|epoch_hostring|poison_mt] [calls]
+//                   epoch|epoch_hostring|poison_mt|cycles_mt] [calls]
 //   -> one JSON line at exit: {"mode", "calls", "repairs_ok", "first_rc", "calls_after_exit", "names",
-//                              "resident_calls", "resident_inline", "resident_vram", "bad_slots", "scrubs"}
+//                              "resident_calls", "resident_inline", "resident_vram", "bad_slots", "scrubs",
+//                              "resident_launches", "resident_servers"}
 // Built by quic-test_amd/csrc/Makefile (target tests); run by tests/test_gpu_coalesce.py.
 #include <dlfcn.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -62,6 +71,7 @@ std::string g_names;
 std::string g_mode = "resident";
 int g_calls = 0, g_first_rc = 0;
 unsigned long long g_resident_calls = 0, g_resident_inline = 0, g_resident_vram = 0, g_bad = 0, g_scrubs = 0;
+unsigned long long g_launches = 0, g_servers = 0;
 bool g_ok = true;
 
 bool from_library(void* ret) {
@@ -86,15 +96,29 @@ void mark_exit() { g_exiting.store(true, std::memory_order_release); }
 void report() {
   std::printf("{\"mode\": \"%s\", \"calls\": %d, \"repairs_ok\": %s, \"first_rc\": %d, \"calls_after_exit\": %d, "
               "\"names\": \"%s\", \"resident_calls\": %llu, \"resident_inline\": %llu, \"resident_vram\": %llu, "
-              "\"bad_slots\": %llu, \"scrubs\": %llu}\n",
+              "\"bad_slots\": %llu, \"scrubs\": %llu, \"resident_launches\": %llu, \"resident_servers\": %llu}\n",
               g_mode.c_str(), g_calls, g_ok ? "true" : "false", g_first_rc, g_after.load(), g_names.c_str(), g_resident_calls,
-              g_resident_inline, g_resident_vram, g_bad, g_scrubs);
+              g_resident_inline, g_resident_vram, g_bad, g_scrubs, g_launches, g_servers);
   std::fflush(stdout);
 }
 
-// One thread of poison_mt: `calls` one-group calls of 10 x 1200 B on a context of its own,
-// every row checked against the XOR.  Returns false on any failure.
-bool poison_thread(int t, int calls) {
+// The library's counters into the report.
+void take_stats() {
+  FECCoalesceStats st{};
+  fec_coalesce_stats(&st, 0);
+  g_resident_calls = st.resident_calls;
+  g_resident_inline = st.resident_inline;
+  g_resident_vram = st.resident_vram;
+  g_bad = st.resident_bad_slots;
+  g_scrubs = st.resident_scrubs;
+  g_launches = st.resident_launches;
+  g_servers = st.resident_servers;
+}
+
+// One thread of poison_mt / cycles_mt: `calls` one-group calls of 10 x 1200 B on a context of its
+// own, every row checked against the XOR; pause_every > 0: a 2-ms pause after every that many
+// calls.  Returns false on any failure.
+bool call_thread(int t, int calls, int pause_every) {
   constexpr uint32_t K = 10, P = 1200;
   FECEncoderCtx* ctx = fec_encoder_new(0.10, 1024);
   if (!ctx) return false;
@@ -115,6 +139,7 @@ bool poison_thread(int t, int calls) {
       for (uint32_t i = 0; i < P; ++i) want[i] ^= slab[j * P + i];
     const int rc = fec_encode_batch(ctx, slab, offsets, 1, P, rep);
     if (rc != 0 || std::memcmp(rep, want.data(), P) != 0) ok = false;
+    if (pause_every > 0 && (c + 1) % pause_every == 0) std::this_thread::sleep_for(std::chrono::milliseconds(2));
   }
   return ok;  // the context and buffers stay alive (a Go process exiting)
 }
@@ -158,19 +183,19 @@ int main(int argc, char** argv) {
   if (tear || epoch) setenv("QUICFEC_RESIDENT_TEST_TEAR", "1", 1);
   if (epoch) setenv("QUICFEC_RESIDENT_TEST_EPOCH", "2", 1);
   if (g_mode == "epoch_hostring") setenv("QUICFEC_RESIDENT_VRAM", "0", 1);
-  if (g_mode == "poison_mt") {
-    setenv("QUICFEC_RESIDENT_TEST_FAIL_AT", "600", 1);
-    constexpr int kThreads = 8;
+  if (g_mode == "poison_mt" || g_mode == "cycles_mt") {
+    const bool cycles = g_mode == "cycles_mt";
+    if (cycles) setenv("QUICFEC_RESIDENT_IDLE_US", "300", 1);
+    else setenv("QUICFEC_RESIDENT_TEST_FAIL_AT", "600", 1);
+    const int threads = cycles ? 4 : 8;
     std::vector<std::thread> th;
-    std::vector<char> ok(kThreads, 0);
-    for (int t = 0; t < kThreads; ++t) th.emplace_back([t, calls, &ok] { ok[t] = poison_thread(t, calls / kThreads) ? 1 : 0; });
+    std::vector<char> ok(threads, 0);
+    for (int t = 0; t < threads; ++t)
+      th.emplace_back([t, calls, threads, cycles, &ok] { ok[t] = call_thread(t, calls / threads, cycles ? 8 : 0) ? 1 : 0; });
     for (auto& x : th) x.join();
-    for (int t = 0; t < kThreads; ++t) g_ok = g_ok && ok[t] != 0;
-    g_calls = calls / kThreads * kThreads;
-    FECCoalesceStats st{};
-    fec_coalesce_stats(&st, 0);
-    g_resident_calls = st.resident_calls;
-    g_resident_vram = st.resident_vram;
+    for (int t = 0; t < threads; ++t) g_ok = g_ok && ok[t] != 0;
+    g_calls = calls / threads * threads;
+    take_stats();
     std::atexit(mark_exit);
     return 0;
   }
@@ -236,13 +261,7 @@ int main(int argc, char** argv) {
     if (rc != 0 || std::memcmp(repair, want.data(), size_t(G) * P) != 0) g_ok = false;
     ++g_calls;
   }
-  FECCoalesceStats st{};
-  fec_coalesce_stats(&st, 0);
-  g_resident_calls = st.resident_calls;
-  g_resident_inline = st.resident_inline;
-  g_resident_vram = st.resident_vram;
-  g_bad = st.resident_bad_slots;
-  g_scrubs = st.resident_scrubs;
+  take_stats();
   std::atexit(mark_exit);  // registered after the library's shutdown_all: runs before it
   return 0;               // encoders, slabs and repair buffers stay alive (a Go process exiting)
 }

@@ -368,13 +368,17 @@ lib.fec_encoder_free(ctx)
     assert first_us < 5000, f"first legacy call took {first_us:.0f} us"
 
 
-def _exit_path_run(mode, calls=300):
+def _exit_path_run(mode, calls=300, servers=None):
     import json
+    import os
     import subprocess
     from pathlib import Path
     exe = Path(__file__).resolve().parents[1] / "quic-test_amd" / "lib" / "exit_path_test"
     assert exe.exists(), "build() makes quic-test_amd/lib/exit_path_test (csrc Makefile target tests)"
-    out = subprocess.run([str(exe), mode, str(calls)], capture_output=True, text=True, timeout=90)
+    env = dict(os.environ)
+    if servers is not None:
+        env["QUICFEC_RESIDENT_SERVERS"] = str(servers)
+    out = subprocess.run([str(exe), mode, str(calls)], capture_output=True, text=True, timeout=90, env=env)
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert out.returncode == 0 and lines, (out.returncode, out.stdout, out.stderr)
     return json.loads(lines[-1])
@@ -482,3 +486,47 @@ def test_poisoned_resident_fails_no_in_flight_call():
     assert rec["repairs_ok"] is True and rec["calls"] == 2_400, rec
     assert rec["calls_after_exit"] == 0, rec["names"]
     assert 600 <= rec["resident_calls"] < 2_400, rec
+
+
+def test_resident_relaunch_cycles_under_concurrent_calls():
+    """4 threads with a context each make one-group calls in bursts of 8 with 2-ms pauses, the
+    idle bound at 300 us: resident instances leave and are relaunched many times while other
+    threads' calls are in flight, and every row equals the CPU XOR."""
+    rec = _exit_path_run("cycles_mt", calls=2_000)
+    if "skip" in rec:
+        pytest.skip(rec["skip"])
+    assert rec["repairs_ok"] is True and rec["calls"] == 2_000, rec
+    assert rec["calls_after_exit"] == 0, rec["names"]
+    assert rec["resident_calls"] == 2_000 and rec["resident_launches"] > 5, rec
+
+
+# (mode, calls) of the runs above, repeated with several serving workgroups per resident instance
+_SERVER_MODES = [("resident", 300), ("mixed", 360), ("mixed_hostring", 360), ("tear", 300), ("epoch", 6 * 1024),
+                 ("poison_mt", 2_400), ("cycles_mt", 2_000)]
+
+
+@pytest.mark.parametrize("servers", [2, 4])
+@pytest.mark.parametrize("mode,calls", _SERVER_MODES, ids=[m for m, _ in _SERVER_MODES])
+def test_resident_serving_classes(mode, calls, servers):
+    """QUICFEC_RESIDENT_SERVERS: the resident instance is `servers` workgroups, workgroup c
+    serving the seqs of class c (seq % servers == c) with its own poll, run, done words and
+    progress mark (fec_kernels.hip legacy_server).  Every ring-protocol run above -- mixed shapes on
+    both ring kinds, torn chunks and late address words, epoch scrubs, poisoning under 8 threads,
+    relaunch cycles under 4 -- gives every row equal to the CPU XOR with several classes, and the
+    exit stays HIP-free."""
+    rec = _exit_path_run(mode, calls=calls, servers=servers)
+    if "skip" in rec:
+        pytest.skip(rec["skip"])
+    assert rec["repairs_ok"] is True and rec["calls"] == calls, rec
+    assert rec["calls_after_exit"] == 0, rec["names"]
+    assert rec["resident_servers"] == servers, rec
+    if mode == "poison_mt":
+        assert 600 <= rec["resident_calls"] < calls, rec
+    elif mode in ("tear", "epoch") and rec["resident_vram"]:
+        assert rec["resident_calls"] == calls and rec["bad_slots"] > 0, rec
+        if mode == "epoch":
+            assert rec["scrubs"] >= 2 * 1024, rec
+    elif mode == "cycles_mt":
+        assert rec["resident_calls"] == calls and rec["resident_launches"] > 5, rec
+    else:
+        assert rec["resident_calls"] > 0, rec
