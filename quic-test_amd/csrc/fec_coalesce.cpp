@@ -31,13 +31,15 @@
 // Resident server (the default for the Go wrapper's calls: page-locked slab, 1..8 groups, P >=
 // 16).  A launch per batch costs the leader ~6-9 us of HIP API time and ~12 us until it sees
 // the completion (profiles/r03_legacy_v3_tuning.jsonl), so batching alone only matches the
-// per-context path.  Instead one workgroup stays resident on each device and serves a ring of
+// per-context path.  Instead workgroups stay resident on each device and serve a ring of
 // submission slots in page-locked coherent host memory (fec_kernels.hpp ServerSlot,
 // legacy_server): a caller takes a sequence number, writes its packets' device addresses and
 // its repair rows' address into slot seq % kServerSlots, every word tagged with the slot's lap,
 // and polls the slot's done word; the workgroup takes every complete slot in order each time it
 // polls (one PCIe round trip reads the next 64 slots' headers and first groups), so concurrent
-// callers share one pass without any host-side batch.
+// callers share one pass without any host-side batch.  An instance is 8 workgroups
+// (QUICFEC_RESIDENT_SERVERS), workgroup c serving the seqs with seq % 8 == c: eight
+// independent poll -> serve -> done cycles.
 // VRAM ring (large-BAR devices, the default where setup_vram succeeds; QUICFEC_RESIDENT_VRAM=0
 // keeps the page-locked ring): the slots live in uncached device memory the host writes
 // through the BAR, and a call of <= 4 groups with P % 4 == 0 and P <= 1536 -- the Go wrapper's
@@ -522,10 +524,13 @@ class Resident {
     // no word of a slot that was never written carries a tag (tags are 1 .. epoch; alloc_coherent zeroed it)
     std::memset(r->ring.host, 0, sizeof(ServerSlot) * kServerSlots);
     if (env_long("QUICFEC_RESIDENT_VRAM", 1) != 0) r->setup_vram();
-    // Serving classes (fec_kernels.hpp kServerMaxClasses): QUICFEC_RESIDENT_SERVERS workgroups, a
-    // power of two up to 8 (rounded down); more than one share a few words of uncached device
-    // memory, and without them the instance is one workgroup.
-    const long want = std::min<long>(kServerMaxClasses, std::max(1L, env_long("QUICFEC_RESIDENT_SERVERS", 1)));
+    // Serving classes (fec_kernels.hpp kServerMaxClasses): QUICFEC_RESIDENT_SERVERS workgroups
+    // (default 8), a power of two up to 8 (rounded down); more than one share a few words of
+    // uncached device memory, and without them the instance is one workgroup.  Same box,
+    // alternating (profiles/r05{q,s}/ab_servers.jsonl): 16 streams 0.69-0.74 M groups/s with one
+    // class, 1.15-1.16 M with 8; 64 streams 0.26-0.29 vs 0.39-0.42 M; one stream 7.9-8.1 vs
+    // 8.5-8.7 us a call (a workgroup's poll takes 1.5-1.7 us instead of 1.3 while others poll).
+    const long want = std::min<long>(kServerMaxClasses, std::max(1L, env_long("QUICFEC_RESIDENT_SERVERS", 8)));
     while (r->classes * 2 <= static_cast<uint32_t>(want)) r->classes *= 2;
     if (r->classes > 1) {
       void* c = nullptr;
@@ -538,7 +543,6 @@ class Resident {
       }
       r->coord = static_cast<ServerCoord*>(c);
     }
-    r->poll_slots = static_cast<uint32_t>(std::min<long>(kServerPoll, std::max(1L, env_long("QUICFEC_RESIDENT_POLL", kServerPoll))));
     r->collected.reset(new std::atomic<uint64_t>[kServerSlots]);
     for (uint32_t i = 0; i < kServerSlots; ++i) r->collected[i].store(0, std::memory_order_relaxed);
     return r.release();
@@ -793,7 +797,6 @@ class Resident {
   uint64_t fail_at = ~0ull;                   // QUICFEC_RESIDENT_TEST_FAIL_AT
   uint32_t epoch = kServerEpoch;              // QUICFEC_RESIDENT_TEST_EPOCH
   uint32_t classes = 1;                       // QUICFEC_RESIDENT_SERVERS
-  uint32_t poll_slots = kServerPoll;          // QUICFEC_RESIDENT_POLL
   ServerCoord* coord = nullptr;               // device memory shared by the classes' workgroups
   std::atomic<bool> outs_ready{false};
   // The slots as the host writes them and as the device reads them: the page-locked ring, or
@@ -963,7 +966,7 @@ class Resident {
     // every class resumes from its own progress mark (ServerControl::progress, read by the instance)
     BindDevice bd(device);
     const hipError_t e = bd.ok ? launch_legacy_server(ring_d, vinl, reinterpret_cast<uint64_t*>(done.dev),
-                                                      reinterpret_cast<ServerControl*>(ctl.dev), coord, classes, poll_slots, g,
+                                                      reinterpret_cast<ServerControl*>(ctl.dev), coord, classes, g,
                                                       idle_ticks, life_ticks,
                                                       stamps.host ? reinterpret_cast<uint64_t*>(stamps.dev) : nullptr,
                                                       epoch, stream)

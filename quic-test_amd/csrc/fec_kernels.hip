@@ -1823,7 +1823,8 @@ __global__ __launch_bounds__(256) void copy_words(const uint4* __restrict__ src,
   if (t < n16) dst[t] = src[t];
 }
 
-// Resident legacy encoder (fec_kernels.hpp ServerSlot): one workgroup of 16 waves.  One poll
+// Resident legacy encoder (fec_kernels.hpp ServerSlot): workgroups of 16 waves, one per serving
+// class (below).  One poll
 // is one round trip over PCIe: 128 lanes read the first two 64-B lines of each of the next 16
 // slots (the header words and the first group's 10 packet addresses, 16 B a lane: 32 line reads
 // in all -- reading every word of 64 slots separately took 5 us a poll, 2x a round trip); a
@@ -1907,7 +1908,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
                                                                 uint64_t* __restrict__ done,
                                                                 ServerControl* __restrict__ ctl,
                                                                 ServerCoord* __restrict__ coord, uint32_t classes,
-                                                                uint32_t poll_slots, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+                                                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
                                                                 uint64_t* __restrict__ stamps, uint32_t epoch) {
   __shared__ uint64_t s_next;
   __shared__ uint32_t s_n, s_exit, s_stop, s_ack, s_told;
@@ -1916,6 +1917,8 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
   __shared__ uint32_t s_P[kServerPoll], s_cpp[kServerPoll], s_inl[kServerPoll], s_bad[kServerPoll];
   __shared__ uint64_t s_head[kServerPoll][kServerHeadWords];  // out, shape, addr[0..13] (tagged)
   const uint32_t K = classes, cls = blockIdx.x;
+  // the shared words are read by every 8th poll (an instance leaves within 8 polls of the word)
+  constexpr uint32_t kCoordEvery = 7u;
   if (cls != 0) stamps = nullptr;  // class 0's stamps only
   // VRAM ring: every poll also reads the first 16 KB of the next slot's inline data area, one
   // 16-B chunk a thread, in flight with the header loads -- an inline slot found complete at
@@ -1933,6 +1936,8 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
     const uint64_t p = *reinterpret_cast<const volatile uint64_t*>(&ctl->progress[cls]);
     s_next = p + (cls + K - static_cast<uint32_t>(p % K)) % K;
     t0 = t_last = static_cast<uint64_t>(wall_clock64());
+    s_told = 0;
+    for (uint32_t c = 0; c < kServerMaxClasses; ++c) s_idle[c] = 0;
     n_bad = *reinterpret_cast<const volatile uint64_t*>(&ctl->bad_slots[cls]);
     n_scrub = *reinterpret_cast<const volatile uint64_t*>(&ctl->scrubs[cls]);
   }
@@ -1953,7 +1958,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
     constexpr uint32_t kPollLanes = kServerPoll * kServerHeadWords / 2;
     if (tid < kPollLanes) {
       const uint32_t i = tid / (kServerHeadWords / 2), piece = tid % (kServerHeadWords / 2);
-      const u64x2 v = i >= poll_slots ? u64x2{0, 0} : sys_load_16(reinterpret_cast<const uint64_t*>(ring + (next + uint64_t(i) * K) % kServerSlots) + 2 * piece);
+      const u64x2 v = sys_load_16(reinterpret_cast<const uint64_t*>(ring + (next + uint64_t(i) * K) % kServerSlots) + 2 * piece);
       s_head[i][2 * piece] = v.x;
       s_head[i][2 * piece + 1] = v.y;
     } else if (tid == kPollLanes) {
@@ -1961,9 +1966,10 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
       // trip again: every 16th poll reads it (the idle and life bounds hold regardless)
       s_stop = (inl == nullptr || (it & 15u) == 0) ? (*reinterpret_cast<const volatile uint64_t*>(&ctl->stop) != 0 ? 1u : 0u)
                                                    : 0u;
-    } else if (coord != nullptr && tid == kPollLanes + 1) {
+    } else if (coord != nullptr && (it & kCoordEvery) == 0 && tid == kPollLanes + 1) {
       s_told = sys_load_16(&coord->leave).x == gen ? 1u : 0u;
-    } else if (coord != nullptr && tid >= kPollLanes + 2 && tid < kPollLanes + 2 + kServerMaxClasses / 2) {
+    } else if (coord != nullptr && (it & kCoordEvery) == 0 && tid >= kPollLanes + 2 &&
+               tid < kPollLanes + 2 + kServerMaxClasses / 2) {
       const uint32_t q = tid - (kPollLanes + 2);
       const u64x2 v = sys_load_16(&coord->idle[2 * q]);
       s_idle[2 * q] = v.x;
@@ -1974,7 +1980,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
     if (tid < 64) {
       const uint64_t seq = next + uint64_t(lane) * K;
       const uint64_t tag = server_tag(seq, epoch);
-      bool ok = lane < poll_slots;
+      bool ok = lane < kServerPoll;
       bool inline_slot = false;
       if (ok) {
         // out, shape and (unless the packets are inline) the first group's 10 addresses (words 0 .. 11)
@@ -2968,17 +2974,16 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
 }
 
 hipError_t launch_legacy_server(ServerSlot* ring, uint8_t* inl, uint64_t* done, ServerControl* ctl,
-                                ServerCoord* coord, uint32_t classes, uint32_t poll_slots, uint64_t gen,
-                                uint64_t idle_ticks, uint64_t life_ticks, uint64_t* stamps, uint32_t epoch,
-                                hipStream_t s) {
+                                ServerCoord* coord, uint32_t classes, uint64_t gen, uint64_t idle_ticks,
+                                uint64_t life_ticks, uint64_t* stamps, uint32_t epoch, hipStream_t s) {
   if (epoch < 1u || epoch > kServerEpoch || (epoch & (epoch - 1u)) != 0) return hipErrorInvalidValue;
   // classes: a power of two (it divides kServerSlots), with the shared words when more than one;
   // gen fits the exit count's 56 bits
   if (classes < 1u || classes > kServerMaxClasses || (classes & (classes - 1u)) != 0 || (classes > 1u && !coord) ||
-      gen == 0 || gen >= (1ull << 56) || poll_slots < 1u || poll_slots > kServerPoll)
+      gen == 0 || gen >= (1ull << 56))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(legacy_server, dim3(classes), dim3(kServerThreads), 0, s, ring, inl, done, ctl,
-                     classes > 1u ? coord : nullptr, classes, poll_slots, gen, idle_ticks, life_ticks, stamps, epoch);
+                     classes > 1u ? coord : nullptr, classes, gen, idle_ticks, life_ticks, stamps, epoch);
   return hipGetLastError();
 }
 

@@ -214,7 +214,7 @@ constexpr uint32_t kInlineSlotBytes = kInlineMaxGroups * kServerPackets * (kInli
 // so it divides kServerSlots): workgroup c serves the seqs with seq % classes == c, in order, so
 // concurrent callers are served by independent poll -> serve -> done cycles.
 constexpr uint32_t kServerMaxClasses = 8;
-constexpr uint32_t kServerPoll = 16;  // the most slots one poll reads (and one batch serves)
+constexpr uint32_t kServerPoll = 16;  // slots of its class a workgroup reads per poll (the longest run it serves)
 struct alignas(64) ServerControl {
   uint64_t stop;            // host -> device: leave at the next poll
   uint64_t pad0[7];
@@ -237,17 +237,15 @@ struct alignas(64) ServerCoord {
 // has found nothing to do for idle_ticks, or it lived life_ticks (wall-clock ticks,
 // hipDeviceAttributeWallClockRate), or the host sets ctl->stop; on leaving a workgroup stores its
 // class's progress, and the last one to leave stores exited = gen.
-// coord: nullptr when classes == 1.  poll_slots: slots of its class a workgroup reads per poll
-// (1 .. kServerPoll), the longest run one batch serves.
+// coord: nullptr when classes == 1.
 // stamps: nullptr, or 256 x 8 words of host memory for the diagnostic phase stamps of class 0
 // (QUICFEC_RESIDENT_STAMPS).
 // inl: the inline data areas (kInlineSlotBytes per slot) when the ring is in VRAM, else nullptr;
 // then the host's stop word (host memory) is read by every 16th poll only, not every poll.
 // epoch: laps per tag epoch (server_tag), a power of two, 1 .. kServerEpoch.
 hipError_t launch_legacy_server(ServerSlot* ring, uint8_t* inl, uint64_t* done, ServerControl* ctl,
-                                ServerCoord* coord, uint32_t classes, uint32_t poll_slots, uint64_t gen,
-                                uint64_t idle_ticks, uint64_t life_ticks, uint64_t* stamps, uint32_t epoch,
-                                hipStream_t s);
+                                ServerCoord* coord, uint32_t classes, uint64_t gen, uint64_t idle_ticks,
+                                uint64_t life_ticks, uint64_t* stamps, uint32_t epoch, hipStream_t s);
 
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);

@@ -491,10 +491,12 @@ def test_poisoned_resident_fails_no_in_flight_call():
 def test_resident_relaunch_cycles_under_concurrent_calls():
     """4 threads with a context each make one-group calls in bursts of 8 with 2-ms pauses, the
     idle bound at 300 us: resident instances leave and are relaunched many times while other
-    threads' calls are in flight, and every row equals the CPU XOR."""
+    threads' calls are in flight (each of the 8 serving classes resumes from its own progress
+    mark), and every row equals the CPU XOR."""
     rec = _exit_path_run("cycles_mt", calls=2_000)
     if "skip" in rec:
         pytest.skip(rec["skip"])
+    assert rec["resident_servers"] == 8, rec
     assert rec["repairs_ok"] is True and rec["calls"] == 2_000, rec
     assert rec["calls_after_exit"] == 0, rec["names"]
     assert rec["resident_calls"] == 2_000 and rec["resident_launches"] > 5, rec
@@ -505,15 +507,15 @@ _SERVER_MODES = [("resident", 300), ("mixed", 360), ("mixed_hostring", 360), ("t
                  ("poison_mt", 2_400), ("cycles_mt", 2_000)]
 
 
-@pytest.mark.parametrize("servers", [2, 4])
+@pytest.mark.parametrize("servers", [1, 2, 4])
 @pytest.mark.parametrize("mode,calls", _SERVER_MODES, ids=[m for m, _ in _SERVER_MODES])
 def test_resident_serving_classes(mode, calls, servers):
-    """QUICFEC_RESIDENT_SERVERS: the resident instance is `servers` workgroups, workgroup c
-    serving the seqs of class c (seq % servers == c) with its own poll, run, done words and
-    progress mark (fec_kernels.hip legacy_server).  Every ring-protocol run above -- mixed shapes on
-    both ring kinds, torn chunks and late address words, epoch scrubs, poisoning under 8 threads,
-    relaunch cycles under 4 -- gives every row equal to the CPU XOR with several classes, and the
-    exit stays HIP-free."""
+    """QUICFEC_RESIDENT_SERVERS: the resident instance is `servers` workgroups (default 8, which
+    the runs above use), workgroup c serving the seqs of class c (seq % servers == c) with its own
+    poll, run, done words and progress mark (fec_kernels.hip legacy_server).  Every ring-protocol
+    run above -- mixed shapes on both ring kinds, torn chunks and late address words, epoch scrubs,
+    poisoning under 8 threads, relaunch cycles under 4 -- gives every row equal to the CPU XOR
+    with one, two and four classes too, and the exit stays HIP-free."""
     rec = _exit_path_run(mode, calls=calls, servers=servers)
     if "skip" in rec:
         pytest.skip(rec["skip"])
