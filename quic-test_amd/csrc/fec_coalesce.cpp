@@ -497,6 +497,7 @@ class Resident {
     }
     const uint64_t per_us = static_cast<uint64_t>(khz) / 1000u;
     r->idle_ticks = per_us * static_cast<uint64_t>(std::max(10L, env_long("QUICFEC_RESIDENT_IDLE_US", 2000)));
+    r->slow_ticks = per_us * static_cast<uint64_t>(std::max(1L, env_long("QUICFEC_RESIDENT_SLOW_US", 50)));
     r->life_ticks = per_us * static_cast<uint64_t>(std::max(100L, env_long("QUICFEC_RESIDENT_LIFE_US", 50000)));
     // The per-slot staging of pageable repair buffers (16 MB) comes with the first call that
     // needs it (ensure_outs): the first context of every process sets a Resident up
@@ -517,8 +518,12 @@ class Resident {
     // tests: every inline call lands one chunk in two 8-B pieces, the half with the tag first and
     // the other ~100 us after the slot's header (a write-combined store evicted in pieces)
     r->tear = env_long("QUICFEC_RESIDENT_TEST_TEAR", 0) != 0;
-    // tests: the call of this seq fails as if its deadline had passed (poisoning under load)
+    // tests: the call of this number (0 = the Resident's first) fails as if its deadline had
+    // passed (poisoning under load)
     r->fail_at = static_cast<uint64_t>(env_long("QUICFEC_RESIDENT_TEST_FAIL_AT", -1));
+    // every call to the next class round robin, however few are in flight (tests: one thread's
+    // n-th call then takes seq n)
+    r->spread = env_long("QUICFEC_RESIDENT_SPREAD", 0) != 0;
     if (env_long("QUICFEC_RESIDENT_STAMPS", 0) != 0 && !alloc_coherent(r->stamps, 256 * 8 * sizeof(uint64_t))) return nullptr;
     r->tick_khz = static_cast<uint64_t>(khz);
     // no word of a slot that was never written carries a tag (tags are 1 .. epoch; alloc_coherent zeroed it)
@@ -543,6 +548,7 @@ class Resident {
       }
       r->coord = static_cast<ServerCoord*>(c);
     }
+    for (uint32_t c = 0; c < kServerMaxClasses; ++c) r->class_next[c].store(c, std::memory_order_relaxed);
     r->collected.reset(new std::atomic<uint64_t>[kServerSlots]);
     for (uint32_t i = 0; i < kServerSlots; ++i) r->collected[i].store(0, std::memory_order_relaxed);
     return r.release();
@@ -583,7 +589,20 @@ class Resident {
     if (!inline_pk && slab_dev == nullptr) return kNotTaken;
     if (!inline_pk && !repair_dev && !ensure_outs()) return kNotTaken;
     const uint64_t base = reinterpret_cast<uint64_t>(slab_dev);
-    const uint64_t seq = next_seq.fetch_add(1, std::memory_order_relaxed);
+    // The call's serving class: while few calls are in flight only the lowest classes take them
+    // (a lone caller's calls all go to class 0, whose workgroup stays busy, while the others poll
+    // slowly: a poll is slower while other workgroups poll fast), under load all of
+    // them, round robin.  Each class's seqs are c, c + classes, c + 2 * classes, ... in the order
+    // taken, which is the order its workgroup serves them.
+    struct InFlight {
+      std::atomic<uint32_t>& n;
+      uint32_t now;
+      explicit InFlight(std::atomic<uint32_t>& c) : n(c), now(c.fetch_add(1, std::memory_order_relaxed) + 1) {}
+      ~InFlight() { n.fetch_sub(1, std::memory_order_relaxed); }
+    } inflight(in_flight);
+    const uint32_t span = spread ? classes : std::min(classes, inflight.now);
+    const uint32_t cls = span > 1 ? rr.fetch_add(1, std::memory_order_relaxed) % span : 0u;
+    const uint64_t seq = class_next[cls].fetch_add(classes, std::memory_order_relaxed);
     const uint32_t si = static_cast<uint32_t>(seq % kServerSlots);
     const uint32_t tag16 = server_tag(seq, epoch);
     const uint64_t tag = uint64_t(tag16) << kServerTagShift;
@@ -672,7 +691,7 @@ class Resident {
       while (landed < 2 * G * nch && half_ok(landed)) ++landed;
       return landed == 2 * G * nch;
     };
-    if (seq == fail_at) {  // tests: this call's deadline passes at once
+    if (call_no.fetch_add(1, std::memory_order_relaxed) == fail_at) {  // tests: this call's deadline passes at once
       set_last_error("fec_encode_batch: QUICFEC_RESIDENT_TEST_FAIL_AT");
       rc = FEC_ERR_HIP;
     }
@@ -783,11 +802,14 @@ class Resident {
  private:
   int device = 0;
   hipStream_t stream = nullptr;
-  uint64_t idle_ticks = 0, life_ticks = 0;
+  uint64_t idle_ticks = 0, slow_ticks = 0, life_ticks = 0;
   Pinned ring, done, ctl, outs, stamps;
   uint64_t tick_khz = 100000;
   std::unique_ptr<std::atomic<uint64_t>[]> collected;  // per slot: seq + 1 of its last collected call
-  std::atomic<uint64_t> next_seq{0};
+  std::atomic<uint64_t> class_next[kServerMaxClasses];  // the next seq of each class (c, then + classes)
+  std::atomic<uint32_t> in_flight{0};                   // calls inside encode()
+  std::atomic<uint32_t> rr{0};                          // round robin over the classes in use
+  std::atomic<uint64_t> call_no{0};                     // calls so far (QUICFEC_RESIDENT_TEST_FAIL_AT)
   std::mutex mu;
   std::atomic<uint64_t> gen{0};  // generation of the last launched instance (0 = none yet)
   std::atomic<bool> broken{false};
@@ -795,6 +817,7 @@ class Resident {
   bool no_launch = false;                     // QUICFEC_RESIDENT_TEST_NOLAUNCH
   bool tear = false;                          // QUICFEC_RESIDENT_TEST_TEAR
   uint64_t fail_at = ~0ull;                   // QUICFEC_RESIDENT_TEST_FAIL_AT
+  bool spread = false;                        // QUICFEC_RESIDENT_SPREAD
   uint32_t epoch = kServerEpoch;              // QUICFEC_RESIDENT_TEST_EPOCH
   uint32_t classes = 1;                       // QUICFEC_RESIDENT_SERVERS
   ServerCoord* coord = nullptr;               // device memory shared by the classes' workgroups
@@ -967,7 +990,7 @@ class Resident {
     BindDevice bd(device);
     const hipError_t e = bd.ok ? launch_legacy_server(ring_d, vinl, reinterpret_cast<uint64_t*>(done.dev),
                                                       reinterpret_cast<ServerControl*>(ctl.dev), coord, classes, g,
-                                                      idle_ticks, life_ticks,
+                                                      idle_ticks, slow_ticks, life_ticks,
                                                       stamps.host ? reinterpret_cast<uint64_t*>(stamps.dev) : nullptr,
                                                       epoch, stream)
                                : hipErrorInvalidDevice;

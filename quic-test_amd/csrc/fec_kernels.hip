@@ -1908,10 +1908,11 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
                                                                 uint64_t* __restrict__ done,
                                                                 ServerControl* __restrict__ ctl,
                                                                 ServerCoord* __restrict__ coord, uint32_t classes,
-                                                                uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks,
-                                                                uint64_t* __restrict__ stamps, uint32_t epoch) {
+                                                                uint64_t gen, uint64_t idle_ticks, uint64_t slow_ticks,
+                                                                uint64_t life_ticks, uint64_t* __restrict__ stamps,
+                                                                uint32_t epoch) {
   __shared__ uint64_t s_next;
-  __shared__ uint32_t s_n, s_exit, s_stop, s_ack, s_told;
+  __shared__ uint32_t s_n, s_exit, s_stop, s_ack, s_told, s_slow;
   __shared__ uint64_t s_idle[kServerMaxClasses];
   __shared__ uint32_t s_first[kServerPoll + 1];  // work items before slot i of the run
   __shared__ uint32_t s_P[kServerPoll], s_cpp[kServerPoll], s_inl[kServerPoll], s_bad[kServerPoll];
@@ -2019,6 +2020,8 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
         s_n = n;
         s_ack = addressed != 0 ? 1u : 0u;
         const bool idle = n == 0 && now - t_last > idle_ticks;
+        // (class 0, where the host puts a lone caller's calls, never polls slowly)
+        s_slow = cls != 0 && n == 0 && now - t_last > slow_ticks ? 1u : 0u;
         bool leave = stop || now - t0 > life_ticks || it + 1 == kServerMaxPolls;
         if (coord == nullptr) {
           leave = leave || idle;
@@ -2207,7 +2210,12 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
         st_polls = 0;
       }
     } else if (!leave) {
-      __builtin_amdgcn_s_sleep(8);
+      // a class other than 0 without work for slow_ticks polls every ~5 us instead of every ~1.5
+      // (the host gives a lone caller's calls to class 0, whose polls other classes' polls slow down)
+      if (s_slow != 0)
+        __builtin_amdgcn_s_sleep(127);
+      else
+        __builtin_amdgcn_s_sleep(8);
     }
     lds_barrier();
     if (leave) break;
@@ -2975,7 +2983,8 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, ui
 
 hipError_t launch_legacy_server(ServerSlot* ring, uint8_t* inl, uint64_t* done, ServerControl* ctl,
                                 ServerCoord* coord, uint32_t classes, uint64_t gen, uint64_t idle_ticks,
-                                uint64_t life_ticks, uint64_t* stamps, uint32_t epoch, hipStream_t s) {
+                                uint64_t slow_ticks, uint64_t life_ticks, uint64_t* stamps, uint32_t epoch,
+                                hipStream_t s) {
   if (epoch < 1u || epoch > kServerEpoch || (epoch & (epoch - 1u)) != 0) return hipErrorInvalidValue;
   // classes: a power of two (it divides kServerSlots), with the shared words when more than one;
   // gen fits the exit count's 56 bits
@@ -2983,7 +2992,7 @@ hipError_t launch_legacy_server(ServerSlot* ring, uint8_t* inl, uint64_t* done, 
       gen == 0 || gen >= (1ull << 56))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(legacy_server, dim3(classes), dim3(kServerThreads), 0, s, ring, inl, done, ctl,
-                     classes > 1u ? coord : nullptr, classes, gen, idle_ticks, life_ticks, stamps, epoch);
+                     classes > 1u ? coord : nullptr, classes, gen, idle_ticks, slow_ticks, life_ticks, stamps, epoch);
   return hipGetLastError();
 }
 

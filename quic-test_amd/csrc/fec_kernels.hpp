@@ -237,7 +237,8 @@ struct alignas(64) ServerCoord {
 // has found nothing to do for idle_ticks, or it lived life_ticks (wall-clock ticks,
 // hipDeviceAttributeWallClockRate), or the host sets ctl->stop; on leaving a workgroup stores its
 // class's progress, and the last one to leave stores exited = gen.
-// coord: nullptr when classes == 1.
+// coord: nullptr when classes == 1.  slow_ticks: a workgroup other than class 0's without work
+// for that long polls slowly (~5 us apart instead of ~1.5) until it finds some.
 // stamps: nullptr, or 256 x 8 words of host memory for the diagnostic phase stamps of class 0
 // (QUICFEC_RESIDENT_STAMPS).
 // inl: the inline data areas (kInlineSlotBytes per slot) when the ring is in VRAM, else nullptr;
@@ -245,7 +246,8 @@ struct alignas(64) ServerCoord {
 // epoch: laps per tag epoch (server_tag), a power of two, 1 .. kServerEpoch.
 hipError_t launch_legacy_server(ServerSlot* ring, uint8_t* inl, uint64_t* done, ServerControl* ctl,
                                 ServerCoord* coord, uint32_t classes, uint64_t gen, uint64_t idle_ticks,
-                                uint64_t life_ticks, uint64_t* stamps, uint32_t epoch, hipStream_t s);
+                                uint64_t slow_ticks, uint64_t life_ticks, uint64_t* stamps, uint32_t epoch,
+                                hipStream_t s);
 
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
                                 hipStream_t s);

@@ -55,5 +55,9 @@ case "${1:-run}" in
     timeout -k 10 120 $A/exit_path_test tear 300
     timeout -k 10 300 $A/exit_path_test epoch 6144
     timeout -k 10 300 $A/exit_path_test poison_mt 2400
+    # relaunch cycles under 4 threads (8 serving classes, the default), and the tag runs with one class
+    timeout -k 10 300 $A/exit_path_test cycles_mt 2000
+    QUICFEC_RESIDENT_SERVERS=1 timeout -k 10 120 $A/exit_path_test tear 300
+    QUICFEC_RESIDENT_SERVERS=1 timeout -k 10 300 $A/exit_path_test poison_mt 2400
     ;;
 esac

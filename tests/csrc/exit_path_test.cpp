@@ -27,8 +27,8 @@
 //    calls on odd laps, so an 8-group call's later address words from two laps back carry the
 //    current tag unless the epoch scrub zeroed them -- and the late stores make the server read
 //    those words before the new ones land.
-//  * poison_mt: 8 threads with a context each make one-group calls; the call of seq 600 fails as
-//    if its deadline had passed (QUICFEC_RESIDENT_TEST_FAIL_AT).  Every call of every thread --
+//  * poison_mt: 8 threads with a context each make one-group calls; the Resident's 601st call
+//    fails as if its deadline had passed (QUICFEC_RESIDENT_TEST_FAIL_AT).  Every call of every thread --
 //    that one and the ones in flight when the Resident went out of service included -- must
 //    return 0 with the right row (served, or run on the coalescer path).
 //
@@ -182,6 +182,8 @@ int main(int argc, char** argv) {
   const bool tear = g_mode == "tear", epoch = g_mode.rfind("epoch", 0) == 0;
   if (tear || epoch) setenv("QUICFEC_RESIDENT_TEST_TEAR", "1", 1);
   if (epoch) setenv("QUICFEC_RESIDENT_TEST_EPOCH", "2", 1);
+  // epoch: call c must take seq c (slot c % 1024, lap c / 1024) whatever the serving classes
+  if (epoch) setenv("QUICFEC_RESIDENT_SPREAD", "1", 1);
   if (g_mode == "epoch_hostring") setenv("QUICFEC_RESIDENT_VRAM", "0", 1);
   if (g_mode == "poison_mt" || g_mode == "cycles_mt") {
     const bool cycles = g_mode == "cycles_mt";

@@ -477,7 +477,7 @@ def test_resident_tag_epoch_scrub_under_mixed_calls(mode):
 def test_poisoned_resident_fails_no_in_flight_call():
     """when one call poisons the Resident (its deadline passed), the calls
     other threads have in flight must not fail with it.  8 threads with a context each make
-    one-group calls; seq 600 fails at once (QUICFEC_RESIDENT_TEST_FAIL_AT).  Its slot and every
+    one-group calls; the 601st fails at once (QUICFEC_RESIDENT_TEST_FAIL_AT).  Its slot and every
     other published slot are either served before the instance leaves or, once it has left
     without serving them, run on the coalescer path: all 2,400 calls return 0 with the right row."""
     rec = _exit_path_run("poison_mt", calls=2_400)
