@@ -35,11 +35,12 @@
 // submission slots in page-locked coherent host memory (fec_kernels.hpp ServerSlot,
 // legacy_server): a caller takes a sequence number, writes its packets' device addresses and
 // its repair rows' address into slot seq % kServerSlots, every word tagged with the slot's lap,
-// and polls the slot's done word; the workgroup takes every complete slot in order each time it
-// polls (one PCIe round trip reads the next 64 slots' headers and first groups), so concurrent
-// callers share one pass without any host-side batch.  An instance is 8 workgroups
+// and polls the slot's done word; a workgroup takes every complete slot of its class in order
+// each time it polls (one round trip reads the next 16 slots' headers and first groups), so
+// concurrent callers share one pass without any host-side batch.  An instance is 8 workgroups
 // (QUICFEC_RESIDENT_SERVERS), workgroup c serving the seqs with seq % 8 == c: eight
-// independent poll -> serve -> done cycles.
+// independent poll -> serve -> done cycles; the host gives a call the class by the calls in
+// flight (Resident::encode).
 // VRAM ring (large-BAR devices, the default where setup_vram succeeds; QUICFEC_RESIDENT_VRAM=0
 // keeps the page-locked ring): the slots live in uncached device memory the host writes
 // through the BAR, and a call of <= 4 groups with P % 4 == 0 and P <= 1536 -- the Go wrapper's
@@ -530,12 +531,13 @@ class Resident {
     std::memset(r->ring.host, 0, sizeof(ServerSlot) * kServerSlots);
     if (env_long("QUICFEC_RESIDENT_VRAM", 1) != 0) r->setup_vram();
     // Serving classes (fec_kernels.hpp kServerMaxClasses): QUICFEC_RESIDENT_SERVERS workgroups
-    // (default 8), a power of two up to 8 (rounded down); more than one share a few words of
-    // uncached device memory, and without them the instance is one workgroup.  Same box,
+    // (default 8 with the VRAM ring; 1 with the page-locked ring, whose every poll is a PCIe round
+    // trip), a power of two up to 8 (rounded down); more than one share a few words of uncached
+    // device memory, and without them the instance is one workgroup.  Same box,
     // alternating (profiles/r05{q,s}/ab_servers.jsonl): 16 streams 0.69-0.74 M groups/s with one
     // class, 1.15-1.16 M with 8; 64 streams 0.26-0.29 vs 0.39-0.42 M; one stream 7.9-8.1 vs
     // 8.5-8.7 us a call (a workgroup's poll takes 1.5-1.7 us instead of 1.3 while others poll).
-    const long want = std::min<long>(kServerMaxClasses, std::max(1L, env_long("QUICFEC_RESIDENT_SERVERS", 8)));
+    const long want = std::min<long>(kServerMaxClasses, std::max(1L, env_long("QUICFEC_RESIDENT_SERVERS", r->vinl ? 8 : 1)));
     while (r->classes * 2 <= static_cast<uint32_t>(want)) r->classes *= 2;
     if (r->classes > 1) {
       void* c = nullptr;

@@ -496,7 +496,7 @@ def test_resident_relaunch_cycles_under_concurrent_calls():
     rec = _exit_path_run("cycles_mt", calls=2_000)
     if "skip" in rec:
         pytest.skip(rec["skip"])
-    assert rec["resident_servers"] == 8, rec
+    assert rec["resident_servers"] == (8 if rec["resident_vram"] else 1), rec  # the defaults per ring kind
     assert rec["repairs_ok"] is True and rec["calls"] == 2_000, rec
     assert rec["calls_after_exit"] == 0, rec["names"]
     assert rec["resident_calls"] == 2_000 and rec["resident_launches"] > 5, rec
@@ -510,8 +510,8 @@ _SERVER_MODES = [("resident", 300), ("mixed", 360), ("mixed_hostring", 360), ("t
 @pytest.mark.parametrize("servers", [1, 2, 4])
 @pytest.mark.parametrize("mode,calls", _SERVER_MODES, ids=[m for m, _ in _SERVER_MODES])
 def test_resident_serving_classes(mode, calls, servers):
-    """QUICFEC_RESIDENT_SERVERS: the resident instance is `servers` workgroups (default 8, which
-    the runs above use), workgroup c serving the seqs of class c (seq % servers == c) with its own
+    """QUICFEC_RESIDENT_SERVERS: the resident instance is `servers` workgroups (default 8 on the
+    VRAM ring, which the runs above use, 1 on the page-locked ring), workgroup c serving the seqs of class c (seq % servers == c) with its own
     poll, run, done words and progress mark (fec_kernels.hip legacy_server).  Every ring-protocol
     run above -- mixed shapes on both ring kinds, torn chunks and late address words, epoch scrubs,
     poisoning under 8 threads, relaunch cycles under 4 -- gives every row equal to the CPU XOR
