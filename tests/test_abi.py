@@ -156,6 +156,21 @@ def test_kernel_arithmetic_emulation(tmp_path, oracle_mod):
     assert out.returncode == 0 and out.stdout.startswith("OK"), out.stdout + out.stderr
 
 
+def test_resident_ring_protocol_model(tmp_path):
+    """The resident ring's acceptance rules checked on the CPU against the product's own
+    definitions (fec_kernels.hpp server_tag / server_scrub_after, the slot, control and
+    coordination layouts): tags unique within an epoch and never 0, no stale 8-B word accepted
+    over 40 epochs of torn, partly rewritten laps with the epoch scrub (and a stale acceptance
+    without it, the control), serving classes' seqs confined to their own slots with the
+    previous occupant seq - 1024 (tests/csrc/ring_protocol_test.cpp)."""
+    exe = tmp_path / "ring_protocol_test"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    "-I", str(REPO / "quic-test_amd" / "csrc"), str(REPO / "tests" / "csrc" / "ring_protocol_test.cpp"),
+                    "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.startswith("OK"), out.stdout + out.stderr
+
+
 def test_ctx_last_error_null_context(quicfec_mod):
     lib = quicfec_mod.load_library()
     import ctypes
