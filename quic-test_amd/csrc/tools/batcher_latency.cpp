@@ -502,7 +502,8 @@ int legacy(int S, double rate, double seconds) {
                 "\"coalesced_calls\": %llu, \"launches\": %llu, \"mean_batch\": %.2f, \"max_batch\": %llu, "
                 "\"us_per_launch\": {\"close\": %.2f, \"launch\": %.2f, \"done\": %.2f}, \"resident\": %d, "
                 "\"resident_calls\": %llu, \"resident_launches\": %llu, \"resident_inline\": %llu, \"resident_vram\": %llu, "
-                "\"resident_servers\": %llu, \"resident_us_per_call\": {\"pre\": %.2f, \"wait\": %.2f, \"post\": %.2f}",
+                "\"resident_servers\": %llu, \"resident_bad_slots\": %llu, \"resident_scrubs\": %llu, "
+                "\"resident_us_per_call\": {\"pre\": %.2f, \"wait\": %.2f, \"post\": %.2f}",
                 S, rate, co && co[0] == '0' ? 0 : 1, errors.load(), fallback.load(), (unsigned long long)cs.calls,
                 (unsigned long long)cs.batches, cs.batches ? double(cs.groups) / cs.batches : 0.0,
                 (unsigned long long)cs.max_batch, cs.batches ? cs.close_ns / 1e3 / cs.batches : 0.0,
@@ -510,6 +511,7 @@ int legacy(int S, double rate, double seconds) {
                 res && res[0] == '0' ? 0 : 1, (unsigned long long)cs.resident_calls,
                 (unsigned long long)cs.resident_launches, (unsigned long long)cs.resident_inline,
                 (unsigned long long)cs.resident_vram, (unsigned long long)cs.resident_servers,
+                (unsigned long long)cs.resident_bad_slots, (unsigned long long)cs.resident_scrubs,
                 cs.resident_calls ? cs.resident_pre_ns / 1e3 / cs.resident_calls : 0.0,
                 cs.resident_calls ? cs.resident_wait_ns / 1e3 / cs.resident_calls : 0.0,
                 cs.resident_calls ? cs.resident_post_ns / 1e3 / cs.resident_calls : 0.0);
