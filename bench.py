@@ -493,20 +493,27 @@ def e2e_pinned(ctx, d_data, d_parity, d_masks, G: int, cfg: dict, reps: int = 3)
 CALL_SITE_TOOL = REPO / "quic-test_amd" / "lib" / "call_site"
 
 
-def call_site(seconds: float = 2.0) -> dict:
+def call_site(ref_1t_GiBps=None, seconds: float = 2.0) -> dict:
     """The reference's unchanged product call site next to the headline: every QUIC stream's own
     HybridFECEncoder making one fec_encode_batch call per group of 10 x 1200 B
     (encoder_hybrid.go:115 -> fec_cgo.go:138), through the C++ mirror, measured by
     quic-test_amd/lib/call_site (tools/call_site.cpp) in a process of its own, as a Go binary
-    would be: raw calls with FECEncoderCXX's buffers, then 1 and 16 streams back to back.  Every
-    repair is checked against the XOR inside the tool (no oracle).  Not the headline metric."""
+    would be: raw calls with FECEncoderCXX's buffers, then 1 and 16 streams back to back.  Then
+    the opt-in integration that changes the call site: 16 streams' BatchedFECEncoders
+    on one shared batcher, r = 1 (the reference's row) and r = 3.  Every repair row is checked
+    inside the tool (no oracle).  ref_1t_GiBps (cpu_baseline's ref_encode_batch_1t_GiBps, the
+    reference library on one core) is quoted beside them in groups/s.  Not the headline metric."""
     import subprocess
     if not CALL_SITE_TOOL.exists():
         return {"skipped": "quic-test_amd/lib/call_site not built (__graft_entry__.build())"}
     out = {"reference_call": "encoder_hybrid.go:115 -> fec_cgo.go:138 fec_encode_batch, 1 group of 10 x 1200 B per call",
            "tool": "quic-test_amd/lib/call_site"}
+    if ref_1t_GiBps:
+        out["ref_encode_batch_1t_groups_per_s"] = round(ref_1t_GiBps * 2**30 / (10 * 1200), 1)
     for name, argv in (("raw", ["raw", "20000"]), ("streams_1", ["streams", "1", str(seconds)]),
-                       ("streams_16", ["streams", "16", str(seconds)])):
+                       ("streams_16", ["streams", "16", str(seconds)]),
+                       ("batcher_16_r1", ["batcher", "16", str(seconds), "1"]),
+                       ("batcher_16_r3", ["batcher", "16", str(seconds), "3"])):
         try:
             p = subprocess.run([str(CALL_SITE_TOOL), *argv], capture_output=True, text=True, timeout=120)
         except subprocess.TimeoutExpired:
@@ -517,8 +524,10 @@ def call_site(seconds: float = 2.0) -> dict:
             out[name] = {"error": f"exit {p.returncode}: {p.stderr.strip()[-300:]}"}
             break
         rec = json.loads(lines[-1])
-        out[name] = {k: rec[k] for k in ("groups_per_s", "delay_us", "errors", "resident_inline", "resident_vram")
-                     if k in rec}
+        out[name] = {k: rec[k] for k in ("groups_per_s", "delay_us", "errors", "resident_inline", "resident_vram",
+                                         "batches", "max_batch") if k in rec}
+        if ref_1t_GiBps and "groups_per_s" in rec:
+            out[name]["vs_ref_1t"] = round(rec["groups_per_s"] / out["ref_encode_batch_1t_groups_per_s"], 3)
     return out
 
 
@@ -1012,7 +1021,7 @@ def main() -> int:
     site = None  # beside the headline like cpu_baseline, and skipped with it (profiled and A/B runs)
     t = time.monotonic()
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_call_site:
-        site = call_site()
+        site = call_site(cpu.get("ref_encode_batch_1t_GiBps") if cpu else None)
         wall["call_site"] = round(time.monotonic() - t, 2)
     wall["total"] = round(time.monotonic() - T_START, 2)
 

@@ -305,7 +305,13 @@ typedef struct {
                                   largest over devices; 0 before any resident encoder exists (not reset) */
 } FECCoalesceStats;
 
-/* Process-wide totals over every device and packet size; reset = 1 zeroes them after the read. */
+/* Process-wide totals over every device and packet size; reset = 1 zeroes them after the read.
+ * Writes min(out_bytes, sizeof(FECCoalesceStats)) bytes: pass sizeof(*out) of the struct the
+ * caller was built with, so fields a later library appends are never written past it.
+ * FEC_ERR_RANGE when out_bytes is below the first published layout (15 words). */
+int fec_coalesce_stats_sized(FECCoalesceStats* out, size_t out_bytes, int reset);
+
+/* The first published form: writes the first 15 fields only (calls .. resident_vram). */
 int fec_coalesce_stats(FECCoalesceStats* out, int reset);
 
 #ifdef __cplusplus

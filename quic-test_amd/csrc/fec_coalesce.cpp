@@ -72,6 +72,7 @@
 #include "fec_hip.h"
 #include "fec_internal.hpp"
 #include "fec_kernels.hpp"
+#include "fec_knobs.hpp"
 
 #define QFEC_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -83,6 +84,8 @@ constexpr uint32_t kMaxBatchGroups = 1024;
 constexpr uint64_t kStageBudget = 16ull << 20;  // page-locked staging bytes per batch
 constexpr size_t kMaxCoalescers = 16;           // (device, packet size) pairs
 constexpr uint32_t kCoalesceMaxP = 16u << 10;   // larger packets: no shared launches (staging bound)
+// FECCoalesceStats as published in round 4: calls .. resident_vram (15 words)
+constexpr size_t kCoalesceStatsV4Bytes = 15 * sizeof(uint64_t);
 
 long env_long(const char* name, long def) {
   const char* v = std::getenv(name);
@@ -165,11 +168,30 @@ bool alloc_batch(Batch& b, size_t groups, size_t out_bytes) {
   return true;
 }
 
+// The device's shared-launch stream, non-blocking: a batch holding other contexts' calls never
+// waits on legacy null-stream work or on a leader context's own queued work.  Made
+// with the first context too (a stream that needs a new hardware queue costs ~9 ms); nullptr
+// when that failed (the leader then launches on its caller's context stream).  Never destroyed.
+std::map<int, hipStream_t> g_launch_stream;
+
 void prepare_spare_batch(int device) {
   std::lock_guard<std::mutex> lk(g_spare_mu);
   if (g_spare.count(device)) return;
   auto b = std::make_unique<Batch>();
   g_spare.emplace(device, alloc_batch(*b, kMaxBatchGroups, kBatchOutMax) ? std::move(b) : nullptr);
+  hipStream_t s = nullptr;
+  BindDevice bd(device);
+  if (!bd.ok || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    s = nullptr;
+  }
+  g_launch_stream[device] = s;
+}
+
+hipStream_t launch_stream_for(int device) {
+  std::lock_guard<std::mutex> lk(g_spare_mu);
+  auto it = g_launch_stream.find(device);
+  return it == g_launch_stream.end() ? nullptr : it->second;
 }
 
 std::unique_ptr<Batch> take_spare_batch(int device) {
@@ -198,12 +220,13 @@ class Coalescer {
  public:
   // NULL when the device or page-locked memory cannot be set up (the call then runs alone).
   // Nothing but the first batch's page-locked buffers and event is made here: no context and no
-  // stream (the leader launches on its caller's context stream), further batches when concurrent
+  // stream (the leader launches on the device's shared-launch stream, made with the first context,
+  // launch_stream_for), further batches when concurrent
   // callers need them.  A context and a stream of its own each cost ~9 ms here (a stream that
   // needs a new hardware queue), and the first shared-launch call of a process paid both: 18-22 ms
-  // against a p99 of 21-35 us (QUICFEC_COALESCE_STAMPS, profiles/r05e/legacy_coalescer_*.err).
+  // against a p99 of 21-35 us (coalescer stamps, profiles/r05e/legacy_coalescer_*.err).
   static Coalescer* create(int device, uint32_t P) {
-    // QUICFEC_COALESCE_STAMPS: the creation's time to stderr (diagnostic)
+    // the test library's TestKnob::kCoalesceStamps: the creation's time to stderr (diagnostic)
     const uint64_t t0 = now_ns();
     std::unique_ptr<Coalescer> c(new Coalescer());
     c->device = device;
@@ -211,11 +234,12 @@ class Coalescer {
     const uint64_t fit = kStageBudget / (uint64_t(kPackets) * P);
     c->cap = static_cast<uint32_t>(std::max<uint64_t>(8, std::min<uint64_t>(kMaxBatchGroups, fit)));
     c->max_inflight = static_cast<int>(std::max(1L, std::min(8L, env_long("QUICFEC_COALESCE_INFLIGHT", 2))));
+    c->launch_stream = launch_stream_for(device);
     BindDevice bd(device);
     if (!bd.ok || !c->add_batch()) return nullptr;
     std::lock_guard<std::mutex> lk(c->mu);
     c->open_free();
-    if (env_long("QUICFEC_COALESCE_STAMPS", 0) != 0)
+    if (test_knob(TestKnob::kCoalesceStamps, 0) != 0)
       std::fprintf(stderr, "{\"coalescer_create_us\": %.1f}\n", (now_ns() - t0) / 1e3);
     return c.release();
   }
@@ -230,7 +254,8 @@ class Coalescer {
   }
 
   // The legacy call's body; slab_dev is the slab's device address when it is page-locked; stream:
-  // the caller's context stream (a leader launches its batch there).
+  // the caller's context stream (a leader launches its batch there only when the device has no
+  // shared-launch stream).
   int encode(const uint8_t* slab, const uint8_t* slab_dev, const uint32_t* offsets, uint32_t G, uint8_t* repair_out,
              hipStream_t stream) {
     std::unique_lock<std::mutex> lk(mu);
@@ -311,7 +336,8 @@ class Coalescer {
   int device = 0;
   uint32_t P = 0, cap = 0;
   int max_inflight = 2;
-  std::atomic<int> stamps_left{env_long("QUICFEC_COALESCE_STAMPS", 0) != 0 ? 3 : 0};  // diagnostic: the first batches
+  hipStream_t launch_stream = nullptr;  // the device's non-blocking shared-launch stream, if made
+  std::atomic<int> stamps_left{test_knob(TestKnob::kCoalesceStamps, 0) != 0 ? 3 : 0};  // diagnostic: the first batches
   std::mutex mu;
   std::condition_variable cv_room;  // callers waiting for an open batch with room
   std::vector<std::unique_ptr<Batch>> batches;
@@ -319,8 +345,8 @@ class Coalescer {
   std::atomic<int> inflight{0};     // batches closed by a leader and not done yet
   bool staging_ready = false;
   // waiting callers' spin budget before they sleep (pause rounds, then yields)
-  uint32_t spin_pause = static_cast<uint32_t>(env_long("QUICFEC_COALESCE_SPIN_PAUSE", 256));
-  uint32_t spin_yield = static_cast<uint32_t>(env_long("QUICFEC_COALESCE_SPIN_YIELD", 3840));
+  uint32_t spin_pause = static_cast<uint32_t>(test_knob(TestKnob::kCoalesceSpinPause, 256));
+  uint32_t spin_yield = static_cast<uint32_t>(test_knob(TestKnob::kCoalesceSpinYield, 3840));
 
   // One more batch (its page-locked address list and output, its event, and staging when pageable
   // callers have needed it).  Caller holds mu, or owns the coalescer alone (create).
@@ -365,7 +391,8 @@ class Coalescer {
 
   // Closes, launches and completes batch b.  Called with mu held through `lk`; returns with it
   // released.
-  void lead(Batch& b, std::unique_lock<std::mutex>& lk, hipStream_t stream) {
+  void lead(Batch& b, std::unique_lock<std::mutex>& lk, hipStream_t caller_stream) {
+    const hipStream_t stream = launch_stream ? launch_stream : caller_stream;
     b.state.store(Batch::kClosed, std::memory_order_relaxed);
     open = -1;
     open_free();
@@ -407,7 +434,7 @@ class Coalescer {
       }
     }
     const uint64_t t3 = now_ns();
-    if (stamps_left.load(std::memory_order_relaxed) > 0 && stamps_left.fetch_sub(1) > 0) {  // QUICFEC_COALESCE_STAMPS
+    if (stamps_left.load(std::memory_order_relaxed) > 0 && stamps_left.fetch_sub(1) > 0) {  // TestKnob::kCoalesceStamps
       std::fprintf(stderr, "{\"coalescer_batch_us\": {\"close\": %.1f, \"launch\": %.1f, \"done\": %.1f}}\n", (t1 - t0) / 1e3,
                    (t2 - t1) / 1e3, (t3 - t2) / 1e3);
     }
@@ -462,26 +489,15 @@ std::atomic<uint64_t> g_res_inline{0}, g_res_vram{0};
 // while legacy calls were being served, the context's own stream's p50 to 48 ms
 // (scripts/probe_resident_interference.py, profiles/r03_probe_resident_interference.txt).
 // Streams of another priority come from another queue pool, so the instance runs on a
-// non-blocking stream of the highest priority ("high", the default: other streams' p99 52 us,
-// and the instance's relaunch is dispatched ahead of bulk work); a normal-priority stream of
-// the caller never shares its queue.  QUICFEC_RESIDENT_STREAM: "plain" (the old form), "low"
-// (lowest priority), "cumask" (a CU-masked stream, always a queue of its own, but blocking:
-// it orders against the legacy null stream).
-bool create_server_stream(int device, hipStream_t* s) {
-  const char* v = std::getenv("QUICFEC_RESIDENT_STREAM");
-  const std::string mode = v && *v ? v : "high";
-  if (mode == "cumask") {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) return false;
-    std::vector<uint32_t> mask((cus + 31) / 32, 0xFFFFFFFFu);
-    return hipExtStreamCreateWithCUMask(s, static_cast<uint32_t>(mask.size()), mask.data()) == hipSuccess;
-  }
-  if (mode == "high" || mode == "low") {
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return false;
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, mode == "high" ? hi : lo) == hipSuccess;
-  }
-  return hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess;
+// non-blocking stream of the highest priority (other streams' p99 52 us, and the instance's
+// relaunch is dispatched ahead of bulk work); a normal-priority stream of the caller never
+// shares its queue.  (Also measured and not kept: the lowest priority, and a CU-masked stream,
+// which always gets a queue of its own but is blocking: it orders against the legacy null
+// stream.)
+bool create_server_stream(hipStream_t* s) {
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return false;
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi) == hipSuccess;
 }
 
 class Resident {
@@ -492,13 +508,13 @@ class Resident {
     BindDevice bd(device);
     int khz = 0;
     if (!bd.ok || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0 ||
-        !create_server_stream(device, &r->stream)) {
+        !create_server_stream(&r->stream)) {
       (void)hipGetLastError();
       return nullptr;
     }
     const uint64_t per_us = static_cast<uint64_t>(khz) / 1000u;
     r->idle_ticks = per_us * static_cast<uint64_t>(std::max(10L, env_long("QUICFEC_RESIDENT_IDLE_US", 2000)));
-    r->slow_ticks = per_us * static_cast<uint64_t>(std::max(1L, env_long("QUICFEC_RESIDENT_SLOW_US", 50)));
+    r->slow_ticks = per_us * static_cast<uint64_t>(std::max(1L, test_knob(TestKnob::kResidentSlowUs, 50)));
     r->life_ticks = per_us * static_cast<uint64_t>(std::max(100L, env_long("QUICFEC_RESIDENT_LIFE_US", 50000)));
     // The per-slot staging of pageable repair buffers (16 MB) comes with the first call that
     // needs it (ensure_outs): the first context of every process sets a Resident up
@@ -509,23 +525,25 @@ class Resident {
     r->ring_w = reinterpret_cast<ServerSlot*>(r->ring.host);
     r->ring_d = reinterpret_cast<ServerSlot*>(r->ring.dev);
     r->deadline = std::chrono::milliseconds(std::max(1L, env_long("QUICFEC_RESIDENT_DEADLINE_MS", 10000)));
-    // tests: an instance that never serves (relaunch records a launch without launching)
-    r->no_launch = env_long("QUICFEC_RESIDENT_TEST_NOLAUNCH", 0) != 0;
-    // tests: a short tag epoch (fec_kernels.hpp server_tag), so the scrubs at its boundaries run
-    // within a few thousand calls
-    const long ep = std::min<long>(kServerEpoch, std::max(1L, env_long("QUICFEC_RESIDENT_TEST_EPOCH", kServerEpoch)));
+    // Test switches (libfec_hip_test.so only; fec_knobs.hpp):
+    // an instance that never serves (relaunch records a launch without launching);
+    r->no_launch = test_knob(TestKnob::kResidentNoLaunch, 0) != 0;
+    // a short tag epoch (fec_kernels.hpp server_tag), so the scrubs at its boundaries run within
+    // a few thousand calls;
+    const long ep = std::min<long>(kServerEpoch, std::max(1L, test_knob(TestKnob::kResidentEpoch, kServerEpoch)));
     r->epoch = 1u;
     while (r->epoch * 2 <= static_cast<uint32_t>(ep)) r->epoch *= 2;  // a power of two (server_tag)
-    // tests: every inline call lands one chunk in two 8-B pieces, the half with the tag first and
-    // the other ~100 us after the slot's header (a write-combined store evicted in pieces)
-    r->tear = env_long("QUICFEC_RESIDENT_TEST_TEAR", 0) != 0;
-    // tests: the call of this number (0 = the Resident's first) fails as if its deadline had
-    // passed (poisoning under load)
-    r->fail_at = static_cast<uint64_t>(env_long("QUICFEC_RESIDENT_TEST_FAIL_AT", -1));
-    // every call to the next class round robin, however few are in flight (tests: one thread's
-    // n-th call then takes seq n)
-    r->spread = env_long("QUICFEC_RESIDENT_SPREAD", 0) != 0;
-    if (env_long("QUICFEC_RESIDENT_STAMPS", 0) != 0 && !alloc_coherent(r->stamps, 256 * 8 * sizeof(uint64_t))) return nullptr;
+    // every inline call lands one chunk in two 8-B pieces, the half with the tag first and the
+    // other ~100 us after the slot's header (a write-combined store evicted in pieces);
+    r->tear = test_knob(TestKnob::kResidentTear, 0) != 0;
+    // the call of this number (0 = the Resident's first) fails as if its deadline had passed
+    // (poisoning under load);
+    r->fail_at = static_cast<uint64_t>(test_knob(TestKnob::kResidentFailAt, -1));
+    // every call to the next class round robin, however few are in flight (one thread's n-th
+    // call then takes seq n);
+    r->spread = test_knob(TestKnob::kResidentSpread, 0) != 0;
+    // the served batches' phase stamps, printed at exit.
+    if (test_knob(TestKnob::kResidentStamps, 0) != 0 && !alloc_coherent(r->stamps, 256 * 8 * sizeof(uint64_t))) return nullptr;
     r->tick_khz = static_cast<uint64_t>(khz);
     // no word of a slot that was never written carries a tag (tags are 1 .. epoch; alloc_coherent zeroed it)
     std::memset(r->ring.host, 0, sizeof(ServerSlot) * kServerSlots);
@@ -640,7 +658,7 @@ class Resident {
       std::memset(iouts.host + size_t(si) * kInlineOutBytes, 0, kInlineOutBytes);
       std::atomic_thread_fence(std::memory_order_seq_cst);
     }
-    uint64_t torn = ~0ull;  // QUICFEC_RESIDENT_TEST_TEAR: the chunk whose low half is stored late
+    uint64_t torn = ~0ull;  // test switch kResidentTear: the chunk whose low half is stored late
     if (inline_pk) {
       // the packets into the slot's data area (both halves of each chunk carry the tag), then the header
       uint8_t* const area = vinl + size_t(si) * kInlineSlotBytes;
@@ -693,8 +711,10 @@ class Resident {
       while (landed < 2 * G * nch && half_ok(landed)) ++landed;
       return landed == 2 * G * nch;
     };
-    if (call_no.fetch_add(1, std::memory_order_relaxed) == fail_at) {  // tests: this call's deadline passes at once
-      set_last_error("fec_encode_batch: QUICFEC_RESIDENT_TEST_FAIL_AT");
+    // test switch kResidentFailAt: this call's deadline passes at once (no shared counter
+    // otherwise: every call would pay one more contended atomic)
+    if (fail_at != ~0ull && call_no.fetch_add(1, std::memory_order_relaxed) == fail_at) {
+      set_last_error("fec_encode_batch: injected failure (test library)");
       rc = FEC_ERR_HIP;
     }
     for (uint32_t spins = 0; rc == FEC_OK; ++spins) {
@@ -782,7 +802,7 @@ class Resident {
     if (stream) (void)hipStreamDestroy(stream);
   }
 
-  // QUICFEC_RESIDENT_STAMPS: mean phase times of the last (up to) 256 served batches, to stderr.
+  // Test switch kResidentStamps: mean phase times of the last (up to) 256 served batches, to stderr.
   void print_stamps() const {
     const uint64_t* st = reinterpret_cast<const uint64_t*>(stamps.host);
     double sum[7] = {};
@@ -809,18 +829,19 @@ class Resident {
   uint64_t tick_khz = 100000;
   std::unique_ptr<std::atomic<uint64_t>[]> collected;  // per slot: seq + 1 of its last collected call
   std::atomic<uint64_t> class_next[kServerMaxClasses];  // the next seq of each class (c, then + classes)
-  std::atomic<uint32_t> in_flight{0};                   // calls inside encode()
-  std::atomic<uint32_t> rr{0};                          // round robin over the classes in use
-  std::atomic<uint64_t> call_no{0};                     // calls so far (QUICFEC_RESIDENT_TEST_FAIL_AT)
+  // every call updates both: each on a cache line of its own
+  alignas(64) std::atomic<uint32_t> in_flight{0};       // calls inside encode()
+  alignas(64) std::atomic<uint32_t> rr{0};              // round robin over the classes in use
+  std::atomic<uint64_t> call_no{0};                     // calls so far (test switch kResidentFailAt)
   std::mutex mu;
   std::atomic<uint64_t> gen{0};  // generation of the last launched instance (0 = none yet)
   std::atomic<bool> broken{false};
   std::chrono::milliseconds deadline{10000};  // QUICFEC_RESIDENT_DEADLINE_MS
-  bool no_launch = false;                     // QUICFEC_RESIDENT_TEST_NOLAUNCH
-  bool tear = false;                          // QUICFEC_RESIDENT_TEST_TEAR
-  uint64_t fail_at = ~0ull;                   // QUICFEC_RESIDENT_TEST_FAIL_AT
-  bool spread = false;                        // QUICFEC_RESIDENT_SPREAD
-  uint32_t epoch = kServerEpoch;              // QUICFEC_RESIDENT_TEST_EPOCH
+  bool no_launch = false;                     // test switch kResidentNoLaunch
+  bool tear = false;                          // test switch kResidentTear
+  uint64_t fail_at = ~0ull;                   // test switch kResidentFailAt
+  bool spread = false;                        // test switch kResidentSpread
+  uint32_t epoch = kServerEpoch;              // test switch kResidentEpoch
   uint32_t classes = 1;                       // QUICFEC_RESIDENT_SERVERS
   ServerCoord* coord = nullptr;               // device memory shared by the classes' workgroups
   std::atomic<bool> outs_ready{false};
@@ -906,7 +927,7 @@ class Resident {
 
   // An inline slot's packets into its data area through the BAR (fec_kernels.hpp kServerInline):
   // packet p = g * 10 + j as nch 16-B chunks, each two 8-B halves of 6 payload bytes and the tag;
-  // each chunk one 16-B store (write-combined).  torn (tests, QUICFEC_RESIDENT_TEST_TEAR): that
+  // each chunk one 16-B store (write-combined).  torn (test switch kResidentTear): that
   // chunk gets only its high half here; the caller stores the low half after the header.
   static void pack_inline(uint8_t* area, const uint8_t* slab, const uint32_t* offsets, uint32_t G, uint32_t P,
                           uint32_t tag16, uint64_t torn) {
@@ -1110,7 +1131,7 @@ bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* off
   const uint64_t t_for = now_ns();
   *rc = c->encode(slab, sm == HostMem::kPinned ? static_cast<const uint8_t*>(sdev) : nullptr, offsets, num_groups,
                   repair_out, stream);
-  static std::atomic<int> stamps_left{env_long("QUICFEC_COALESCE_STAMPS", 0) != 0 ? 3 : 0};
+  static std::atomic<int> stamps_left{test_knob(TestKnob::kCoalesceStamps, 0) != 0 ? 3 : 0};
   if (stamps_left.load(std::memory_order_relaxed) > 0 && stamps_left.fetch_sub(1) > 0)  // diagnostic
     std::fprintf(stderr, "{\"coalesced_call_us\": {\"classify\": %.1f, \"coalescer_for\": %.1f, \"encode\": %.1f}}\n",
                  (t_cls - t_enter) / 1e3, (t_for - t_cls) / 1e3, (now_ns() - t_for) / 1e3);
@@ -1119,9 +1140,14 @@ bool coalesce_legacy_encode(int device, const uint8_t* slab, const uint32_t* off
 
 }  // namespace qfec
 
-QFEC_EXPORT int fec_coalesce_stats(FECCoalesceStats* out, int reset) {
-  if (!out) return FEC_ERR_NULL;
+// The totals are gathered into a full struct of this build and copied out at the caller's size:
+// a binary built against an older fec_hip.h (a smaller struct) never has fields written past it.
+QFEC_EXPORT int fec_coalesce_stats_sized(FECCoalesceStats* caller, size_t caller_bytes, int reset) {
+  if (!caller) return FEC_ERR_NULL;
   using namespace qfec;
+  if (caller_bytes < kCoalesceStatsV4Bytes) return FEC_ERR_RANGE;
+  FECCoalesceStats full{};
+  FECCoalesceStats* const out = &full;
   out->calls = g_calls.load();
   out->groups = g_groups.load();
   out->batches = g_batches.load();
@@ -1165,5 +1191,12 @@ QFEC_EXPORT int fec_coalesce_stats(FECCoalesceStats* out, int reset) {
     g_max_batch = 0;
     g_max_calls = 0;
   }
+  std::memcpy(caller, &full, std::min(caller_bytes, sizeof(full)));
   return FEC_OK;
+}
+
+// The round-4 entry point: the 15 fields it was published with, never more (its callers' struct
+// may end there).  New callers use fec_coalesce_stats_sized.
+QFEC_EXPORT int fec_coalesce_stats(FECCoalesceStats* out, int reset) {
+  return fec_coalesce_stats_sized(out, qfec::kCoalesceStatsV4Bytes, reset);
 }

@@ -30,6 +30,7 @@
 #include "bitslice.hpp"
 #include "coef_tables.hpp"
 #include "fec_kernels.hpp"
+#include "fec_knobs.hpp"
 
 namespace qfec {
 namespace {
@@ -80,7 +81,7 @@ constexpr int kPairMac = 4096;
 // pieces of different instructions (PMC writes 1.046x algorithmic at k=10 r=3, 1.053x at k=20
 // r=5).
 constexpr int kStageRows = 8192;
-constexpr int kEncodeStageDefault = 1;  // QUICFEC_ENCODE_STAGE unset: on (C2 encode 2.753 -> 2.659 ms, C4 5.578 -> 5.520; profiles/r05a)
+constexpr int kEncodeStageDefault = 1;  // on: C2 encode 2.753 -> 2.659 ms, C4 5.578 -> 5.520 (profiles/r05a)
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
@@ -1943,7 +1944,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
     n_scrub = *reinterpret_cast<const volatile uint64_t*>(&ctl->scrubs[cls]);
   }
   lds_barrier();
-  // Diagnostic stamps (stamps != nullptr, QUICFEC_RESIDENT_STAMPS): thread 0's wall clock at the
+  // Diagnostic stamps (stamps != nullptr; the test library's TestKnob::kResidentStamps): thread 0's wall clock at the
   // phases of each served batch, into a ring of 256 records of 8 words in host memory that no
   // other code reads; never part of a result.
   uint64_t st_batches = 0, st_polls = 0, st_t[7] = {};
@@ -2027,8 +2028,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
           leave = leave || idle;
         } else {
           // every class idle (this one now, the others by their published flags), or told to leave
-          bool all_idle = idle;
-          for (uint32_t c = 0; c < K; ++c) all_idle = all_idle && (c == cls || s_idle[c] == gen);
+          const bool all_idle = server_all_idle(idle, s_idle, K, cls, gen);
           if (idle != was_idle) {
             sys_store_relaxed(&coord->idle[cls], idle ? gen : 0);
             was_idle = idle;
@@ -2228,10 +2228,10 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
       // count until the first of this one's); at most `classes` contenders, so the loop ends
       uint64_t v = __hip_atomic_load(&coord->exits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), nv = 0;
       do {
-        nv = (v >> 8) == gen ? v + 1 : (gen << 8) | 1u;
+        nv = server_exits_next(v, gen);
       } while (!__hip_atomic_compare_exchange_strong(&coord->exits, &v, nv, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_SYSTEM));
-      last = (nv & 0xFFu) == K;
+      last = server_exits_last(nv, K);
     }
     if (last) sys_store_release(&ctl->exited, gen);
   }
@@ -2241,11 +2241,11 @@ constexpr uint32_t kMaxThreadsPerLaunch = 1u << 30;
 // Wave-per-group decode launches: 256-thread workgroups, so at most 2^22 of them keep the
 // grid's work-item count (blocks * 256) inside 32 bits with room to spare.
 constexpr uint64_t kMaxWaveBlocks = kMaxThreadsPerLaunch / 256u;
-// Blocks per wave-per-group decode launch: kMaxWaveBlocks, or QUICFEC_MAX_WAVE_BLOCKS (tests
-// force the chunked launches, which otherwise start only past 16.7M groups).
-uint64_t max_wave_blocks() {  // read per launch: tests switch it inside one process
-  const char* e = std::getenv("QUICFEC_MAX_WAVE_BLOCKS");
-  const long long n = e && *e ? std::atoll(e) : 0;
+// Blocks per wave-per-group decode launch: kMaxWaveBlocks (the test library's
+// TestKnob::kMaxWaveBlocks forces the chunked launches, which otherwise start only past 16.7M
+// groups).
+uint64_t max_wave_blocks() {
+  const long n = test_knob(TestKnob::kMaxWaveBlocks, 0);
   return n > 0 && static_cast<uint64_t>(n) < kMaxWaveBlocks ? static_cast<uint64_t>(n) : kMaxWaveBlocks;
 }
 constexpr uint32_t kVecMinP = 16;  // shorter packets take the byte kernels
@@ -2259,17 +2259,13 @@ inline uint32_t blocks_for(uint64_t n) { return static_cast<uint32_t>((n + 255) 
 // ---------------------------------------------------------------------------------
 namespace {
 
-// Tuning override of an occupancy cap from the environment (-1 = none), else `def`.
-int env_waves(const char* name, int def) {
-  const char* v = std::getenv(name);
-  return v && *v ? std::atoi(v) : def;
-}
+// A test-library switch (fec_knobs.hpp) as an int; `def` in the product library.
+int knob(TestKnob k, int def) { return static_cast<int>(test_knob(k, def)); }
 
 // XCD-aware group order for a decode kernel: at k=10 r=3 measured +10% for decode_fused and
 // -1%..+5% for decode_wave over two boxes (tools/probe_decode.hip; tunable per kernel).
 uint32_t decode_swizzle(const DecodeLaunch& a, int tuned) {
-  // QUICFEC_DECODE_SWIZZLE: 0 / 1 overrides the tuned default (A/B across boxes)
-  return static_cast<uint32_t>(a.xcd_swizzle >= 0 ? a.xcd_swizzle : env_waves("QUICFEC_DECODE_SWIZZLE", tuned));
+  return static_cast<uint32_t>(a.xcd_swizzle >= 0 ? a.xcd_swizzle : tuned);
 }
 
 
@@ -2294,11 +2290,11 @@ uint32_t pick_tile(uint32_t cpp, uint32_t k, uint32_t P) {
   return best;
 }
 
-// Groups per workgroup of the tiled encodes (encode_bits: per half): QUICFEC_ENCODE_TILE (tuning
-// A/B; must fit 512 lanes), else pick_tile.
+// Groups per workgroup of the tiled encodes (encode_bits: per half): pick_tile (the test
+// library's TestKnob::kEncodeTile overrides it when the tile fits 512 lanes).
 uint32_t encode_tile(const EncodeLaunch& a) {
   const uint32_t cpp = (a.P + 15u) / 16u;
-  const int tile_env = env_waves("QUICFEC_ENCODE_TILE", 0);
+  const int tile_env = knob(TestKnob::kEncodeTile, 0);
   return tile_env > 0 && cpp > 0 && uint32_t(tile_env) * cpp <= 512 ? uint32_t(tile_env) : pick_tile(cpp, a.k, a.P);
 }
 
@@ -2306,7 +2302,6 @@ uint32_t encode_tile(const EncodeLaunch& a) {
 template <int K, int R, int OFF, bool FIRST, int POL = kNtStore>
 hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
   const uint32_t cpp = (a.P + 15u) / 16u;
-  // QUICFEC_ENCODE_TILE: groups per workgroup override (tuning A/B; must fit 512 lanes)
   const uint32_t tile = encode_tile(a);
   const uint64_t gchunk = kMaxThreadsPerLaunch / cpp;
   for (uint64_t g0 = 0; g0 < a.groups; g0 += gchunk) {
@@ -2324,12 +2319,12 @@ hipError_t run_encode_v16(const EncodeLaunch& a, uint32_t row0, hipStream_t s) {
       // 4; at 1400 B (7-wave workgroups) 2 (14 waves) beats 3 (21) by 1.7%
       // (profiles/r02_ab_encode_blocks_r1.txt, r02_ab_encode_blocks_r2.txt).
       constexpr int kDefBlocks = K == 0 ? 0 : (R >= 4 ? kEncodeBlocksPerCU + 2 : kEncodeBlocksPerCU);
-      const int blocks_per_cu = env_waves("QUICFEC_ENCODE_BLOCKS", kDefBlocks);
-      const char* eb = std::getenv("QUICFEC_ENCODE_BLOCKS");
-      const bool xor_waves = K > 0 && FIRST && R == 1 && !(eb && *eb);
+      const int blocks_env = knob(TestKnob::kEncodeBlocks, -1);
+      const int blocks_per_cu = blocks_env >= 0 ? blocks_env : kDefBlocks;
+      const bool xor_waves = K > 0 && FIRST && R == 1 && blocks_env < 0;
       const int waves = a.waves_per_cu ? a.waves_per_cu
-                                       : env_waves("QUICFEC_ENCODE_WAVES", xor_waves ? kEncodeXorWavesPerCU
-                                                                                     : blocks_per_cu * static_cast<int>(bs / 64));
+                                       : knob(TestKnob::kEncodeWaves, xor_waves ? kEncodeXorWavesPerCU
+                                                                                : blocks_per_cu * static_cast<int>(bs / 64));
       uint32_t smem = occupancy_cap_lds(waves, bs / 64);
       if constexpr ((POL & kStageRows) != 0) smem = std::max<uint32_t>(smem, tile * R * a.P);
       hipLaunchKernelGGL((encode_v16<K, R, OFF, FIRST, POL>), dim3(blocks), dim3(bs), smem, s, a.data,
@@ -2360,7 +2355,7 @@ hipError_t run_encode_bits(const EncodeLaunch& a, hipStream_t s) {
     // VGPRs).  Staged rows (kStageRows): 2 workgroups per CU, 5.163 vs 5.246 ms uncapped on two
     // boxes (scripts/sweep_encode_tiles.py, profiles/r05h, r05i).
     constexpr int kDefWaves = (POL & kStageRows) != 0 ? 10 : 0;
-    const int waves = a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_ENCODE_WAVES", kDefWaves);
+    const int waves = a.waves_per_cu ? a.waves_per_cu : knob(TestKnob::kEncodeWaves, kDefWaves);
     uint32_t smem = occupancy_cap_lds(waves, bs / 64);
     if constexpr ((POL & kStageRows) != 0) smem = std::max<uint32_t>(smem, 2 * tile * R * a.P);
     hipLaunchKernelGGL((encode_bits<K, R, W, POL>), dim3(blocks), dim3(bs), smem, s, a.data, a.parity, g0, cpp, a.P,
@@ -2371,18 +2366,18 @@ hipError_t run_encode_bits(const EncodeLaunch& a, hipStream_t s) {
   return hipSuccess;
 }
 
-// Bit-sliced encode for a compile-time shape: QUICFEC_ENCODE_BITS=0 never, 1 for every
-// instantiated shape, default (-1) where it is faster than the tables (r >= 4: the table
-// form is VALU-bound there).
+// Bit-sliced encode for a compile-time shape where it is faster than the tables (r >= 4: the
+// table form is VALU-bound there); the test library's TestKnob::kEncodeBits forces it on (1,
+// every compiled shape) or off (0).
 bool use_encode_bits(uint32_t r) {
-  const int mode = env_waves("QUICFEC_ENCODE_BITS", -1);
+  const int mode = knob(TestKnob::kEncodeBits, -1);
   return mode == 1 || (mode < 0 && r >= 4);
 }
 
 // kStageRows for a launch whose workgroup window (groups_per_block * r * P bytes) fits the LDS a
-// workgroup may take: QUICFEC_ENCODE_STAGE=1 on, 0 off (read per launch: A/B in one process).
+// workgroup may take (the test library's TestKnob::kEncodeStage: 1 on, 0 off).
 bool use_stage_rows(const EncodeLaunch& a, uint32_t groups_per_block) {
-  const int mode = env_waves("QUICFEC_ENCODE_STAGE", kEncodeStageDefault);
+  const int mode = knob(TestKnob::kEncodeStage, kEncodeStageDefault);
   return mode == 1 && a.P % 16 == 0 && uint64_t(groups_per_block) * a.r * a.P <= 64u * 1024u;
 }
 
@@ -2443,50 +2438,29 @@ hipError_t launch_encode(const EncodeLaunch& a, hipStream_t s) {
     if (a.off_kind == OffsetKind::kNone) {
       // The paired-coefficient arithmetic (kPairMac): +0.9% at k=20 r=5 (5.53 vs 5.58 ms),
       // +1.0% at k=10 r=3 (2.65 vs 2.68 ms), same box, alternating runs
-      // (profiles/r02_ab_encode_pair.txt).  QUICFEC_ENCODE_PAIR=0 restores the single form.
-      static const bool pair = env_waves("QUICFEC_ENCODE_PAIR", 1) == 1;
+      // (profiles/r02_ab_encode_pair.txt).  Staged rows keep the default cache policy, NT stores
+      // with cached loads (C2 2.590 ms vs 2.606-2.702, C4 4.991 vs 5.062-5.345 for the other
+      // three; profiles/r05k/sweep_mempol.jsonl).
       // Bit-sliced form (bitslice.hpp) while a workgroup holds whole groups.  k=20 r=5 (VALU-
       // bound with the tables): 5.24-5.41 vs 5.37-5.54 ms over six boxes; k=10 r=3 (HBM-bound
-      // with the tables) 2.74-2.76 vs 2.63-2.66 ms, so opt-in there (QUICFEC_ENCODE_BITS=1).
-      // QUICFEC_ENCODE_BITS_WINDOW: packets in flight per lane (4; 2: 5.70 ms, 8: 5.28, 20: 5.91-6.03).
+      // with the tables) 2.74-2.76 vs 2.63-2.66 ms, so not chosen there.  4 packets in flight per
+      // lane (2: 5.70 ms, 8: 5.28, 20: 5.91-6.03; profiles/r03_ab_bits.txt).
       if (a.P <= 8192 && use_encode_bits(a.r)) {
-        const int w = env_waves("QUICFEC_ENCODE_BITS_WINDOW", 4);
         const bool stg = use_stage_rows(a, 2 * encode_tile(a));
-        if (a.k == 20 && a.r == 5) {
-          if (stg) {
-            switch (env_waves("QUICFEC_ENCODE_MEMPOL", 0)) {  // as for k=10 r=3 below
-              case 1: return run_encode_bits<20, 5, 4, kStageRows>(a, s);
-              case 2: return run_encode_bits<20, 5, 4, kNtLoad | kNtStore | kStageRows>(a, s);
-              case 3: return run_encode_bits<20, 5, 4, kNtLoad | kStageRows>(a, s);
-              default: return run_encode_bits<20, 5, 4, kNtStore | kStageRows>(a, s);
-            }
-          }
-          return w >= 8 ? run_encode_bits<20, 5, 8>(a, s) : run_encode_bits<20, 5, 4>(a, s);
-        }
+        if (a.k == 20 && a.r == 5)
+          return stg ? run_encode_bits<20, 5, 4, kNtStore | kStageRows>(a, s) : run_encode_bits<20, 5, 4>(a, s);
         if (a.k == 10 && a.r == 3) return stg ? run_encode_bits<10, 3, 4, kNtStore | kStageRows>(a, s) : run_encode_bits<10, 3, 4>(a, s);
       }
-      if (a.k == 10 && a.r == 3) {
-        if (pair && use_stage_rows(a, encode_tile(a))) {
-          switch (env_waves("QUICFEC_ENCODE_MEMPOL", 0)) {  // tuning A/B of the staged form's cache policy
-            case 1: return run_encode_v16<10, 3, 0, true, kPairMac | kStageRows>(a, 0, s);
-            case 2: return run_encode_v16<10, 3, 0, true, kNtLoad | kNtStore | kPairMac | kStageRows>(a, 0, s);
-            case 3: return run_encode_v16<10, 3, 0, true, kNtLoad | kPairMac | kStageRows>(a, 0, s);
-            default: return run_encode_v16<10, 3, 0, true, kNtStore | kPairMac | kStageRows>(a, 0, s);
-          }
-        }
-        return pair ? run_encode_v16<10, 3, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<10, 3, 0, true>(a, 0, s);
-      }
+      if (a.k == 10 && a.r == 3) return run_encode_v16_staged<10, 3, 0, kNtStore | kPairMac>(a, s);
       // staged rows measured per shape (scripts/ab_stage_rows.py, profiles/r05k): k=10 r=1 level
       // (2.383 vs 2.378 ms), k=10 r=2 -1.5% (2.537 vs 2.575), k=4 r=2 +8.9% (1.351 vs 1.241): the
       // XOR row and k=4 keep their direct stores
       if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 0, true>(a, 0, s);
-      if (a.k == 20 && a.r == 5)
-        return pair ? run_encode_v16<20, 5, 0, true, kNtStore | kPairMac>(a, 0, s) : run_encode_v16<20, 5, 0, true>(a, 0, s);
+      if (a.k == 20 && a.r == 5) return run_encode_v16<20, 5, 0, true, kNtStore | kPairMac>(a, 0, s);
       if (a.k == 4 && a.r == 2) return run_encode_v16<4, 2, 0, true>(a, 0, s);
-      // k=10 r=2 (the campaign's 20% FEC rate): compile-time k unless QUICFEC_ENCODE_RUNTIME_K=1
-      // (A/B against the runtime-k loop)
-      static const bool rt_k = env_waves("QUICFEC_ENCODE_RUNTIME_K", 0) == 1;
-      if (a.k == 10 && a.r == 2 && !rt_k) return run_encode_v16_staged<10, 2, 0, kNtStore | kPairMac>(a, s);
+      // k=10 r=2 (the campaign's 20% FEC rate): compile-time k (2.50 vs 2.56 ms for the runtime-k
+      // loop, profiles/r02_ab_encode_r1r2_defaults.txt)
+      if (a.k == 10 && a.r == 2) return run_encode_v16_staged<10, 2, 0, kNtStore | kPairMac>(a, s);
     } else if (a.off_kind == OffsetKind::kU32) {
       if (a.k == 10 && a.r == 1) return run_encode_v16<10, 1, 1, true>(a, 0, s);
     } else if (a.off_kind == OffsetKind::kAddr) {
@@ -2533,7 +2507,7 @@ hipError_t run_decode_v16(const DecodeLaunch& a, hipStream_t s) {
 template <int K, int MAXE, int POL>
 hipError_t run_decode_wave(const DecodeLaunch& a, hipStream_t s) {
   const uint32_t passes = (a.r + MAXE - 1) / MAXE;  // e <= r
-  const uint32_t cap = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_DECODE_WAVES", kDecodeWavesPerCU), 4);
+  const uint32_t cap = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : knob(TestKnob::kDecodeWaves, kDecodeWavesPerCU), 4);
   for (uint32_t p = 0; p < passes; ++p) {
     const uint32_t m0 = p * MAXE;
     // kLdsTabs: per-wave slice of whole 1 KiB wave-loads covering this pass's rows
@@ -2562,7 +2536,7 @@ template <int K, int MAXE, int POL, int NM, int NT, bool DIRECT = false, bool IN
 hipError_t run_decode_fused(const DecodeLaunch& a, hipStream_t s) {
   constexpr uint64_t kGroupsPerBlock = SCAN > 64 ? SCAN : 4u * (SCAN > 0 ? SCAN : 1);
   const uint32_t passes = (a.r + MAXE - 1) / MAXE;
-  const uint32_t smem = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : env_waves("QUICFEC_DECODE_WAVES", kDecodeWavesPerCU), 4);
+  const uint32_t smem = occupancy_cap_lds(a.waves_per_cu ? a.waves_per_cu : knob(TestKnob::kDecodeWaves, kDecodeWavesPerCU), 4);
   RankMeta rm{};
   for (int e = 1; e <= 3; ++e) {
     rm.base[e] = a.meta.base[e];
@@ -2640,16 +2614,6 @@ hipError_t try_decode_fused(const DecodeLaunch& a, hipStream_t s, bool direct, b
 #define QFEC_FUSED_P(M, KK, RR)                                                               \
   M(KK, RR, 0, 1) M(KK, RR, 0, 2) M(KK, RR, 0, 3) M(KK, RR, 0, 4) M(KK, RR, 1, 0) M(KK, RR, 1, 1) \
   M(KK, RR, 1, 2) M(KK, RR, 1, 3) M(KK, RR, 1, 4)
-  // tuning A/B of the C3 slot recover's cache policy in the bench's step (QUICFEC_DECODE_MEMPOL,
-  // read per launch: 1 NT loads + plain stores, 2 plain loads + NT stores, 3 plain both)
-  if (!dry && direct && a.compact_out && a.scan != kDecodeScanGroups && a.k == 10 && a.r == 3 && nm == 1 && nt == 1) {
-    switch (env_waves("QUICFEC_DECODE_MEMPOL", 0)) {
-      case 1: return run_decode_fused<10, 3, kNtLoad | kCompactOut, 1, 1, true>(a, s);
-      case 2: return run_decode_fused<10, 3, kNtStore | kCompactOut, 1, 1, true>(a, s);
-      case 3: return run_decode_fused<10, 3, kCompactOut, 1, 1, true>(a, s);
-      default: break;
-    }
-  }
   QFEC_FUSED_P(QFEC_FUSED_DS, 10, 3)
   QFEC_FUSED_R(10, 3, 1, 1)
   QFEC_FUSED_P(QFEC_FUSED_L, 20, 5)
@@ -2734,8 +2698,8 @@ hipError_t launch_rows_prefix(const uint64_t* masks, uint64_t groups, uint32_t k
   if (groups == 0) return hipSuccess;
   const uint64_t nb = (groups + kRowsPerBlock - 1) / kRowsPerBlock;
   if (nb > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  // QUICFEC_ROWS_DIRECT_BLOCKS: the two-launch form's block limit (tests force the other form)
-  const uint64_t direct_max = static_cast<uint64_t>(env_waves("QUICFEC_ROWS_DIRECT_BLOCKS", kRowsDirectBlocks));
+  // the two-launch form's block limit (the test library's TestKnob::kRowsDirectBlocks forces the other form)
+  const uint64_t direct_max = static_cast<uint64_t>(knob(TestKnob::kRowsDirectBlocks, kRowsDirectBlocks));
   const dim3 grid(static_cast<uint32_t>(nb));
   hipLaunchKernelGGL(rows_block_sums, grid, dim3(256), 0, s, masks, groups, k, r, block_sums);
   if (nb <= direct_max) {
@@ -2762,23 +2726,14 @@ uint64_t runs_blocks_per_launch(uint64_t groups) {
   return nb < mb ? nb : mb;
 }
 
-// The tile recover's row stores: non-temporal (default) or plain (QUICFEC_RUNS_NT_STORE=0, read
-// per launch).  Back-to-back recovers alone favour plain stores by 10-15% on this round's boxes
-// (profiles/r05c, r05e, r05i probe_runs_c5.txt), but there the 0.13 GB of rows stay in the
-// Infinity Cache from one launch to the next (the form's time equals its no-store floor); in the
-// bench's step, after the encode's 15.6 GB, the two policies recover in the same 0.254 ms and the
-// plain rows' write-back lands in the next encode (+0.01 ms; profiles/r05j/ab_legs.jsonl).
-template <int K, int R, int NM, int NT, int POL>
-hipError_t run_recover_runs_pol(const RunsLaunch& a, uint32_t stage, hipStream_t s);
-
-template <int K, int R, int NM, int NT>
+// The tile recover's row stores are non-temporal.  Back-to-back recovers alone favour plain
+// stores by 10-15% on round 5's boxes (profiles/r05c, r05e, r05i probe_runs_c5.txt), but there
+// the 0.13 GB of rows stay in the Infinity Cache from one launch to the next (the form's time
+// equals its no-store floor); in the bench's step, after the encode's 15.6 GB, the two policies
+// recover in the same 0.254 ms and the plain rows' write-back lands in the next encode (+0.01 ms;
+// profiles/r05j/ab_legs.jsonl).
+template <int K, int R, int NM, int NT, int POL = kNtLoad | kNtStore>
 hipError_t run_recover_runs(const RunsLaunch& a, uint32_t stage, hipStream_t s) {
-  return env_waves("QUICFEC_RUNS_NT_STORE", 1) == 1 ? run_recover_runs_pol<K, R, NM, NT, kNtLoad | kNtStore>(a, stage, s)
-                                                    : run_recover_runs_pol<K, R, NM, NT, kNtLoad>(a, stage, s);
-}
-
-template <int K, int R, int NM, int NT, int POL>
-hipError_t run_recover_runs_pol(const RunsLaunch& a, uint32_t stage, hipStream_t s) {
   RankMeta rm{};
   for (int e = 1; e <= 3; ++e) {
     rm.base[e] = a.meta.base[e];
@@ -2846,7 +2801,7 @@ bool runs_supported(uint32_t k, uint32_t r, uint32_t P) {
 uint32_t runs_stage_bytes(const RunsLaunch& a) {
   // the run image needs 16-B aligned row starts in LDS and in HBM
   if (a.P % 16u != 0 || reinterpret_cast<uintptr_t>(a.out) % 16u != 0) return 0;
-  const int v = a.stage_bytes >= 0 ? a.stage_bytes : env_waves("QUICFEC_RUNS_STAGE", kRunsStageBytes);
+  const int v = a.stage_bytes >= 0 ? a.stage_bytes : knob(TestKnob::kRunsStage, kRunsStageBytes);
   if (v <= 0) return 0;
   const uint32_t cap = 64u * 1024u;  // dynamic LDS per workgroup (160 KiB per CU)
   return static_cast<uint32_t>(v) < cap ? static_cast<uint32_t>(v) : cap;

@@ -137,11 +137,11 @@ struct RunsLaunch {
   // look-back epoch of the first launch; a call takes runs_launches(groups) epochs, never
   // reused while the workspace lives (the caller counts; < 2^30, then re-zero the workspace)
   uint32_t epoch;
-  int stage_bytes = -1;      // LDS run image: -1 tuned default (QUICFEC_RUNS_STAGE), 0 none
+  int stage_bytes = -1;      // LDS run image: -1 tuned default (test switch kRunsStage), 0 none
 };
 // LDS run image per workgroup of 512 groups (tools/probe_runs.hip): C5's
 // ~59 rows per tile fit 48 KB (40 rows) mostly; two workgroups per CU.
-// recover_runs' run image per workgroup (QUICFEC_RUNS_STAGE).
+// recover_runs' run image per workgroup.
 constexpr int kRunsStageBytes = 48 * 1024;
 bool runs_supported(uint32_t k, uint32_t r, uint32_t P);
 uint32_t runs_launches(uint64_t groups);
@@ -166,7 +166,7 @@ bool decode_compact_tables(const DecodeLaunch& a);
 //
 // Tags and the epoch.  A slot's tag is (lap & (epoch - 1)) + 1 with lap = seq / kServerSlots and
 // epoch a power of two (no division on the server's critical path), so the tags of one slot
-// repeat every `epoch` laps (32768 by default; QUICFEC_RESIDENT_TEST_EPOCH for tests).  A word left from the previous epoch could carry the current tag (a word written
+// repeat every `epoch` laps (32768; shorter in the test library, fec_knobs.hpp kResidentEpoch).  A word left from the previous epoch could carry the current tag (a word written
 // exactly `epoch` laps ago and not since, e.g. a later group's address word under inline-only
 // calls), so the slot is scrubbed at every epoch boundary: the server zeroes the slot's words
 // and its inline data area after serving the last lap of an epoch, before that slot's done word
@@ -233,6 +233,22 @@ struct alignas(64) ServerCoord {
   uint64_t pad[6];
   uint64_t idle[kServerMaxClasses];    // gen while class c's workgroup has been idle for idle_ticks, else 0
 };
+// The coordination rules, shared by legacy_server and the CPU model (tests/csrc/ring_protocol_test.cpp).
+// Whether every class of instance gen is idle: this one (idle, now) and the others by the flags
+// it last read (idle_seen[c] == gen; a flag of an earlier instance never counts).
+__host__ __device__ inline bool server_all_idle(bool idle, const uint64_t* idle_seen, uint32_t classes, uint32_t cls,
+                                                uint64_t gen) {
+  bool all = idle;
+  for (uint32_t c = 0; c < classes; ++c) all = all && (c == cls || idle_seen[c] == gen);
+  return all;
+}
+// The exit count: a workgroup leaving instance gen turns the word v into this (the word still
+// holds the previous instance's count until the first of this one's); the workgroup whose new
+// word counts all `classes` is the last out and stores ctl->exited = gen.
+__host__ __device__ inline uint64_t server_exits_next(uint64_t v, uint64_t gen) {
+  return (v >> 8) == gen ? v + 1 : (gen << 8) | 1u;
+}
+__host__ __device__ inline bool server_exits_last(uint64_t nv, uint32_t classes) { return (nv & 0xFFu) == classes; }
 // One resident instance serving the ring, each class from its progress mark, until every class
 // has found nothing to do for idle_ticks, or it lived life_ticks (wall-clock ticks,
 // hipDeviceAttributeWallClockRate), or the host sets ctl->stop; on leaving a workgroup stores its
@@ -240,7 +256,7 @@ struct alignas(64) ServerCoord {
 // coord: nullptr when classes == 1.  slow_ticks: a workgroup other than class 0's without work
 // for that long polls slowly (~5 us apart instead of ~1.5) until it finds some.
 // stamps: nullptr, or 256 x 8 words of host memory for the diagnostic phase stamps of class 0
-// (QUICFEC_RESIDENT_STAMPS).
+// (test library, fec_knobs.hpp kResidentStamps).
 // inl: the inline data areas (kInlineSlotBytes per slot) when the ring is in VRAM, else nullptr;
 // then the host's stop word (host memory) is read by every 16th poll only, not every poll.
 // epoch: laps per tag epoch (server_tag), a power of two, 1 .. kServerEpoch.

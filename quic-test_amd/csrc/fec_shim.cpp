@@ -32,6 +32,7 @@
 #include "fec_hip.h"
 #include "fec_internal.hpp"
 #include "fec_kernels.hpp"
+#include "fec_knobs.hpp"
 #include "gf256.hpp"
 
 #define QFEC_EXPORT extern "C" __attribute__((visibility("default")))
@@ -621,8 +622,6 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   a.r = r;
   a.P = P;
   a.rec_ready = !plan->dense;
-  // same-box A/B of the decode forms (tuning; the qfec::kDecode* numbers)
-  if (const char* v = std::getenv("QUICFEC_DECODE_VARIANT")) a.variant = std::atoi(v);
   if (plan->dense && qfec::decode_compact_tables(a)) {
     // the form reads bare coefficient bytes: the compact book of the same patterns
     if (!plan->cbook.ptr) {
@@ -644,10 +643,10 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
   }
   // Groups per wave of the mask-addressed form: the scan form when the caller knows that
   // few groups need a rebuild (need_share, from a host scan of the masks); device-resident
-  // callers get one wave per group unless QUICFEC_DECODE_SCAN asks otherwise (tuning).
+  // callers get one wave per group (the test library's TestKnob::kDecodeScan overrides it).
   if (need_share < 0.0) need_share = ctx->decode_need_share;
   if (need_share >= 0.0 && need_share < qfec::kDecodeScanMaxShare) a.scan = qfec::kDecodeScanGroups;
-  if (const char* v = std::getenv("QUICFEC_DECODE_SCAN")) a.scan = static_cast<uint32_t>(std::atoi(v));
+  a.scan = static_cast<uint32_t>(qfec::test_knob(qfec::TestKnob::kDecodeScan, a.scan));
   if (row_start != nullptr) {
     // packed rows: only the mask-addressed (inline-classify) forms place rows by row_start,
     // which they read from rec_off
@@ -655,15 +654,13 @@ int decode_dev_locked(FECEncoderCtx* ctx, uint8_t* d_data, const uint8_t* d_pari
       set_error("packed recover: no mask-addressed form for k=%u r=%u P=%u (use fec_recover_batch_rs_dev)", k, r, P);
       return FEC_ERR_RANGE;
     }
-    // Sparse loss (the scan form's share, or QUICFEC_PACKED_RUNS=1): one launch, recover_runs --
+    // Sparse loss (the scan form's share): one launch, recover_runs --
     // each workgroup finds its rows' place by decoupled look-back and writes them as one run
     // (C5: 0.229-0.235 vs 0.242-0.268 ms for the slot rows; profiles/r04_probe_runs_*.txt).
     // Dense loss keeps the prefix launches + decode_fused (the runs form rebuilds a workgroup's
-    // groups wave by wave: 2.7-2.8 vs 2.2-2.45 ms at C3).  QUICFEC_PACKED_RUNS=0: never.
-    const long runs_env = [] {
-      const char* v = std::getenv("QUICFEC_PACKED_RUNS");
-      return v && *v ? std::atol(v) : -1L;
-    }();
+    // groups wave by wave: 2.7-2.8 vs 2.2-2.45 ms at C3).  The test library's
+    // TestKnob::kPackedRuns forces it on (1) or off (0).
+    const long runs_env = qfec::test_knob(qfec::TestKnob::kPackedRuns, -1);
     if (runs_env != 0 && (runs_env == 1 || a.scan == qfec::kDecodeScanGroups) && qfec::runs_supported(k, r, P)) {
       qfec::RunsLaunch ra{};
       ra.data = d_data;

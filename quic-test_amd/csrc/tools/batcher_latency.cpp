@@ -453,7 +453,7 @@ int legacy(int S, double rate, double seconds) {
     oracle_xor_avx2(p, kK, kP, xr.data() + size_t(g) * kP);
   }
   FECCoalesceStats cs{};
-  fec_coalesce_stats(&cs, 1);
+  fec_coalesce_stats_sized(&cs, sizeof(cs), 1);
   std::mutex mu;
   std::vector<double> all;
   std::atomic<long> groups{0}, errors{0}, fallback{0};
@@ -493,7 +493,7 @@ int legacy(int S, double rate, double seconds) {
   for (auto& t : th) t.join();
   const double wall = rate > 0 ? seconds : std::chrono::duration<double>(Clock::now() - t0).count();
   const double cpu = cpu_seconds() - c0;
-  fec_coalesce_stats(&cs, 0);
+  fec_coalesce_stats_sized(&cs, sizeof(cs), 0);
   const char* co = std::getenv("QUICFEC_COALESCE");
   const char* res = std::getenv("QUICFEC_RESIDENT");
   char cfg[1024];
@@ -534,7 +534,7 @@ int legacy_raw(int calls) {
   for (int j = 0; j < kK; ++j) p[j] = slab + size_t(j) * kP;
   oracle_xor_avx2(p, kK, kP, xr.data());
   FECCoalesceStats cs{};
-  fec_coalesce_stats(&cs, 1);
+  fec_coalesce_stats_sized(&cs, sizeof(cs), 1);
   std::vector<double> us;
   long errors = 0;
   const auto t0 = Clock::now();
@@ -545,7 +545,7 @@ int legacy_raw(int calls) {
     if (std::memcmp(rep, xr.data(), kP)) ++errors;
   }
   const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
-  fec_coalesce_stats(&cs, 0);
+  fec_coalesce_stats_sized(&cs, sizeof(cs), 0);
   // where the slowest calls are (the first call pays any lazily created state)
   const size_t imax = us.empty() ? 0 : size_t(std::max_element(us.begin(), us.end()) - us.begin());
   std::vector<double> rest(us.begin() + (us.empty() ? 0 : 1), us.end());

@@ -6,8 +6,14 @@
 // is checked against the XOR computed here -- no oracle, so bench.py may run it outside its
 // cpu_baseline leg.  Links only libfec_hip.so and the mirror (libquicfec_host.so).
 //
+// `batcher` is the opt-in integration that changes the call site: every stream's
+// BatchedFECEncoder shares one SharedFECBatcher (fec_batcher_*), submits its groups without
+// waiting and collects the repair packets as batches finish; r rows per group, every row checked
+// (row 0 the XOR, rows 1.. the code's GF(2^8) rows from fec_parity_matrix and a multiply here).
+//
 //   call_site raw CALLS
 //   call_site streams S SECONDS
+//   call_site batcher S SECONDS R
 //   -> one JSON line: {"mode", "streams", "groups", "seconds", "groups_per_s", "delay_us": {p50, p99},
 //                      "errors", "resident_calls", "resident_inline", "resident_vram"}
 #include <algorithm>
@@ -46,11 +52,34 @@ struct Data {
   }
 };
 
+// GF(2^8), polynomial 0x11D (include/fec_hip.h fec_parity_matrix's field)
+uint8_t gf_mul(uint8_t a, uint8_t b) {
+  uint8_t p = 0;
+  for (; b; b >>= 1) {
+    if (b & 1) p ^= a;
+    a = static_cast<uint8_t>((a << 1) ^ ((a & 0x80) ? 0x1D : 0));
+  }
+  return p;
+}
+
+// Row i of every group of Data: sum over j of M[i][j] * packet j (row 0 = the XOR)
+std::vector<uint8_t> expected_rows(const Data& d, uint32_t r) {
+  std::vector<uint8_t> M(size_t(r) * kK);
+  if (fec_parity_matrix(kK, r, M.data()) != 0) return {};
+  std::vector<uint8_t> rows(size_t(kGroups) * r * kP, 0);
+  for (uint32_t g = 0; g < kGroups; ++g)
+    for (uint32_t i = 0; i < r; ++i)
+      for (uint32_t j = 0; j < kK; ++j)
+        for (uint32_t b = 0; b < kP; ++b)
+          rows[(size_t(g) * r + i) * kP + b] ^= gf_mul(M[size_t(i) * kK + j], d.pk[(size_t(g) * kK + j) * kP + b]);
+  return rows;
+}
+
 void report(const char* mode, int streams, std::vector<double>& us, double seconds, long errors) {
   std::sort(us.begin(), us.end());
   auto pct = [&](double p) { return us.empty() ? 0.0 : us[std::min(us.size() - 1, size_t(p * us.size()))]; };
   FECCoalesceStats cs{};
-  fec_coalesce_stats(&cs, 0);
+  fec_coalesce_stats_sized(&cs, sizeof(cs), 0);
   std::printf("{\"mode\": \"%s\", \"streams\": %d, \"groups\": %zu, \"seconds\": %.3f, \"groups_per_s\": %.1f, "
               "\"delay_us\": {\"p50\": %.2f, \"p99\": %.2f}, \"errors\": %ld, \"resident_calls\": %llu, "
               "\"resident_inline\": %llu, \"resident_vram\": %llu, \"resident_servers\": %llu}\n",
@@ -69,7 +98,7 @@ int raw(int calls) {
   uint32_t offs[kK];
   for (uint32_t j = 0; j < kK; ++j) offs[j] = j * kP;
   FECCoalesceStats cs{};
-  fec_coalesce_stats(&cs, 1);
+  fec_coalesce_stats_sized(&cs, sizeof(cs), 1);
   std::vector<double> us;
   us.reserve(size_t(calls));
   long errors = 0;
@@ -93,7 +122,7 @@ int raw(int calls) {
 int streams(int S, double seconds) {
   const Data d;
   FECCoalesceStats cs{};
-  fec_coalesce_stats(&cs, 1);
+  fec_coalesce_stats_sized(&cs, sizeof(cs), 1);
   std::mutex mu;
   std::vector<double> all;
   std::atomic<long> errors{0};
@@ -127,12 +156,85 @@ int streams(int S, double seconds) {
   return errors ? 1 : 0;
 }
 
+// The opt-in shared batcher: S streams, each a BatchedFECEncoder on one
+// SharedFECBatcher (512-group batches, 1 ms deadline), submitting groups back to back without
+// waiting and collecting repair packets as batches complete (at most 256 groups outstanding per
+// stream).  delay = submit of a group's 10th packet until its rows were collected.
+int batcher(int S, double seconds, int r) {
+  const Data d;
+  const std::vector<uint8_t> want = expected_rows(d, uint32_t(r));
+  constexpr int kMaxGroups = 512;
+  auto sb = SharedFECBatcher::New(kK, r, kP, kMaxGroups, 1000, -1, 8192 / kMaxGroups);
+  if (!sb || want.empty()) {
+    std::printf("{\"mode\": \"batcher\", \"error\": \"no batcher\"}\n");
+    return 2;
+  }
+  std::mutex mu;
+  std::vector<double> all;
+  std::atomic<long> errors{0};
+  const auto t0 = Clock::now();
+  const auto t_end = t0 + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(seconds));
+  std::vector<std::thread> th;
+  for (int s = 0; s < S; ++s)
+    th.emplace_back([&, s] {
+      BatchedFECEncoder be(sb);
+      std::vector<Clock::time_point> sub;  // submit time of each outstanding group, in order
+      std::vector<uint32_t> grp;           // its data group
+      size_t head = 0;
+      std::vector<double> lat;
+      std::vector<Bytes> out;
+      auto drain = [&](int64_t timeout) {
+        out.clear();
+        if (!be.Poll(&out, timeout).ok()) ++errors;
+        const auto now = Clock::now();
+        if (out.size() % size_t(r) != 0) ++errors;
+        for (size_t q = 0; q + size_t(r) <= out.size(); q += size_t(r), ++head) {
+          lat.push_back(std::chrono::duration<double, std::micro>(now - sub[head]).count());
+          for (int i = 0; i < r; ++i) {
+            const Bytes& pkt = out[q + size_t(i)];
+            const size_t hl = i == 0 ? 11u : 14u;  // FE C0 / FE C1 headers (host/fec.cpp MakeRepairPacket)
+            if (pkt.size() != hl + kP ||
+                std::memcmp(pkt.data() + hl, want.data() + (size_t(grp[head]) * r + i) * kP, kP) != 0)
+              ++errors;
+          }
+        }
+      };
+      for (uint64_t i = 0; Clock::now() < t_end; ++i) {
+        const uint32_t g = uint32_t((uint64_t(s) * 7 + i) % kGroups);
+        for (uint32_t j = 0; j < kK; ++j)
+          if (!be.AddPacketAsync(d.pk.data() + (size_t(g) * kK + j) * kP, kP, i * kK + j).ok()) ++errors;
+        sub.push_back(Clock::now());
+        grp.push_back(g);
+        drain(sub.size() - head >= 256 ? 100000 : 0);
+      }
+      if (!be.FlushAsync().ok()) ++errors;
+      drain(-1);
+      if (head != sub.size()) ++errors;
+      std::lock_guard<std::mutex> lk(mu);
+      all.insert(all.end(), lat.begin(), lat.end());
+    });
+  for (auto& t : th) t.join();
+  const double wall = std::chrono::duration<double>(Clock::now() - t0).count();
+  const std::vector<uint64_t> st = sb->Stats();  // groups, batches, full_flushes, deadline_flushes, max_batch
+  std::sort(all.begin(), all.end());
+  auto pct = [&](double p) { return all.empty() ? 0.0 : all[std::min(all.size() - 1, size_t(p * all.size()))]; };
+  std::printf("{\"mode\": \"batcher\", \"streams\": %d, \"r\": %d, \"max_groups\": %d, \"deadline_us\": 1000, "
+              "\"groups\": %zu, \"seconds\": %.3f, \"groups_per_s\": %.1f, \"delay_us\": {\"p50\": %.2f, \"p99\": %.2f}, "
+              "\"errors\": %ld, \"batches\": %llu, \"max_batch\": %llu}\n",
+              S, r, kMaxGroups, all.size(), wall, double(all.size()) / wall, pct(0.5), pct(0.99), errors.load(),
+              (unsigned long long)(st.size() > 1 ? st[1] : 0), (unsigned long long)(st.size() > 4 ? st[4] : 0));
+  std::fflush(stdout);
+  return errors ? 1 : 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "raw";
   if (mode == "raw") return raw(argc > 2 ? std::atoi(argv[2]) : 20000);
   if (mode == "streams") return streams(argc > 2 ? std::atoi(argv[2]) : 16, argc > 3 ? std::atof(argv[3]) : 1.0);
-  std::fprintf(stderr, "usage: call_site raw CALLS | call_site streams S SECONDS\n");
+  if (mode == "batcher")
+    return batcher(argc > 2 ? std::atoi(argv[2]) : 16, argc > 3 ? std::atof(argv[3]) : 1.0, argc > 4 ? std::atoi(argv[4]) : 1);
+  std::fprintf(stderr, "usage: call_site raw CALLS | call_site streams S SECONDS | call_site batcher S SECONDS R\n");
   return 2;
 }

@@ -21,6 +21,9 @@ import numpy as np
 PKG_ROOT = Path(__file__).resolve().parent.parent          # quic-test_amd/
 REPO_ROOT = PKG_ROOT.parent
 LIB_PATH = PKG_ROOT / "lib" / "libfec_hip.so"
+# The same library with the test and tuning switches live (csrc/fec_knobs.hpp): only tests that
+# force a kernel form, a size or a fault load it (tests/conftest.py gpu_ctx_hooks).
+TEST_LIB_PATH = PKG_ROOT / "lib" / "libfec_hip_test.so"
 INCLUDE_DIR = REPO_ROOT / "include"
 
 FEC_OK = 0
@@ -50,7 +53,7 @@ HIP_SYMBOLS = (
     "fec_batcher_wait", "fec_batcher_flush", "fec_batcher_stats", "fec_batcher_last_error",
     "fec_batcher_new_decoder", "fec_batcher_submit_shards", "fec_batcher_wait_rebuilt",
     "fec_batcher_new_multi", "fec_batcher_new_decoder_multi", "fec_batcher_devices",
-    "fec_recover_batch_rs_dev_packed", "fec_coalesce_stats",
+    "fec_recover_batch_rs_dev_packed", "fec_coalesce_stats", "fec_coalesce_stats_sized",
 )
 
 
@@ -61,6 +64,7 @@ class FecError(RuntimeError):
 
 
 _lib: Optional[ctypes.CDLL] = None
+_test_lib: Optional[ctypes.CDLL] = None
 
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 _vp = ctypes.c_void_p
@@ -139,6 +143,7 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
         "fec_batcher_new_decoder_multi": (_vp, [_vp, _int, _u32, _u32, _u32, _u32, _u32, _u32]),
         "fec_batcher_devices": (_int, [_vp]),
         "fec_coalesce_stats": (_int, [_vp, _int]),
+        "fec_coalesce_stats_sized": (_int, [_vp, _sz, _int]),
         "fec_recover_batch_rs_dev_packed": (_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _u32, _u32, _u32, _vp, _vp,
                                                    _vp, _vp, _vp]),
     }
@@ -151,8 +156,16 @@ def load_library(path: Optional[os.PathLike] = None) -> ctypes.CDLL:
     return lib
 
 
-def last_error() -> str:
-    return (load_library().fec_hip_last_error() or b"").decode(errors="replace")
+def load_test_library() -> ctypes.CDLL:
+    """libfec_hip_test.so (tests only): the product's objects with the test switches live."""
+    global _test_lib
+    if _test_lib is None:
+        _test_lib = load_library(TEST_LIB_PATH)
+    return _test_lib
+
+
+def last_error(lib: Optional[ctypes.CDLL] = None) -> str:
+    return ((lib or load_library()).fec_hip_last_error() or b"").decode(errors="replace")
 
 
 def device_count() -> int:
@@ -182,22 +195,24 @@ def _ptr(a) -> int:
     raise TypeError(f"unsupported buffer type {type(a)!r}")
 
 
-def _check(rc: int, what: str) -> None:
+def _check(rc: int, what: str, lib: Optional[ctypes.CDLL] = None) -> None:
     if rc != FEC_OK:
-        raise FecError(what, rc, last_error())
+        raise FecError(what, rc, last_error(lib))
 
 
 class Context:
     """An FECEncoderCtx (one per stream of work / per GPU)."""
 
-    def __init__(self, device: Optional[int] = None, redundancy: float = 0.10, max_groups: int = 1024):
-        self.lib = load_library()
+    def __init__(self, device: Optional[int] = None, redundancy: float = 0.10, max_groups: int = 1024,
+                 lib: Optional[ctypes.CDLL] = None):
+        """lib: the loaded library to bind (default libfec_hip.so; tests pass load_test_library())."""
+        self.lib = lib or load_library()
         if device is None:
             h = self.lib.fec_encoder_new(redundancy, max_groups)
         else:
             h = self.lib.fec_encoder_new_device(redundancy, max_groups, device)
         if not h:
-            raise FecError("fec_encoder_new", FEC_ERR_NODEV, last_error())
+            raise FecError("fec_encoder_new", FEC_ERR_NODEV, last_error(self.lib))
         self.handle = h
 
     def last_error(self) -> str:
@@ -242,7 +257,7 @@ class Context:
         G = num_groups if num_groups is not None else _nbytes(data) // (k * packet_size)
         rc = self.lib.fec_encode_batch_rs(self.handle, _ptr(data), _ptr(offsets) if offsets is not None else None,
                                           G, k, r, packet_size, _ptr(parity_out))
-        _check(rc, "fec_encode_batch_rs")
+        _check(rc, "fec_encode_batch_rs", self.lib)
 
     def decode(self, data, parity, masks, k: int, r: int, packet_size: int, status_out=None,
                num_groups: Optional[int] = None) -> int:
@@ -251,7 +266,7 @@ class Context:
         rc = self.lib.fec_decode_batch_rs(self.handle, _ptr(data), _ptr(parity), _ptr(masks), G, k, r,
                                           packet_size, _ptr(status_out) if status_out is not None else None,
                                           ctypes.byref(bad))
-        _check(rc, "fec_decode_batch_rs")
+        _check(rc, "fec_decode_batch_rs", self.lib)
         return int(bad.value)
 
     # ---- device-resident API ----
@@ -259,14 +274,14 @@ class Context:
                    stream: Optional[int] = None) -> None:
         rc = self.lib.fec_encode_batch_rs_dev(self.handle, _ptr(d_data), num_groups, k, r, packet_size,
                                               _ptr(d_parity), stream)
-        _check(rc, "fec_encode_batch_rs_dev")
+        _check(rc, "fec_encode_batch_rs_dev", self.lib)
 
     def decode_dev(self, d_data, d_parity, d_masks, num_groups: int, k: int, r: int, packet_size: int,
                    d_status=None, stream: Optional[int] = None) -> None:
         rc = self.lib.fec_decode_batch_rs_dev(self.handle, _ptr(d_data), _ptr(d_parity), _ptr(d_masks),
                                               num_groups, k, r, packet_size,
                                               _ptr(d_status) if d_status is not None else None, stream)
-        _check(rc, "fec_decode_batch_rs_dev")
+        _check(rc, "fec_decode_batch_rs_dev", self.lib)
 
     def recover_dev(self, d_data, d_parity, d_masks, num_groups: int, k: int, r: int, packet_size: int,
                     d_rebuilt, d_status=None, stream: Optional[int] = None) -> None:
@@ -275,7 +290,7 @@ class Context:
         rc = self.lib.fec_recover_batch_rs_dev(self.handle, _ptr(d_data), _ptr(d_parity), _ptr(d_masks),
                                                num_groups, k, r, packet_size, _ptr(d_rebuilt),
                                                _ptr(d_status) if d_status is not None else None, stream)
-        _check(rc, "fec_recover_batch_rs_dev")
+        _check(rc, "fec_recover_batch_rs_dev", self.lib)
 
     def recover_packed_dev(self, d_data, d_parity, d_masks, num_groups: int, k: int, r: int, packet_size: int,
                            d_rebuilt, d_row_start, d_total=None, d_status=None, stream: Optional[int] = None) -> None:
@@ -287,29 +302,29 @@ class Context:
                                                       _ptr(d_row_start),
                                                       _ptr(d_total) if d_total is not None else None,
                                                       _ptr(d_status) if d_status is not None else None, stream)
-        _check(rc, "fec_recover_batch_rs_dev_packed")
+        _check(rc, "fec_recover_batch_rs_dev_packed", self.lib)
 
     def decode_prepare(self, k: int, r: int) -> int:
         n = ctypes.c_uint64(0)
-        _check(self.lib.fec_decode_prepare(self.handle, k, r, ctypes.byref(n)), "fec_decode_prepare")
+        _check(self.lib.fec_decode_prepare(self.handle, k, r, ctypes.byref(n)), "fec_decode_prepare", self.lib)
         return int(n.value)
 
     def copy_dev(self, d_src, d_dst, nbytes: int, stream=None) -> None:
         """d_dst <- d_src (box HBM copy calibration; nbytes a multiple of 16)."""
         _check(self.lib.fec_copy_dev(self.handle, _ptr(d_src), _ptr(d_dst), nbytes, stream),
-               "fec_copy_dev")
+               "fec_copy_dev", self.lib)
 
     def fill_random_dev(self, d_dst, nbytes: int, seed: int, byte_offset: int = 0,
                         stream: Optional[int] = None) -> None:
         _check(self.lib.fec_fill_random_dev(self.handle, _ptr(d_dst), nbytes, seed, byte_offset, stream),
-               "fec_fill_random_dev")
+               "fec_fill_random_dev", self.lib)
 
     def decode_loss_hint(self, share: float) -> None:
         """Expected share of groups with lost data in device-resident decodes (< 0: unknown)."""
-        _check(self.lib.fec_decode_loss_hint(self.handle, share), "fec_decode_loss_hint")
+        _check(self.lib.fec_decode_loss_hint(self.handle, share), "fec_decode_loss_hint", self.lib)
 
     def synchronize(self) -> None:
-        _check(self.lib.fec_synchronize(self.handle), "fec_synchronize")
+        _check(self.lib.fec_synchronize(self.handle), "fec_synchronize", self.lib)
 
 
 class DeviceGroup:
@@ -517,5 +532,5 @@ def coalesce_stats(reset: bool = False) -> dict:
     """Process-wide totals of the legacy-call coalescer (fec_coalesce_stats)."""
     lib = load_library()
     st = np.zeros(len(COALESCE_STATS), dtype=np.uint64)
-    _check(lib.fec_coalesce_stats(st.ctypes.data, 1 if reset else 0), "fec_coalesce_stats")
+    _check(lib.fec_coalesce_stats_sized(st.ctypes.data, st.nbytes, 1 if reset else 0), "fec_coalesce_stats_sized")
     return dict(zip(COALESCE_STATS, (int(x) for x in st)))

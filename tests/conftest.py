@@ -66,3 +66,18 @@ def gpu_ctx(quicfec_mod):
     ctx = quicfec_mod.Context(device=0)
     yield ctx
     ctx.close()
+
+
+@pytest.fixture(scope="session")
+def quicfec_hooks(quicfec_mod):
+    """libfec_hip_test.so: the product library's objects with the test and tuning switches live
+    (quic-test_amd/csrc/fec_knobs.hpp).  Only tests that force a kernel form, a size or a fault
+    use it; every other GPU test runs libfec_hip.so, which ignores those switches."""
+    return quicfec_mod.load_test_library()
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_hooks(quicfec_mod, quicfec_hooks):
+    ctx = quicfec_mod.Context(device=0, lib=quicfec_hooks)
+    yield ctx
+    ctx.close()

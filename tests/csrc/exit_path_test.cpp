@@ -105,7 +105,7 @@ void report() {
 // The library's counters into the report.
 void take_stats() {
   FECCoalesceStats st{};
-  fec_coalesce_stats(&st, 0);
+  fec_coalesce_stats_sized(&st, sizeof(st), 0);
   g_resident_calls = st.resident_calls;
   g_resident_inline = st.resident_inline;
   g_resident_vram = st.resident_vram;

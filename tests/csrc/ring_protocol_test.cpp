@@ -13,7 +13,15 @@
 //  3. serving classes: with per-class seq counters (class c takes c, c + K, c + 2K, ...; the host's
 //     choice by calls in flight) every class's seqs map to slots of that class only
 //     (seq % kServerSlots), and a slot's previous occupant is always seq - kServerSlots;
-//  4. layout: the structures' sizes the host, the device and the inline data area assume.
+//  4. layout: the structures' sizes the host, the device and the inline data area assume;
+//  5. leaving as a whole: the workgroups of one instance share idle flags, a leave
+//     word and an exit count (ServerCoord, server_all_idle / server_exits_next / server_exits_last)
+//     -- modelled over thousands of instances with random interleavings, workgroups dispatched
+//     late (after another one set the leave word), the host's stop word and the previous
+//     instance's words left in place: every workgroup leaves within its next coordination read
+//     once the leave word is set, none leaves on an earlier instance's words, and exactly one
+//     workgroup per instance -- the last to count out -- stores exited = gen.  Controls with the
+//     generation checks removed must fail.
 // Prints "OK <checks>" or the first violation.
 #include <algorithm>
 #include <cstdint>
@@ -147,6 +155,115 @@ static void layout() {
   CHECK(kServerPoll * 16 / 2 + 2 + kServerMaxClasses / 2 <= 1024, "the poll's lanes fit the workgroup");
 }
 
+// 5. The coordination words, modelled.  One instance = K workgroups; a step runs one poll of one
+// workgroup (its reads and stores of the shared words are the kernel's, each atomic) or one
+// step of its exit count (the load, then CAS attempts).  Returns the violations found; with
+// `control` != 0 the model runs a broken rule (1: the leave word read without its generation,
+// 2: the exit count without the generation reset) and must find violations.
+struct CoordModel {
+  uint64_t leave = 0, exits = 0, idle[kServerMaxClasses] = {}, exited = 0;
+};
+
+static long coordination(int control, long* instances_out) {
+  constexpr uint32_t kEvery = 8;    // the kernel reads the shared words every 8th poll (kCoordEvery + 1)
+  constexpr uint32_t kMaxPolls = 4000;
+  long violations = 0, instances = 0;
+  std::mt19937_64 rng(0xC0DEu + control);
+  for (uint32_t K : {2u, 4u, 8u}) {
+    CoordModel m;  // a Resident's coordination words start zeroed (fec_coalesce.cpp hipMemsetAsync)
+    for (uint64_t gen = 1; gen <= 1500; ++gen, ++instances) {
+      // the host relaunches only once the previous instance's exited word is its generation
+      if (m.exited != gen - 1) {
+        ++violations;
+        m.exited = gen - 1;
+      }
+      struct Wg {
+        bool started = false, leaving = false, counted = false;
+        uint32_t it = 0, t_last = 0, polls_after_leave = 0;
+        bool told = false, was_idle = false;
+        uint64_t idle_seen[kServerMaxClasses] = {};
+        uint64_t v = 0;
+        bool have_v = false;
+      };
+      std::vector<Wg> wg(K);
+      // work per class: busy for a random number of polls (some classes none at all)
+      std::vector<uint32_t> busy_until(K);
+      for (auto& b : busy_until) b = static_cast<uint32_t>(rng() % 3 == 0 ? 0 : rng() % 200);
+      const uint32_t idle_polls = 5 + static_cast<uint32_t>(rng() % 40);
+      const uint32_t life_polls = rng() % 4 == 0 ? 30 + static_cast<uint32_t>(rng() % 200) : kMaxPolls;
+      const bool host_stop = rng() % 8 == 0;
+      const uint64_t stop_at_step = rng() % 3000;
+      bool any_legit = false;   // a workgroup of this instance had a reason of its own to leave
+      uint32_t exited_stores = 0, counted = 0;
+      int last_counter = -1;
+      uint64_t step = 0;
+      for (; counted < K && step < 2000000; ++step) {
+        const uint32_t c = static_cast<uint32_t>(rng() % K);
+        Wg& w = wg[c];
+        if (w.counted) continue;
+        if (!w.started) {  // dispatched late: often long after the others
+          if (rng() % 64 != 0) continue;
+          w.started = true;
+        }
+        if (!w.leaving) {
+          if (w.it % kEvery == 0) {
+            w.told = control == 1 ? m.leave != 0 : m.leave == gen;
+            for (uint32_t q = 0; q < K; ++q) w.idle_seen[q] = m.idle[q];
+          }
+          if (m.leave == gen) ++w.polls_after_leave;
+          const bool work = w.it < busy_until[c];
+          if (work) w.t_last = w.it;
+          const bool idle = !work && w.it - w.t_last > idle_polls;
+          const bool stop = host_stop && step >= stop_at_step;
+          const bool own = stop || w.it > life_polls || w.it + 1 == kMaxPolls;
+          const bool all_idle = server_all_idle(idle, w.idle_seen, K, c, gen);
+          if (idle != w.was_idle) {
+            m.idle[c] = idle ? gen : 0;
+            w.was_idle = idle;
+          }
+          if (own || all_idle) any_legit = true;
+          if ((own || all_idle) && !w.told) m.leave = gen;
+          if (w.told && !any_legit) ++violations;  // left on an earlier instance's word
+          w.leaving = own || all_idle || w.told;
+          ++w.it;
+          continue;
+        }
+        // counting out: the load, then CAS attempts (another workgroup may get in between)
+        if (!w.have_v) {
+          w.v = m.exits;
+          w.have_v = true;
+          continue;
+        }
+        const uint64_t nv = control == 2 ? w.v + 1 : server_exits_next(w.v, gen);
+        if (m.exits != w.v) {
+          w.v = m.exits;
+          continue;
+        }
+        m.exits = nv;
+        w.counted = true;
+        ++counted;
+        if (server_exits_last(nv, K)) {
+          m.exited = gen;
+          ++exited_stores;
+          last_counter = static_cast<int>(c);
+        }
+      }
+      if (counted != K) ++violations;           // a workgroup never left
+      if (exited_stores != 1) ++violations;      // nobody, or more than one, stored exited
+      if (last_counter >= 0) {
+        for (uint32_t q = 0; q < K; ++q)
+          if (static_cast<int>(q) != last_counter && !wg[q].counted) ++violations;
+      }
+      // once the leave word is this instance's, each workgroup leaves within one coordination read
+      for (uint32_t q = 0; q < K; ++q)
+        if (wg[q].polls_after_leave > kEvery + 1) ++violations;
+      if (m.exited != gen) m.exited = gen;  // keep the next instance's precondition for the controls
+    }
+  }
+  *instances_out = instances;
+  return violations;
+}
+
 int main() {
   tags();
   const long with_scrub = stale_acceptances(true), without = stale_acceptances(false);
@@ -154,6 +271,11 @@ int main() {
   CHECK(without > 0, "the control (no scrub) found no stale acceptance: the model has no teeth");
   classes();
   layout();
+  long instances = 0;
+  const long bad = coordination(0, &instances);
+  CHECK(bad == 0, "%ld coordination violations over %ld instances", bad, instances);
+  CHECK(coordination(1, &instances) > 0, "control 1 (leave word without generation) found nothing");
+  CHECK(coordination(2, &instances) > 0, "control 2 (exit count without generation reset) found nothing");
   std::printf("OK %ld\n", g_checks);
   return 0;
 }

@@ -49,6 +49,61 @@ def test_library_exports_every_declared_symbol(quicfec_mod):
     assert set(quicfec_mod.REFERENCE_SYMBOLS) | set(quicfec_mod.HIP_SYMBOLS) <= exported
 
 
+# The product library's only environment switches (INTEGRATION.md §6 lists them with defaults);
+# the test and tuning switches (csrc/fec_knobs.hpp) exist in libfec_hip_test.so alone.
+PRODUCT_KNOBS = {
+    "QUICFEC_BATCHER_BLOCKING_SYNC", "QUICFEC_COALESCE", "QUICFEC_COALESCE_INFLIGHT", "QUICFEC_COALESCE_MAX_GROUPS",
+    "QUICFEC_HOST_THREADS", "QUICFEC_NO_WARMUP", "QUICFEC_PIPE_CHUNK_BYTES", "QUICFEC_RESIDENT",
+    "QUICFEC_RESIDENT_DEADLINE_MS", "QUICFEC_RESIDENT_IDLE_US", "QUICFEC_RESIDENT_LIFE_US", "QUICFEC_RESIDENT_SERVERS",
+    "QUICFEC_RESIDENT_VRAM", "QUICFEC_SMALL_CALL_BYTES",
+}
+
+
+def _knob_names(path):
+    data = Path(path).read_bytes()
+    return {m.decode() for m in re.findall(rb"QUICFEC_[A-Z0-9_]+", data)}
+
+
+def test_product_library_has_no_test_switches(quicfec_mod):
+    """no fault-injection hook and no tuning switch in libfec_hip.so -- its
+    environment names are exactly the operational ones; the test library holds the rest (and
+    exports the same C-ABI)."""
+    prod = _knob_names(quicfec_mod.LIB_PATH)
+    assert prod == PRODUCT_KNOBS, sorted(prod ^ PRODUCT_KNOBS)
+    assert not any("TEST" in n for n in prod)
+    test = _knob_names(quicfec_mod.TEST_LIB_PATH)
+    assert PRODUCT_KNOBS < test
+    assert {"QUICFEC_RESIDENT_TEST_FAIL_AT", "QUICFEC_RESIDENT_TEST_TEAR", "QUICFEC_MAX_WAVE_BLOCKS",
+            "QUICFEC_ENCODE_BITS", "QUICFEC_PACKED_RUNS"} <= test
+    syms = []
+    for lib in (quicfec_mod.LIB_PATH, quicfec_mod.TEST_LIB_PATH):
+        out = subprocess.run(["nm", "-D", "--defined-only", str(lib)], capture_output=True, text=True,
+                             check=True).stdout
+        syms.append({ln.split()[-1] for ln in out.splitlines() if " T " in ln})
+    assert syms[0] == syms[1]
+
+
+def test_coalesce_stats_write_only_the_callers_struct(quicfec_mod):
+    """FECCoalesceStats grew in round 5.  fec_coalesce_stats writes the 15
+    words it was published with; fec_coalesce_stats_sized writes min(caller's size, this build's)
+    and refuses a size below the first layout.  Guard words past the caller's struct stay put."""
+    lib = quicfec_mod.load_library()
+    n = len(quicfec_mod.COALESCE_STATS)
+    guard = np.uint64(0xA5A5A5A5A5A5A5A5)
+    for words, fn in ((15, "old"), (16, "sized"), (n, "sized"), (n + 4, "sized")):
+        buf = np.full(n + 8, guard, dtype=np.uint64)
+        rc = lib.fec_coalesce_stats(buf.ctypes.data, 0) if fn == "old" else \
+            lib.fec_coalesce_stats_sized(buf.ctypes.data, words * 8, 0)
+        assert rc == 0
+        written = min(words, n)
+        assert (buf[written:] == guard).all(), (fn, words)
+        assert not (buf[:written] == guard).any(), (fn, words)   # every field of the caller's struct set
+    buf = np.full(16, guard, dtype=np.uint64)
+    assert lib.fec_coalesce_stats_sized(buf.ctypes.data, 14 * 8, 0) == quicfec_mod.FEC_ERR_RANGE
+    assert (buf == guard).all()
+    assert lib.fec_coalesce_stats_sized(None, 200, 0) == quicfec_mod.FEC_ERR_NULL
+
+
 def test_library_is_built_from_this_tree(quicfec_mod):
     """The loaded libfec_hip.so embeds the hash of the sources it was built from
     (quic-test_amd/csrc/src_hash.py, compiled in by the Makefile); it must equal the hash of the
@@ -162,7 +217,10 @@ def test_resident_ring_protocol_model(tmp_path):
     coordination layouts): tags unique within an epoch and never 0, no stale 8-B word accepted
     over 40 epochs of torn, partly rewritten laps with the epoch scrub (and a stale acceptance
     without it, the control), serving classes' seqs confined to their own slots with the
-    previous occupant seq - 1024 (tests/csrc/ring_protocol_test.cpp)."""
+    previous occupant seq - 1024, and the classes' shared idle / leave / exit-count words over
+    4,500 modelled instances with random interleavings and late-dispatched workgroups: all leave
+    together, none on an earlier instance's words, exactly one stores exited (ADVICE r05;
+    controls without the generation checks must fail) (tests/csrc/ring_protocol_test.cpp)."""
     exe = tmp_path / "ring_protocol_test"
     subprocess.run(["g++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
                     "-I", str(REPO / "quic-test_amd" / "csrc"), str(REPO / "tests" / "csrc" / "ring_protocol_test.cpp"),
@@ -239,7 +297,8 @@ def test_bench_call_site_without_tool_is_skipped(monkeypatch, tmp_path):
 
 
 def test_bench_call_site_reads_the_tool_lines(monkeypatch, tmp_path):
-    """bench.py's call_site section runs the tool once per leg (raw, 1 and 16 streams) and keeps
+    """bench.py's call_site section runs the tool once per leg (raw, 1 and 16 streams, the shared
+    batcher at r = 1 and 3) and keeps
     each leg's rate, delay percentiles, error count and ring kind from its last JSON line."""
     import importlib.util
     import stat
@@ -254,7 +313,12 @@ def test_bench_call_site_reads_the_tool_lines(monkeypatch, tmp_path):
     tool.chmod(tool.stat().st_mode | stat.S_IEXEC)
     monkeypatch.setattr(bench, "CALL_SITE_TOOL", tool)
     out = bench.call_site(seconds=0.1)
-    assert set(out) >= {"raw", "streams_1", "streams_16", "reference_call"}
-    for leg in ("raw", "streams_1", "streams_16"):
+    assert set(out) >= {"raw", "streams_1", "streams_16", "batcher_16_r1", "batcher_16_r3", "reference_call"}
+    for leg in ("raw", "streams_1", "streams_16", "batcher_16_r1", "batcher_16_r3"):
         assert out[leg] == {"groups_per_s": 1000.0, "delay_us": {"p50": 5.5, "p99": 9.0}, "errors": 0,
                             "resident_inline": 7, "resident_vram": 1}
+    # beside the reference library on one core (cpu_baseline's ref_encode_batch_1t_GiBps)
+    gib = 1000.0 * 12000 / 2**30
+    out = bench.call_site(ref_1t_GiBps=2 * gib, seconds=0.1)
+    assert out["ref_encode_batch_1t_groups_per_s"] == 2000.0
+    assert out["batcher_16_r3"]["vs_ref_1t"] == 0.5

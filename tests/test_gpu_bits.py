@@ -3,8 +3,9 @@ code's coefficients compiled into XOR networks over bit planes.  It must write e
 bytes of the table form (encode_v16) and of the oracle's restatement (oracle/fec_oracle.c
 rs_encode) for every packet size (P from 16 up, the last column shifted back), odd group
 counts (a lane's second group past the end), tiles and multi-chunk launches.  Device-contiguous
-packets only.  QUICFEC_ENCODE_BITS: 1 forces it for every instantiated shape, 0 the
-tables; the default takes it for r >= 4."""
+packets only.  QUICFEC_ENCODE_BITS (a switch of the test library, libfec_hip_test.so, which
+these tests load through gpu_ctx_hooks): 1 forces it for every instantiated shape, 0 the
+tables; the product library takes it for r >= 4 (test_bits_is_the_default_for_c4)."""
 import numpy as np
 import pytest
 
@@ -27,7 +28,8 @@ def _encode(ctx, torch, data, G, k, r, P):
 
 @pytest.mark.parametrize("k,r", [(20, 5), (10, 3)])
 @pytest.mark.parametrize("P", SIZES)
-def test_bits_equals_oracle_and_tables(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, k, r, P):
+def test_bits_equals_oracle_and_tables(gpu_ctx_hooks, oracle_mod, torch_cuda, monkeypatch, k, r, P):
+    gpu_ctx = gpu_ctx_hooks
     G = 53
     data = oracle_mod.splitmix_bytes(G * k * P, 0xB175 + 131 * P + k)
     exp = oracle_mod.rs_encode(data, G, k, r, P)
@@ -39,19 +41,20 @@ def test_bits_equals_oracle_and_tables(gpu_ctx, oracle_mod, torch_cuda, monkeypa
     assert np.array_equal(tabs, exp.reshape(-1))
 
 
-@pytest.mark.parametrize("window", ["4", "8"])
+@pytest.mark.parametrize("stage", ["0", "1"])
 @pytest.mark.parametrize("tile", ["0", "1", "3"])
-def test_bits_tiles_and_chunks(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, tile, window):
-    """Groups per workgroup (QUICFEC_ENCODE_TILE), packets in flight per lane
-    (QUICFEC_ENCODE_BITS_WINDOW) and launches split into chunks of QUICFEC_MAX_WAVE_BLOCKS
+def test_bits_tiles_and_chunks(gpu_ctx_hooks, oracle_mod, torch_cuda, monkeypatch, tile, stage):
+    """Groups per workgroup (QUICFEC_ENCODE_TILE), rows staged or stored directly
+    (QUICFEC_ENCODE_STAGE) and launches split into chunks of QUICFEC_MAX_WAVE_BLOCKS
     workgroups: every group's rows land at their global place."""
+    gpu_ctx = gpu_ctx_hooks
     k, r, P, G = 20, 5, 1200, 1_001
     monkeypatch.setenv("QUICFEC_ENCODE_BITS", "1")
-    monkeypatch.setenv("QUICFEC_ENCODE_BITS_WINDOW", window)
+    monkeypatch.setenv("QUICFEC_ENCODE_STAGE", stage)
     if tile != "0":
         monkeypatch.setenv("QUICFEC_ENCODE_TILE", tile)
     monkeypatch.setenv("QUICFEC_MAX_WAVE_BLOCKS", "37")
-    data = oracle_mod.splitmix_bytes(G * k * P, 0xC4C4 + int(tile))
+    data = oracle_mod.splitmix_bytes(G * k * P, 0xC4C4 + int(tile) + 7 * int(stage))
     got = _encode(gpu_ctx, torch_cuda, data, G, k, r, P)
     assert np.array_equal(got, oracle_mod.rs_encode(data, G, k, r, P, nthreads=8).reshape(-1))
 
@@ -72,12 +75,13 @@ def test_bits_is_the_default_for_c4(gpu_ctx, oracle_mod, torch_cuda, monkeypatch
 @pytest.mark.parametrize("k,r", [(10, 3), (20, 5)])
 @pytest.mark.parametrize("P,G", [(1200, 1), (1200, 3), (1200, 4), (1200, 9), (1200, 1_001), (1024, 77), (64, 301),
                                  (1216, 50), (1500, 33), (1201, 21)])
-def test_staged_rows_equal_oracle(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, form, k, r, P, G):
+def test_staged_rows_equal_oracle(gpu_ctx_hooks, oracle_mod, torch_cuda, monkeypatch, form, k, r, P, G):
     """QUICFEC_ENCODE_STAGE=1 (kStageRows): the workgroup's parity rows go
     through LDS and leave as one run of whole 16-B pieces.  Exact for partial last tiles (G not
     a multiple of the tile, a lane's second group past the end), small and large tiles, packet
     sizes that are not a multiple of 16 (the staged form then stands aside), and chunked
     launches, at an odd parity address; the bytes outside the parity are untouched (guard bytes)."""
+    gpu_ctx = gpu_ctx_hooks
     monkeypatch.setenv("QUICFEC_ENCODE_STAGE", "1")
     monkeypatch.setenv("QUICFEC_ENCODE_BITS", "1" if form == "bits" else "0")
     monkeypatch.setenv("QUICFEC_MAX_WAVE_BLOCKS", "37")

@@ -368,13 +368,22 @@ lib.fec_encoder_free(ctx)
     assert first_us < 5000, f"first legacy call took {first_us:.0f} us"
 
 
-def _exit_path_run(mode, calls=300, servers=None):
+# modes that inject faults (tests/csrc/exit_path_test.cpp): they run the program linked against
+# the test library (libfec_hip_test.so, csrc/fec_knobs.hpp), the others the product library
+_HOOK_MODES = ("nolaunch", "tear", "epoch", "epoch_hostring", "poison_mt")
+
+
+def _exit_path_run(mode, calls=300, servers=None, product=None):
+    """product: run the program linked against libfec_hip.so (default: unless the mode injects faults)."""
     import json
     import os
     import subprocess
     from pathlib import Path
-    exe = Path(__file__).resolve().parents[1] / "quic-test_amd" / "lib" / "exit_path_test"
-    assert exe.exists(), "build() makes quic-test_amd/lib/exit_path_test (csrc Makefile target tests)"
+    if product is None:
+        product = mode not in _HOOK_MODES
+    name = "exit_path_test" if product else "exit_path_test_hooks"
+    exe = Path(__file__).resolve().parents[1] / "quic-test_amd" / "lib" / name
+    assert exe.exists(), f"build() makes quic-test_amd/lib/{name} (csrc Makefile target tests)"
     env = dict(os.environ)
     if servers is not None:
         env["QUICFEC_RESIDENT_SERVERS"] = str(servers)
@@ -500,6 +509,17 @@ def test_resident_relaunch_cycles_under_concurrent_calls():
     assert rec["repairs_ok"] is True and rec["calls"] == 2_000, rec
     assert rec["calls_after_exit"] == 0, rec["names"]
     assert rec["resident_calls"] == 2_000 and rec["resident_launches"] > 5, rec
+
+
+def test_product_library_ignores_fault_injection():
+    """The fault-injection switches exist only in the test library: the same poisoning run
+    (QUICFEC_RESIDENT_TEST_FAIL_AT=600, which the program sets) against libfec_hip.so serves
+    every one of the 2,400 calls on the resident encoder -- nothing fails, nothing is poisoned."""
+    rec = _exit_path_run("poison_mt", calls=2_400, product=True)
+    if "skip" in rec:
+        pytest.skip(rec["skip"])
+    assert rec["repairs_ok"] is True and rec["calls"] == 2_400, rec
+    assert rec["resident_calls"] == 2_400, rec
 
 
 # (mode, calls) of the runs above, repeated with several serving workgroups per resident instance

@@ -151,11 +151,12 @@ def test_random_batchers(quicfec_mod, oracle_mod, block):
 
 
 @pytest.mark.parametrize("block", range(PACKED_BLOCKS))
-def test_random_packed_recover(gpu_ctx, oracle_mod, torch_cuda, block):
+def test_random_packed_recover(gpu_ctx_hooks, oracle_mod, torch_cuda, block):
     """The packed recover with random mask-addressed shapes, sizes and loss rates, through both
     of its forms chosen at random per call (the one-launch recover_runs and the prefix launches +
-    decode_fused), one context, calls of different shapes interleaved: rows, row starts, total and
-    statuses against the oracle."""
+    decode_fused; QUICFEC_PACKED_RUNS is a test-library switch), one context, calls of different
+    shapes interleaved: rows, row starts, total and statuses against the oracle."""
+    gpu_ctx = gpu_ctx_hooks
     torch = torch_cuda
     rng = np.random.default_rng(SEED + 200 + block)
     shapes = [(10, 3), (10, 2), (10, 1), (4, 2)]

@@ -66,10 +66,13 @@ def test_packed_rows_match_oracle(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
 @pytest.mark.parametrize("loss,G,scan,direct", [(0.01, 50_000, "8", None), (0.3, 20_011, "8", None),
                                                 (0.05, 30_000, None, None), (0.05, 30_001, None, "4"),
                                                 (0.3, 9_000, "8", "1")])
-def test_packed_rows_sparse_and_many_blocks(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, loss, G, scan, direct):
+def test_packed_rows_sparse_and_many_blocks(gpu_ctx, gpu_ctx_hooks, oracle_mod, torch_cuda, monkeypatch, loss, G,
+                                            scan, direct):
     """iid loss (the scan form when QUICFEC_DECODE_SCAN=8), row starts across many prefix
     blocks of 1024 groups, in the two-launch form and (QUICFEC_ROWS_DIRECT_BLOCKS below the
-    block count) the one with a separate scan of the block sums."""
+    block count) the one with a separate scan of the block sums.  The switches are the test
+    library's (gpu_ctx_hooks); unswitched cases run the product library."""
+    ctx = gpu_ctx_hooks if (scan or direct) else gpu_ctx
     if scan:
         monkeypatch.setenv("QUICFEC_DECODE_SCAN", scan)
     if direct:
@@ -79,7 +82,7 @@ def test_packed_rows_sparse_and_many_blocks(gpu_ctx, oracle_mod, torch_cuda, mon
     w = np.left_shift(np.uint64(1), np.arange(k + r, dtype=np.uint64))
     masks = ((rng.random((G, k + r)) < loss) * w).sum(axis=1, dtype=np.uint64)
     broken, par, st_exp, start, exp = _case(oracle_mod, k, r, P, G, masks)
-    dd, out, rs, tot, st = _run(gpu_ctx, torch_cuda, broken, par, masks, G, k, r, P)
+    dd, out, rs, tot, st = _run(ctx, torch_cuda, broken, par, masks, G, k, r, P)
     n = len(exp)
     assert int(tot.item()) == n
     assert np.array_equal(rs.cpu().numpy().view(np.uint32), start)
@@ -138,10 +141,11 @@ def test_packed_masks_at_odd_word(gpu_ctx, oracle_mod, torch_cuda):
 
 @pytest.mark.parametrize("api", ["packed", "packed_scan", "slots", "in_place"])
 @pytest.mark.parametrize("k,r,P", [(10, 3, 1200), (10, 2, 700), (20, 5, 1200)])
-def test_chunked_launches(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, api, k, r, P):
+def test_chunked_launches(gpu_ctx_hooks, oracle_mod, torch_cuda, monkeypatch, api, k, r, P):
     """Launches split into chunks of QUICFEC_MAX_WAVE_BLOCKS workgroups (otherwise only past
-    16.7M groups): packed rows keep their global row starts in every chunk, and the forms that
-    take no record offsets get none in later chunks."""
+    16.7M groups; a test-library switch): packed rows keep their global row starts in every
+    chunk, and the forms that take no record offsets get none in later chunks."""
+    gpu_ctx = gpu_ctx_hooks
     if k == 20 and api.startswith("packed"):
         pytest.skip("no packed form for the record-addressed shape")
     monkeypatch.setenv("QUICFEC_MAX_WAVE_BLOCKS", "7")
@@ -280,17 +284,16 @@ def _check_packed(gpu_ctx, torch, oracle_mod, k, r, P, G, masks, out_offset=0):
 @pytest.mark.parametrize("k,r,P", [(10, 3, 1200), (10, 3, 700), (10, 3, 1400), (10, 3, 2000), (10, 3, 300),
                                    (10, 3, 1024), (10, 3, 1040), (10, 3, 1201), (10, 1, 1200), (10, 2, 1200),
                                    (10, 2, 700), (4, 2, 513), (4, 2, 1200)])
-@pytest.mark.parametrize("stage", ["default", "0", "16384", "65536", "plain"])
-def test_packed_runs_one_launch(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, k, r, P, stage):
+@pytest.mark.parametrize("stage", ["default", "0", "16384", "65536"])
+def test_packed_runs_one_launch(gpu_ctx_hooks, oracle_mod, torch_cuda, monkeypatch, k, r, P, stage):
     """The one-launch packed recover (recover_runs: decoupled look-back row starts, rows staged
     per workgroup in an LDS image and written as one run) on every mask-addressed piece layout,
     forced for mixed loss (QUICFEC_PACKED_RUNS=1), with the image off, small (most rows past it go
-    straight to HBM), the default 48 KB and 64 KB, and with plain row stores
-    (QUICFEC_RUNS_NT_STORE=0); bit-exact against the oracle."""
+    straight to HBM), the default 48 KB and 64 KB (test-library switches); bit-exact against the
+    oracle."""
+    gpu_ctx = gpu_ctx_hooks
     monkeypatch.setenv("QUICFEC_PACKED_RUNS", "1")
-    if stage == "plain":
-        monkeypatch.setenv("QUICFEC_RUNS_NT_STORE", "0")
-    elif stage != "default":
+    if stage != "default":
         monkeypatch.setenv("QUICFEC_RUNS_STAGE", stage)
     G = 3_001
     rng = np.random.default_rng(k * 1000 + r * 100 + P + len(stage))
@@ -302,12 +305,14 @@ def test_packed_runs_one_launch(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, k,
 
 
 @pytest.mark.parametrize("case", ["chunks", "odd_output", "sparse_hint", "tiny", "one_group_per_tile"])
-def test_packed_runs_edges(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, case):
+def test_packed_runs_edges(gpu_ctx, gpu_ctx_hooks, oracle_mod, torch_cuda, monkeypatch, case):
     """recover_runs edges: chunked launches (QUICFEC_MAX_WAVE_BLOCKS=2, each chunk's rows start
     after the previous chunk's total), an output at an odd address (no LDS image: rows straight
-    to HBM), the library's own choice from the loss hint, calls of 1-7 groups, and tiles where a
-    single group rebuilds."""
+    to HBM), the library's own choice from the loss hint (the product library), calls of 1-7
+    groups, and tiles where a single group rebuilds."""
     torch = torch_cuda
+    if case != "sparse_hint":
+        gpu_ctx = gpu_ctx_hooks  # QUICFEC_PACKED_RUNS / QUICFEC_MAX_WAVE_BLOCKS: test-library switches
     k, r, P = 10, 3, 1200
     rng = np.random.default_rng(hash(case) & 0xFFFF)
     off = 0
@@ -341,10 +346,11 @@ def test_packed_runs_edges(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, case):
         gpu_ctx.decode_loss_hint(-1.0)
 
 
-def test_packed_runs_back_to_back(gpu_ctx, oracle_mod, torch_cuda, monkeypatch):
+def test_packed_runs_back_to_back(gpu_ctx_hooks, oracle_mod, torch_cuda, monkeypatch):
     """Several one-launch packed recovers queued on one stream without a synchronise between
     them, growing and shrinking: every launch takes fresh look-back epochs (words left by the
     earlier launches never match) and the workspace grows under queued work."""
+    gpu_ctx = gpu_ctx_hooks
     monkeypatch.setenv("QUICFEC_PACKED_RUNS", "1")
     torch = torch_cuda
     k, r, P = 10, 3, 700

@@ -609,10 +609,11 @@ def test_ctx_last_error_set_on_failure(gpu_ctx, quicfec_mod):
 
 
 @pytest.mark.parametrize("loss,P", [(0.01, 1200), (0.2, 1200), (0.01, 700), (0.05, 1400)])
-def test_device_decode_scan_form(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, loss, P):
+def test_device_decode_scan_form(gpu_ctx_hooks, oracle_mod, torch_cuda, monkeypatch, loss, P):
     """The mask-addressed decode with 8 groups per wave (DecodeLaunch::scan; host paths pick
     it for sparse loss, QUICFEC_DECODE_SCAN forces it here): statuses of every group and the
     rebuilt bytes equal the oracle's, with unrecoverable groups and a partial last wave."""
+    gpu_ctx = gpu_ctx_hooks  # QUICFEC_DECODE_SCAN: a test-library switch
     monkeypatch.setenv("QUICFEC_DECODE_SCAN", "8")
     torch = torch_cuda
     k, r, G = 10, 3, 20_011
@@ -675,9 +676,10 @@ def test_recover_compact_output(gpu_ctx, oracle_mod, torch_cuda, k, r, P):
 
 
 @pytest.mark.parametrize("loss,P", [(0.01, 1200), (0.3, 1400)])
-def test_recover_scan_form(gpu_ctx, oracle_mod, torch_cuda, monkeypatch, loss, P):
+def test_recover_scan_form(gpu_ctx_hooks, oracle_mod, torch_cuda, monkeypatch, loss, P):
     """fec_recover_batch_rs_dev in the 8-groups-per-wave form (sparse loss): compact rows
     and statuses equal the oracle's."""
+    gpu_ctx = gpu_ctx_hooks  # QUICFEC_DECODE_SCAN: a test-library switch
     monkeypatch.setenv("QUICFEC_DECODE_SCAN", "8")
     torch = torch_cuda
     k, r, G = 10, 3, 10_007
