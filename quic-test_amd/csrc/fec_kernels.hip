@@ -2129,7 +2129,7 @@ __global__ __launch_bounds__(kServerThreads) void legacy_server(ServerSlot* __re
         // All ten packet loads in flight at once, as global (address space 1) loads: the addresses
         // come from integers, so plain pointers compile to flat loads, which count on lgkmcnt too
         // and were issued two at a time with a full wait between pairs -- five dependent PCIe
-        // round trips, ~8 us of a ~12-us call (the server's stamps).
+        // round trips, ~8 us of a ~12-us call (the server's stamps, DESIGN_HISTORY.md §8c round 4).
         u32x4 v[kServerPackets];
 #pragma unroll
         for (uint32_t j = 0; j < kServerPackets; ++j)

@@ -139,7 +139,7 @@ struct RunsLaunch {
   uint32_t epoch;
   int stage_bytes = -1;      // LDS run image: -1 tuned default (test switch kRunsStage), 0 none
 };
-// LDS run image per workgroup of 512 groups (tools/probe_runs.hip): C5's
+// LDS run image per workgroup of 512 groups (tools/probe_runs.hip; DESIGN_HISTORY.md §5 round 4): C5's
 // ~59 rows per tile fit 48 KB (40 rows) mostly; two workgroups per CU.
 // recover_runs' run image per workgroup.
 constexpr int kRunsStageBytes = 48 * 1024;

@@ -213,51 +213,7 @@ int main(int argc, char** argv) {
       std::printf("{\"kind\": \"contiguous\", \"error\": \"alloc\"}\n");
     }
   }
-  // 3. virtual-memory buffers: the same physical handles in three virtual orders
-  const size_t nchunks = (par_bytes + chunk - 1) / chunk;
-  std::vector<size_t> ident(nchunks), rev(nchunks), shuf(nchunks);
-  std::iota(ident.begin(), ident.end(), 0);
-  std::reverse_copy(ident.begin(), ident.end(), rev.begin());
-  shuf = ident;
-  std::shuffle(shuf.begin(), shuf.end(), std::mt19937_64(0xC3C3));
-  for (int pass = 0; pass < 2; ++pass) {
-    const char* names[3] = {"vmm_in_order", "vmm_reversed", "vmm_shuffled"};
-    const std::vector<size_t>* perms[3] = {&ident, &rev, &shuf};
-    for (int v = 0; v < 3; ++v) {
-      VmmBuffer b;
-      if (!b.create(par_bytes, chunk, *perms[v], dev)) {
-        std::printf("{\"kind\": \"%s\", \"error\": \"%s\"}\n", names[v], b.failed);
-        b.destroy();
-        continue;
-      }
-      out(names[v], timed(data, static_cast<uint8_t*>(b.va)), b.va, (",\"pass\": " + std::to_string(pass)).c_str());
-      b.destroy();
-    }
-  }
-  // 4. the first (slow?) plain buffer again, then the data copied into shuffled chunks
-  out("hipMalloc_again", timed(data, plain[0]), plain[0], ",\"order\": 0");
-  if (data_vmm) {  // (aborted inside the runtime on three boxes with 64-MB handles: opt-in)
-    const size_t dchunk = std::max<size_t>(chunk, 64u << 20);  // fewer handles for 12 GB
-    std::vector<size_t> dperm((data_bytes + dchunk - 1) / dchunk);
-    std::iota(dperm.begin(), dperm.end(), 0);
-    std::shuffle(dperm.begin(), dperm.end(), std::mt19937_64(0xDA7A));
-    VmmBuffer d2;
-    if (d2.create(data_bytes, dchunk, dperm, dev)) {
-      // a kernel copy: the runtime's memcpy does not know virtual-memory ranges
-      if (fec_copy_dev(ctx, data, static_cast<uint8_t*>(d2.va), data_bytes, st) != 0) {
-        std::printf("{\"error\": \"copy: %s\"}\n", fec_hip_last_error());
-        return 1;
-      }
-      HIPCHK(hipStreamSynchronize(st));
-      for (int i = 0; i < 3; ++i)
-        out("data_shuffled", timed(static_cast<uint8_t*>(d2.va), plain[i]), plain[i],
-            (",\"order\": " + std::to_string(i)).c_str());
-    } else {
-      std::printf("{\"kind\": \"data_shuffled\", \"error\": \"%s\", \"handles\": %zu}\n", d2.failed, d2.handles.size());
-    }
-    d2.destroy();
-  }
-  // 5. data and rebuilt in one physically contiguous allocation: rebuilt at data_end + delta
+  // 3. data and rebuilt in one physically contiguous allocation: rebuilt at data_end + delta
   if (!skip_delta) {
     const size_t MB = 1 << 20;
     const size_t deltas[] = {0, 4096, 65536, 256 * 1024, MB, 2 * MB, 3 * MB, 4 * MB, 6 * MB, 8 * MB,
@@ -289,6 +245,51 @@ int main(int argc, char** argv) {
         std::fflush(stdout);
       }
       HIPCHK(hipFree(base));
+    }
+  }
+  // 4. the first (slow?) plain buffer again, then the data copied into shuffled chunks
+  out("hipMalloc_again", timed(data, plain[0]), plain[0], ",\"order\": 0");
+  if (data_vmm) {  // (aborted inside the runtime on three boxes with 64-MB handles: opt-in)
+    const size_t dchunk = std::max<size_t>(chunk, 64u << 20);  // fewer handles for 12 GB
+    std::vector<size_t> dperm((data_bytes + dchunk - 1) / dchunk);
+    std::iota(dperm.begin(), dperm.end(), 0);
+    std::shuffle(dperm.begin(), dperm.end(), std::mt19937_64(0xDA7A));
+    VmmBuffer d2;
+    if (d2.create(data_bytes, dchunk, dperm, dev)) {
+      // a kernel copy: the runtime's memcpy does not know virtual-memory ranges
+      if (fec_copy_dev(ctx, data, static_cast<uint8_t*>(d2.va), data_bytes, st) != 0) {
+        std::printf("{\"error\": \"copy: %s\"}\n", fec_hip_last_error());
+        return 1;
+      }
+      HIPCHK(hipStreamSynchronize(st));
+      for (int i = 0; i < 3; ++i)
+        out("data_shuffled", timed(static_cast<uint8_t*>(d2.va), plain[i]), plain[i],
+            (",\"order\": " + std::to_string(i)).c_str());
+    } else {
+      std::printf("{\"kind\": \"data_shuffled\", \"error\": \"%s\", \"handles\": %zu}\n", d2.failed, d2.handles.size());
+    }
+    d2.destroy();
+  }
+  // 5. virtual-memory buffers (last: after a virtual range is freed, the next large ordinary
+  // allocation aborted inside the runtime on three boxes, "Memobj map does not have ptr"): the same physical handles in three virtual orders
+  const size_t nchunks = (par_bytes + chunk - 1) / chunk;
+  std::vector<size_t> ident(nchunks), rev(nchunks), shuf(nchunks);
+  std::iota(ident.begin(), ident.end(), 0);
+  std::reverse_copy(ident.begin(), ident.end(), rev.begin());
+  shuf = ident;
+  std::shuffle(shuf.begin(), shuf.end(), std::mt19937_64(0xC3C3));
+  for (int pass = 0; pass < 2; ++pass) {
+    const char* names[3] = {"vmm_in_order", "vmm_reversed", "vmm_shuffled"};
+    const std::vector<size_t>* perms[3] = {&ident, &rev, &shuf};
+    for (int v = 0; v < 3; ++v) {
+      VmmBuffer b;
+      if (!b.create(par_bytes, chunk, *perms[v], dev)) {
+        std::printf("{\"kind\": \"%s\", \"error\": \"%s\"}\n", names[v], b.failed);
+        b.destroy();
+        continue;
+      }
+      out(names[v], timed(data, static_cast<uint8_t*>(b.va)), b.va, (",\"pass\": " + std::to_string(pass)).c_str());
+      b.destroy();
     }
   }
   for (auto* p : plain) HIPCHK(hipFree(p));

@@ -2,7 +2,7 @@
 //
 // Uses the product's own definitions (fec_kernels.hpp: ServerSlot / ServerControl / ServerCoord
 // layout, server_tag, server_scrub_after, the inline chunk constants) and checks the properties
-// the server's and the host's acceptance rules rest on:
+// the server's and the host's acceptance rules rest on (DESIGN_HISTORY.md §8c round 5):
 //  1. tags: 1 .. epoch, never 0 (the zeroed state); a slot's tags over `epoch` consecutive laps are
 //     all different; the scrub falls on the last lap of every epoch;
 //  2. no stale acceptance: a slot modelled over many laps at 8-B granularity -- the host's halves
