@@ -740,12 +740,13 @@ class Bench:
         ctx.fill_random_dev(data, data.numel(), SEED + 2, byte_offset=g0 * k * P, stream=sp)
         dec_bytes = dec_read = 0
         if api == "auto":
-            # Sparse loss (a loss profile: C5 ~10% of groups lose data): the packed rows, whose
-            # one-launch form (recover_runs: rows leave each workgroup as one run) beats the slot
-            # rows by 7-15% (profiles/r04_probe_runs_*.txt).  Dense loss (C3): the slot rows,
-            # which never lost by more than 4% on any box measured against packed rows
-            # (profiles/r03_final/ab_decode_api_box*.jsonl; same HBM bytes by PMC).
-            api = "packed" if cfg.get("loss") and packed_supported(k, r, P) else "recover"
+            # The slot rows (fec_recover_batch_rs_dev) at every density.  Dense loss (C3): never
+            # more than 4% behind the packed rows on any box measured, same HBM bytes by PMC
+            # (profiles/r03_final/ab_decode_api_box*.jsonl).  Sparse loss (C5, the 8-groups-per-wave
+            # form by the loss hint) against the packed rows' one-launch recover_runs, this build,
+            # in this step, two boxes x 3 rounds (scripts/ab_c5_api.sh, profiles/r06/ab_c5_api_box*.jsonl):
+            # median 0.2410 vs 0.2437 ms in the step, 0.2392 vs 0.2443 ms isolated.
+            api = "recover"
         recover = cfg["decode"] and api in ("recover", "packed")
         rebuilt = dev_buffer(G * r * P, args.rebuilt_offset) if recover else None
         row_start = torch.empty(G, dtype=torch.int32, device="cuda") if cfg["decode"] and api == "packed" else None
@@ -894,10 +895,14 @@ class Bench:
             kernels["decode"]["api"] = api
             kernels["decode"]["isolated"] = isolated(lambda: decode_call(api), dec_bytes)
             # the other decode API on the same buffers, for comparison (not in `value`)
-            other = {"packed": "recover", "recover": "in-place"}.get(api, "recover")
+            # (sparse loss: the packed rows, the form the slot rows were chosen over)
+            other = {"packed": "recover",
+                     "recover": "packed" if cfg.get("loss") and packed_supported(k, r, P) else "in-place"}.get(api, "recover")
             if other_api:
                 if other == "recover" and rebuilt is None:
                     rebuilt = dev_buffer(G * r * P, args.rebuilt_offset)
+                if other == "packed" and row_start is None:
+                    row_start = torch.empty(G, dtype=torch.int32, device="cuda")
                 kernels["decode"]["other_api"] = {"api": other, **isolated(lambda: decode_call(other), dec_bytes)}
         # The box's own HBM copy rate (fec_copy_dev: the encode's 16-B-per-lane pattern, no
         # arithmetic), measured the same way once per process: box-to-box spread is a few

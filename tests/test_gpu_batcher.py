@@ -240,3 +240,22 @@ def test_multi_device_batcher_concurrent_streams_and_decoder(quicfec_mod, oracle
         st_e, st_d = enc.stats(), dec.stats()
     assert not errors, errors[:5]
     assert st_e["groups"] == S * G and st_d["groups"] == S * G
+
+
+@pytest.mark.parametrize("r", [1, 3])
+def test_call_site_tool_batcher_rows_checked(r):
+    """bench.py's call_site.batcher_16_r{1,3} (tools/call_site.cpp `batcher`): 16 streams'
+    BatchedFECEncoders on one shared batcher, submitting without waiting; the tool checks every
+    repair row of every group (row 0 the XOR, rows 1.. from fec_parity_matrix and a GF(2^8)
+    multiply of its own) and every group collected.  A short run here: no errors, rows flowed."""
+    import json
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parents[1] / "quic-test_amd" / "lib" / "call_site"
+    assert exe.exists(), "build() makes quic-test_amd/lib/call_site (csrc Makefile target bench_tools)"
+    out = subprocess.run([str(exe), "batcher", "16", "0.3", str(r)], capture_output=True, text=True, timeout=90)
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert out.returncode == 0 and lines, (out.returncode, out.stdout, out.stderr)
+    rec = json.loads(lines[-1])
+    assert rec["mode"] == "batcher" and rec["r"] == r and rec["errors"] == 0, rec
+    assert rec["groups"] > 1000 and rec["batches"] >= 1, rec
