@@ -32,6 +32,14 @@
 #include "fec_kernels.hpp"
 #include "fec_knobs.hpp"
 
+// Forms only the probes (tools/probe_*.hip, built with -DQUICFEC_PROBE_FORMS) select: the
+// library's own choice never reaches them, so the product library does not carry them.
+#ifdef QUICFEC_PROBE_FORMS
+#define QFEC_PROBE_ONLY(...) (__VA_ARGS__)
+#else
+#define QFEC_PROBE_ONLY(...) hipErrorNotSupported
+#endif
+
 namespace qfec {
 namespace {
 
@@ -2859,12 +2867,15 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     }
     return run_decode_wave<0, 8, kNtStore | kNoCoefBranch | kCompactOut>(a, s);
   }
-  const bool separate_out = a.out != nullptr && a.out != a.data;  // decode_v16 lacks it
   if (tiled) {
+#ifdef QUICFEC_PROBE_FORMS
     const bool nt = a.variant != kDecodeTiledPlain;
+#else
+    constexpr bool nt = true;  // the library never sets a variant (the plain forms are probe-only)
+#endif
 #define QFEC_TILED(KK, RR)                                                                   \
   if (a.k == KK && a.r == RR)                                                                \
-    return nt ? run_decode_tiled<KK, RR, kNtStore>(a, tile, s) : run_decode_tiled<KK, RR, 0>(a, tile, s);
+    return nt ? run_decode_tiled<KK, RR, kNtStore>(a, tile, s) : QFEC_PROBE_ONLY(run_decode_tiled<KK, RR, 0>(a, tile, s));
     QFEC_TILED(10, 3)
     QFEC_TILED(10, 1)
     QFEC_TILED(20, 5)
@@ -2879,6 +2890,10 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     const hipError_t e = try_decode_fused(a, s, false);
     if (e != hipErrorNotSupported) return e;
   }
+#ifdef QUICFEC_PROBE_FORMS
+  // Probe-only forms (tools/probe_decode.hip sets DecodeLaunch::variant; the library never does):
+  // no branch on coefficients 0 / 1, the plain-store wave kernel, 16-B lanes only (decode_v16).
+  const bool separate_out = a.out != nullptr && a.out != a.data;  // decode_v16 lacks it
   if (a.variant == kDecodeWaveNoBranch && !separate_out) {
 #define QFEC_WAVE_NB(KK, RR) \
   if (a.k == KK && a.r == RR) return run_decode_wave<KK, RR, kNtStore | kNoCoefBranch>(a, s);
@@ -2886,11 +2901,21 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     QFEC_WAVE_NB(20, 5)
 #undef QFEC_WAVE_NB
   }
-  if (a.variant != kDecodeWavePerGroup || separate_out) {
-    const bool nt = a.variant != kDecodeWavePlain;
+  if (a.variant == kDecodeWavePerGroup && !separate_out) {
+    if (a.k == 10 && a.r == 3) return run_decode_v16<10, 3>(a, s);
+    if (a.k == 10 && a.r == 1) return run_decode_v16<10, 1>(a, s);
+    if (a.k == 20 && a.r == 5) return run_decode_v16<20, 5>(a, s);
+    if (a.k == 4 && a.r == 2) return run_decode_v16<4, 2>(a, s);
+    return run_decode_v16<0, 8>(a, s);
+  }
+  const bool nt = a.variant != kDecodeWavePlain;
+#else
+  constexpr bool nt = true;
+#endif
+  {
 #define QFEC_WAVE(KK, RR)                                                                    \
   if (a.k == KK && a.r == RR)                                                                \
-    return nt ? run_decode_wave<KK, RR, kNtStore>(a, s) : run_decode_wave<KK, RR, 0>(a, s);
+    return nt ? run_decode_wave<KK, RR, kNtStore>(a, s) : QFEC_PROBE_ONLY(run_decode_wave<KK, RR, 0>(a, s));
     QFEC_WAVE(10, 3)
     QFEC_WAVE(10, 1)
     QFEC_WAVE(20, 5)
@@ -2901,13 +2926,8 @@ hipError_t launch_decode(const DecodeLaunch& a, hipStream_t s) {
     // 4.13 -> 4.79 TB/s, 12+6 2.62 -> 3.20, 16+4 2.67 -> 3.40.  Its tables staged through
     // LDS (kLdsTabs) lose here (2.2-2.8 TB/s): the records of these codebooks are hit often
     // enough in the scalar cache, and the wait for the tables precedes the survivor loads.
-    return nt ? run_decode_wave<0, 8, kNtStore | kNoCoefBranch>(a, s) : run_decode_wave<0, 8, 0>(a, s);
+    return nt ? run_decode_wave<0, 8, kNtStore | kNoCoefBranch>(a, s) : QFEC_PROBE_ONLY(run_decode_wave<0, 8, 0>(a, s));
   }
-  if (a.k == 10 && a.r == 3) return run_decode_v16<10, 3>(a, s);
-  if (a.k == 10 && a.r == 1) return run_decode_v16<10, 1>(a, s);
-  if (a.k == 20 && a.r == 5) return run_decode_v16<20, 5>(a, s);
-  if (a.k == 4 && a.r == 2) return run_decode_v16<4, 2>(a, s);
-  return run_decode_v16<0, 8>(a, s);
 }
 
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64_t byte_offset,
