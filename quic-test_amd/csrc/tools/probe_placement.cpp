@@ -15,7 +15,11 @@
 //   * the data itself copied into chunk-shuffled memory, with the first (slow) rebuilt buffer.
 // One JSON object per line.
 //
-//   probe_placement [--chunk-mb 2] [--reps 10] [--groups 1000000] [--skip-delta] [--data-vmm]
+//   probe_placement [--chunk-mb 2] [--reps 10] [--groups 1000000] [--skip-delta] [--data-vmm] [--waves]
+//
+// --waves (built against libfec_hip_test.so, whose QUICFEC_DECODE_WAVES caps the recover's
+// occupancy): the first plain buffer and a physically contiguous one at 8 .. 40 waves per CU and
+// uncapped -- whether fewer requests in flight ease the slow placement's DRAM credit stalls.
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
@@ -111,13 +115,14 @@ int main(int argc, char** argv) {
   size_t chunk_mb = 2;
   int reps = 10;
   uint64_t G = 1000000;
-  bool skip_delta = false, data_vmm = false;
+  bool skip_delta = false, data_vmm = false, waves_sweep = false;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--chunk-mb") && i + 1 < argc) chunk_mb = std::strtoull(argv[++i], nullptr, 10);
     else if (!std::strcmp(argv[i], "--reps") && i + 1 < argc) reps = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--groups") && i + 1 < argc) G = std::strtoull(argv[++i], nullptr, 10);
     else if (!std::strcmp(argv[i], "--skip-delta")) skip_delta = true;
     else if (!std::strcmp(argv[i], "--data-vmm")) data_vmm = true;
+    else if (!std::strcmp(argv[i], "--waves")) waves_sweep = true;
   }
   if (fec_hip_device_count() <= 0) {
     std::printf("{\"error\": \"no GPU\"}\n");
@@ -212,6 +217,21 @@ int main(int argc, char** argv) {
     } else {
       std::printf("{\"kind\": \"contiguous\", \"error\": \"alloc\"}\n");
     }
+  }
+  if (waves_sweep) {
+    uint8_t* rc = nullptr;
+    const bool have_c =
+        hipExtMallocWithFlags(reinterpret_cast<void**>(&rc), par_bytes, hipDeviceMallocContiguous) == hipSuccess;
+    for (int pass = 0; pass < 2; ++pass)
+      for (int w : {0, 8, 12, 16, 20, 24, 32, 40}) {
+        if (w) setenv("QUICFEC_DECODE_WAVES", std::to_string(w).c_str(), 1);
+        else unsetenv("QUICFEC_DECODE_WAVES");
+        const std::string ex = ",\"waves\": " + std::to_string(w) + ", \"pass\": " + std::to_string(pass);
+        out("waves_hipMalloc", timed(data, plain[0]), plain[0], ex.c_str());
+        if (have_c) out("waves_contiguous", timed(data, rc), rc, ex.c_str());
+      }
+    unsetenv("QUICFEC_DECODE_WAVES");
+    if (have_c) HIPCHK(hipFree(rc));
   }
   // 3. data and rebuilt in one physically contiguous allocation: rebuilt at data_end + delta
   if (!skip_delta) {
