@@ -548,7 +548,9 @@ def lib_sha256() -> str:
     """Hash of the libfec_hip.so this process loads (the build being timed)."""
     import hashlib
     import quicfec
-    return hashlib.sha256(Path(quicfec.LIB_PATH).read_bytes()).hexdigest()
+    # the library quicfec.load_library() loads: QUICFEC_LIB when set (tuning runs against the test
+    # library), else libfec_hip.so
+    return hashlib.sha256(Path(os.environ.get("QUICFEC_LIB", quicfec.LIB_PATH)).read_bytes()).hexdigest()
 
 
 def workload_key(cfg: dict, G: int) -> dict:

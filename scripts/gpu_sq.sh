@@ -5,6 +5,8 @@
 # as QUICFEC_ENCODE_BITS, which the bench processes inherit).
 set -uo pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
+# the tuning switches live in the test library (quic-test_amd/csrc/fec_knobs.hpp); bench.py loads it through quicfec
+export QUICFEC_LIB="${QUICFEC_LIB:-$ROOT/quic-test_amd/lib/libfec_hip_test.so}"
 OUT="$ROOT/gpurun_out/sq${SQ_TAG:-}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
