@@ -322,3 +322,28 @@ def test_bench_call_site_reads_the_tool_lines(monkeypatch, tmp_path):
     out = bench.call_site(ref_1t_GiBps=2 * gib, seconds=0.1)
     assert out["ref_encode_batch_1t_groups_per_s"] == 2000.0
     assert out["batcher_16_r3"]["vs_ref_1t"] == 0.5
+
+
+def test_test_switch_names_match_their_enum():
+    """csrc/fec_knobs.cpp maps each TestKnob (fec_knobs.hpp) to its environment name by position:
+    the two lists must line up one for one (kMaxWaveBlocks <-> QUICFEC_MAX_WAVE_BLOCKS, the
+    resident test hooks under QUICFEC_RESIDENT_TEST_*), or a test would set one switch and move
+    another."""
+    csrc = REPO / "quic-test_amd" / "csrc"
+    hpp = (csrc / "fec_knobs.hpp").read_text()
+    enum = re.search(r"enum class TestKnob : int \{(.*?)\};", hpp, re.S).group(1)
+    keys = [m.group(1) for m in re.finditer(r"^\s*k(\w+),?", enum, re.M)]
+    assert keys[-1] == "Count"
+    keys = keys[:-1]
+    cpp = (csrc / "fec_knobs.cpp").read_text()
+    names = re.findall(r'"(QUICFEC_[A-Z0-9_]+)"', re.search(r"kNames\[\] = \{(.*?)\};", cpp, re.S).group(1))
+    assert len(names) == len(keys)
+
+    def env_of(key):
+        snake = re.sub(r"(?<!^)(?=[A-Z])", "_", key).upper()
+        for hook in ("NO_LAUNCH", "EPOCH", "TEAR", "FAIL_AT"):   # the fault-injection hooks
+            if snake == "RESIDENT_" + hook:
+                return "QUICFEC_RESIDENT_TEST_" + hook.replace("NO_LAUNCH", "NOLAUNCH")
+        return "QUICFEC_" + snake
+
+    assert [env_of(k) for k in keys] == names
