@@ -133,6 +133,41 @@ def bind_local_device(local: int, world: int, ndev: int) -> int:
     raise SystemExit(f"bench.py: local rank {local} of {world} needs GPU {local}, only {ndev} visible")
 
 
+def parse_cpulist(text: str) -> set:
+    """CPUs of a sysfs cpulist ("0-7,16-23")."""
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus.update(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def bind_host_to_gpu(local: int, sysfs: Path = Path("/sys/bus/pci/devices")) -> dict:
+    """One rank of N > 1: confine this process's threads (and so the node its page-locked host
+    buffers are allocated on) to the CPUs local to its GPU's PCIe link, as sysfs lists them, within
+    the CPUs it may already use.  On a two-socket node half the GPUs hang off each socket; without
+    this the host-resident legs (c5_e2e) of some ranks would read and write memory of the other
+    socket across the inter-socket link.  Returns what was done (the line's `host_binding`)."""
+    import torch
+    p = torch.cuda.get_device_properties(local)
+    bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    out = {"gpu": local, "pci": bdf}
+    try:
+        cpus = parse_cpulist((sysfs / bdf / "local_cpulist").read_text())
+        node = int((sysfs / bdf / "numa_node").read_text())
+    except (OSError, ValueError):
+        return {**out, "bound": False, "why": "no sysfs entry"}
+    cur = set(os.sched_getaffinity(0))
+    want = cpus & cur
+    out.update({"numa_node": node, "local_cpus": len(want), "allowed_cpus": len(cur)})
+    if not want or want == cur:
+        return {**out, "bound": False, "why": "no local CPU allowed" if not want else "already local"}
+    os.sched_setaffinity(0, want)
+    return {**out, "bound": True}
+
+
 def _free_port() -> int:
     import socket
     with socket.socket() as s:
@@ -984,7 +1019,10 @@ def main() -> int:
     # one process per GPU; bind the GPU before RCCL creates its communicator.
     local = bind_local_device(local, world, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    host_binding = None
     if world > 1:
+        # before any host allocation (N = 1 keeps every core: its cpu_baseline uses them)
+        host_binding = bind_host_to_gpu(local)
         dist.init_process_group(backend=dist_backend(), init_method="env://")
     cfg = dict(CONFIGS[args.config])
     if args.loss is not None:
@@ -1058,6 +1096,8 @@ def main() -> int:
             out["buffers"] = head["buffers"]
         if legs:
             out.update(legs)
+        if host_binding is not None:
+            out["host_binding"] = host_binding  # rank 0's (every rank binds to its own GPU's CPUs)
         out["wall_s"] = wall
         print(json.dumps(out), flush=True)
     if world > 1:

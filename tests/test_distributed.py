@@ -202,3 +202,33 @@ def test_spawn_parent_never_maps_hip_runtime():
             % str(REPO))
     bad = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
     assert bad.returncode != 0 and "HIP runtime" in bad.stderr
+
+
+def test_rank_binds_host_threads_to_its_gpu(monkeypatch, tmp_path):
+    """bench.py ranks of N > 1 confine their threads to the CPUs sysfs lists as local to their
+    GPU (within the CPUs they may use), so each rank's page-locked buffers sit on its GPU's
+    socket; nothing changes when none of those CPUs is allowed or all already are."""
+    import os
+    import types
+    import torch
+    import bench
+    assert bench.parse_cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    dev = tmp_path / "0000:c1:00.0"
+    dev.mkdir()
+    (dev / "numa_node").write_text("1\n")
+    props = types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0xC1, pci_device_id=0)
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda i: props)
+    allowed = set(range(16))
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(allowed))
+    calls = []
+    monkeypatch.setattr(os, "sched_setaffinity", lambda pid, cpus: calls.append(set(cpus)))
+    (dev / "local_cpulist").write_text("8-23\n")
+    rec = bench.bind_host_to_gpu(3, sysfs=tmp_path)
+    assert rec["bound"] and rec["numa_node"] == 1 and rec["pci"] == "0000:c1:00.0" and rec["local_cpus"] == 8
+    assert calls == [set(range(8, 16))]
+    (dev / "local_cpulist").write_text("32-47\n")                 # none of them allowed: leave it
+    assert not bench.bind_host_to_gpu(3, sysfs=tmp_path)["bound"] and len(calls) == 1
+    (dev / "local_cpulist").write_text("0-63\n")                  # every allowed CPU is local already
+    assert not bench.bind_host_to_gpu(3, sysfs=tmp_path)["bound"] and len(calls) == 1
+    props.pci_bus_id = 0x05                                       # no sysfs entry for the device
+    assert bench.bind_host_to_gpu(3, sysfs=tmp_path)["why"] == "no sysfs entry"
