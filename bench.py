@@ -559,8 +559,8 @@ def call_site(ref_1t_GiBps=None, seconds: float = 2.0) -> dict:
             out[name] = {"error": f"exit {p.returncode}: {p.stderr.strip()[-300:]}"}
             break
         rec = json.loads(lines[-1])
-        out[name] = {k: rec[k] for k in ("groups_per_s", "delay_us", "errors", "resident_inline", "resident_vram",
-                                         "batches", "max_batch") if k in rec}
+        out[name] = {k: rec[k] for k in ("groups_per_s", "delay_us", "errors", "expired", "resident_inline",
+                                         "resident_vram", "batches", "max_batch") if k in rec}
         if ref_1t_GiBps and "groups_per_s" in rec:
             out[name]["vs_ref_1t"] = round(rec["groups_per_s"] / out["ref_encode_batch_1t_groups_per_s"], 3)
     return out

@@ -16,6 +16,8 @@
 //   call_site batcher S SECONDS R
 //   -> one JSON line: {"mode", "streams", "groups", "seconds", "groups_per_s", "delay_us": {p50, p99},
 //                      "errors", "resident_calls", "resident_inline", "resident_vram"}
+//      (batcher: "errors" = wrong or missing rows and failed calls; "expired" = groups whose
+//       result the ring overwrote before their stream collected it, reported apart)
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -171,7 +173,7 @@ int batcher(int S, double seconds, int r) {
   }
   std::mutex mu;
   std::vector<double> all;
-  std::atomic<long> errors{0};
+  std::atomic<long> errors{0}, expired{0};
   const auto t0 = Clock::now();
   const auto t_end = t0 + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(seconds));
   std::vector<std::thread> th;
@@ -185,7 +187,7 @@ int batcher(int S, double seconds, int r) {
       std::vector<Bytes> out;
       auto drain = [&](int64_t timeout) {
         out.clear();
-        if (!be.Poll(&out, timeout).ok()) ++errors;
+        const Error e = be.Poll(&out, timeout);
         const auto now = Clock::now();
         if (out.size() % size_t(r) != 0) ++errors;
         for (size_t q = 0; q + size_t(r) <= out.size(); q += size_t(r), ++head) {
@@ -197,6 +199,14 @@ int batcher(int S, double seconds, int r) {
                 std::memcmp(pkt.data() + hl, want.data() + (size_t(grp[head]) * r + i) * kP, kP) != 0)
               ++errors;
           }
+        }
+        // Poll stops at a ticket it could not collect and drops it: the rows before it are in
+        // `out`, the dropped one is the next group.  A result the ring overwrote before this
+        // stream came back for it (a thread descheduled while 2 * slabs * max_groups newer groups
+        // were encoded) is counted as expired, any other failure as an error.
+        if (!e.ok()) {
+          if (e.msg.find("expired") != std::string::npos) ++expired; else ++errors;
+          if (head < sub.size()) ++head;
         }
       };
       for (uint64_t i = 0; Clock::now() < t_end; ++i) {
@@ -220,9 +230,10 @@ int batcher(int S, double seconds, int r) {
   auto pct = [&](double p) { return all.empty() ? 0.0 : all[std::min(all.size() - 1, size_t(p * all.size()))]; };
   std::printf("{\"mode\": \"batcher\", \"streams\": %d, \"r\": %d, \"max_groups\": %d, \"deadline_us\": 1000, "
               "\"groups\": %zu, \"seconds\": %.3f, \"groups_per_s\": %.1f, \"delay_us\": {\"p50\": %.2f, \"p99\": %.2f}, "
-              "\"errors\": %ld, \"batches\": %llu, \"max_batch\": %llu}\n",
+              "\"errors\": %ld, \"expired\": %ld, \"batches\": %llu, \"max_batch\": %llu}\n",
               S, r, kMaxGroups, all.size(), wall, double(all.size()) / wall, pct(0.5), pct(0.99), errors.load(),
-              (unsigned long long)(st.size() > 1 ? st[1] : 0), (unsigned long long)(st.size() > 4 ? st[4] : 0));
+              expired.load(), (unsigned long long)(st.size() > 1 ? st[1] : 0),
+              (unsigned long long)(st.size() > 4 ? st[4] : 0));
   std::fflush(stdout);
   return errors ? 1 : 0;
 }

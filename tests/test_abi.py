@@ -299,7 +299,7 @@ def test_bench_call_site_without_tool_is_skipped(monkeypatch, tmp_path):
 def test_bench_call_site_reads_the_tool_lines(monkeypatch, tmp_path):
     """bench.py's call_site section runs the tool once per leg (raw, 1 and 16 streams, the shared
     batcher at r = 1 and 3) and keeps
-    each leg's rate, delay percentiles, error count and ring kind from its last JSON line."""
+    each leg's rate, delay percentiles, error and expiry counts and ring kind from its last JSON line."""
     import importlib.util
     import stat
     spec = importlib.util.spec_from_file_location("bench_mod2", REPO / "bench.py")
@@ -308,15 +308,15 @@ def test_bench_call_site_reads_the_tool_lines(monkeypatch, tmp_path):
     tool = tmp_path / "call_site"
     tool.write_text("#!/bin/sh\necho 'warming up'\n"
                     "echo '{\"mode\": \"'$1'\", \"streams\": '${2:-1}', \"groups_per_s\": 1000.0, "
-                    "\"delay_us\": {\"p50\": 5.5, \"p99\": 9.0}, \"errors\": 0, \"resident_inline\": 7, "
-                    "\"resident_vram\": 1, \"extra\": 3}'\n")
+                    "\"delay_us\": {\"p50\": 5.5, \"p99\": 9.0}, \"errors\": 0, \"expired\": 0, "
+                    "\"resident_inline\": 7, \"resident_vram\": 1, \"extra\": 3}'\n")
     tool.chmod(tool.stat().st_mode | stat.S_IEXEC)
     monkeypatch.setattr(bench, "CALL_SITE_TOOL", tool)
     out = bench.call_site(seconds=0.1)
     assert set(out) >= {"raw", "streams_1", "streams_16", "batcher_16_r1", "batcher_16_r3", "reference_call"}
     for leg in ("raw", "streams_1", "streams_16", "batcher_16_r1", "batcher_16_r3"):
         assert out[leg] == {"groups_per_s": 1000.0, "delay_us": {"p50": 5.5, "p99": 9.0}, "errors": 0,
-                            "resident_inline": 7, "resident_vram": 1}
+                            "expired": 0, "resident_inline": 7, "resident_vram": 1}
     # beside the reference library on one core (cpu_baseline's ref_encode_batch_1t_GiBps)
     gib = 1000.0 * 12000 / 2**30
     out = bench.call_site(ref_1t_GiBps=2 * gib, seconds=0.1)

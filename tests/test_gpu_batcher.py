@@ -247,7 +247,11 @@ def test_call_site_tool_batcher_rows_checked(r):
     """bench.py's call_site.batcher_16_r{1,3} (tools/call_site.cpp `batcher`): 16 streams'
     BatchedFECEncoders on one shared batcher, submitting without waiting; the tool checks every
     repair row of every group (row 0 the XOR, rows 1.. from fec_parity_matrix and a GF(2^8)
-    multiply of its own) and every group collected.  A short run here: no errors, rows flowed."""
+    multiply of its own) and every group collected.  A short run here: no wrong or missing rows,
+    rows flowed.  A result the ring overwrote before its stream came back for it (the stream's
+    thread descheduled while 2 x 16 x 512 newer groups were encoded -- the batcher's documented
+    expiry, fec_batcher.cpp) is reported as `expired`, not as a wrong row; on a box whose CPU
+    share is busy that can happen to a few groups, so it is bounded rather than forbidden."""
     import json
     import subprocess
     from pathlib import Path
@@ -258,4 +262,5 @@ def test_call_site_tool_batcher_rows_checked(r):
     assert out.returncode == 0 and lines, (out.returncode, out.stdout, out.stderr)
     rec = json.loads(lines[-1])
     assert rec["mode"] == "batcher" and rec["r"] == r and rec["errors"] == 0, rec
+    assert rec["expired"] <= rec["groups"] // 100, rec
     assert rec["groups"] > 1000 and rec["batches"] >= 1, rec
