@@ -370,7 +370,9 @@ class BatchedFECEncoder {
   AddPacketResult AddPacket(const Bytes& p, uint64_t id) { return AddPacket(p.data(), p.size(), id); }
   // Asynchronous: the k-th packet submits without waiting; Poll appends the repair packets
   // of finished groups (in group order, row order) and waits up to timeoutUs for the oldest
-  // outstanding one (0: no wait, < 0: all of them).
+  // outstanding one (0: no wait, < 0: all of them).  A group it cannot collect (its result
+  // expired in the batcher's ring, or its batch failed) is dropped from the outstanding list
+  // and ends the call with that error; the rows appended before it stay in `out`.
   Error AddPacketAsync(const uint8_t* packet, size_t len, uint64_t packetID);
   Error Poll(std::vector<Bytes>* out, int64_t timeoutUs = 0);
   size_t outstanding() {

@@ -281,6 +281,8 @@ func (e *BatchedFECEncoder) AddPacketAsync(packet []byte, packetID uint64) error
 
 // Poll returns the repair packets of finished groups in group order (row order within a
 // group), waiting up to timeout for the oldest outstanding one (0: no wait, < 0: for all).
+// A group it cannot collect (its result expired in the batcher's ring, or its batch failed)
+// is dropped and ends the call with that error, returned beside the rows collected before it.
 func (e *BatchedFECEncoder) Poll(timeout time.Duration) ([][]byte, error) {
 	e.mu.Lock()
 	defer e.mu.Unlock()
