@@ -232,3 +232,34 @@ def test_rank_binds_host_threads_to_its_gpu(monkeypatch, tmp_path):
     assert not bench.bind_host_to_gpu(3, sysfs=tmp_path)["bound"] and len(calls) == 1
     props.pci_bus_id = 0x05                                       # no sysfs entry for the device
     assert bench.bind_host_to_gpu(3, sysfs=tmp_path)["why"] == "no sysfs entry"
+
+
+@pytest.mark.gpu
+def test_rccl_group_runs_the_bench_reductions():
+    """The reductions of a multi-GPU bench run (barrier with the rank's device, MAX and SUM of a
+    float64 on the GPU) over a real RCCL communicator: one rank on this box's GPU, in a child
+    process so the communicator does not outlive the test.  The driver's N = 2/4/8 runs use the
+    same calls; this is the part of them a one-GPU box can run."""
+    import json
+    import subprocess
+    code = f"""
+import json, os, sys
+sys.path.insert(0, {str(REPO)!r})
+import torch, torch.distributed as dist
+import bench
+torch.cuda.set_device(0)
+dist.init_process_group(backend=bench.dist_backend(), init_method="env://")
+bench.barrier()
+mx = bench.reduce_max(1.25)
+sm = bench.reduce_sum(3.0)
+mn = bench.reduce_min(0.5)
+bench.barrier()
+print(json.dumps({{"backend": dist.get_backend(), "max": mx, "sum": sm, "min": mn}}), flush=True)
+dist.destroy_process_group()
+"""
+    env = {k: v for k, v in os.environ.items() if k != "QUICFEC_DIST_BACKEND"}
+    env.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, (out.stdout, out.stderr[-2000:])
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec == {"backend": "nccl", "max": 1.25, "sum": 3.0, "min": 0.5}, rec
