@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
-# Round 6 evidence on the current build, in two gpurun calls (PART=1: A-C, PART=2: D; everything
-# in gpurun_out/${EVID}/):
+# Round 6 evidence on the current build, in two gpurun calls (PART=1: A-C, PART=2: D, PART=3: D
+# without PMC; everything in gpurun_out/${EVID}/):
 #  A. the GPU suite and smoke (prints the library's source hash against the tree's);
 #  B. the legacy call site and the exit-path program under rocprofv3 (each must exit 0);
 #  C. a soak of the resident ring (16 and 100 streams, every repair
@@ -37,8 +37,11 @@ QUICFEC_FUZZ_SEED=0x5EED5000 QUICFEC_FUZZ_BLOCKS=1200 timeout -k 10 900 python -
 tail -1 "$E/fuzz_12000.log"
 exit 0
 fi
+# PART=3: D on another box without the PMC passes (profiles/pmc_*.json stay as they are)
+if [ "${PART}" != 3 ]; then
 CFGS="${PMC_CFGS:-c2c3 c5 c4}" bash scripts/gpu_pmc.sh > "$E/pmc.log" 2>&1
 for c in ${PMC_CFGS:-c2c3 c5 c4}; do cp "$ROOT/gpurun_out/pmc_$c.json" "$ROOT/profiles/pmc_$c.json"; cp "$ROOT/gpurun_out/pmc_$c.json" "$E/pmc_$c.json"; done
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$E/prof" -o run --output-format csv -- \
   python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$E/prof_bench.json" 2> "$E/prof_bench.err"
 find "$E/prof" -name "*kernel_stats.csv" -exec cp {} "$E/kernel_stats.csv" \;
