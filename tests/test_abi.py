@@ -347,3 +347,30 @@ def test_test_switch_names_match_their_enum():
         return "QUICFEC_" + snake
 
     assert [env_of(k) for k in keys] == names
+
+
+def test_headers_are_plain_c_and_link_from_c(tmp_path, quicfec_mod):
+    """cgo compiles the preamble's headers with a C compiler (fec_cgo.go:10-14 includes
+    fec_xor_simd.h; cgo_hip.go adds fec_hip.h): both headers compile as ISO C99 with -pedantic and
+    no warning, and a C program that takes the address of every function they declare links
+    against libfec_hip.so and runs (the version string; no GPU call)."""
+    names = sorted(_declared_functions())
+    src = tmp_path / "abi_c.c"
+    src.write_text(
+        '#include "fec_xor_simd.h"\n#include "fec_hip.h"\n#include <stdio.h>\n'
+        "typedef void (*any_fn)(void);\n"
+        "static const any_fn fns[] = {\n" + "".join(f"  (any_fn){n},\n" for n in names) + "};\n"
+        "int main(void) {\n"
+        "  size_t i, n = 0;\n"
+        "  for (i = 0; i < sizeof fns / sizeof fns[0]; ++i) n += fns[i] != NULL;\n"
+        '  printf("%zu %s\\n", n, fec_hip_version());\n'
+        "  return 0;\n}\n")
+    exe = tmp_path / "abi_c"
+    lib_dir = Path(quicfec_mod.LIB_PATH).parent
+    for std in ("c99", "c11"):
+        subprocess.run(["gcc", f"-std={std}", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I", str(REPO / "include"),
+                        "-c", str(src), "-o", str(tmp_path / f"abi_{std}.o")], check=True)
+    subprocess.run(["gcc", "-std=c99", "-I", str(REPO / "include"), str(src), "-o", str(exe), "-L", str(lib_dir),
+                    "-lfec_hip", f"-Wl,-rpath,{lib_dir}"], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60, check=True).stdout.split()
+    assert int(out[0]) == len(names) and out[1] == "libfec_hip", out
