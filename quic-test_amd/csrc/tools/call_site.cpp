@@ -218,7 +218,8 @@ int batcher(int S, double seconds, int r) {
         drain(sub.size() - head >= 256 ? 100000 : 0);
       }
       if (!be.FlushAsync().ok()) ++errors;
-      drain(-1);
+      do drain(-1);  // a Poll that drops a ticket returns at it: go on with the rest
+      while (be.outstanding() > 0);
       if (head != sub.size()) ++errors;
       std::lock_guard<std::mutex> lk(mu);
       all.insert(all.end(), lat.begin(), lat.end());
