@@ -150,11 +150,15 @@ int saturate(int S, double seconds, int r, int deadline_us, int max_groups) {
       std::vector<Bytes> out;
       auto drain = [&](int64_t timeout) {
         out.clear();
-        if (!be.Poll(&out, timeout).ok()) ++errors;
+        const bool ok = be.Poll(&out, timeout).ok();
         const auto now = Clock::now();
         for (size_t n = out.size() / size_t(r); n > 0; --n, ++head) {
           lat.push_back(std::chrono::duration<double, std::micro>(now - sub[head]).count());
           ++groups;
+        }
+        if (!ok) {  // Poll dropped the ticket after the rows it returned
+          ++errors;
+          if (head < sub.size()) ++head;
         }
       };
       while (Clock::now() < t_end) {
@@ -164,7 +168,8 @@ int saturate(int S, double seconds, int r, int deadline_us, int max_groups) {
         drain(sub.size() - head >= 256 ? 100000 : 0);
       }
       if (!be.FlushAsync().ok()) ++errors;
-      drain(-1);
+      do drain(-1);
+      while (be.outstanding() > 0);
       std::lock_guard<std::mutex> lk(mu);
       all.insert(all.end(), lat.begin(), lat.end());
     });
