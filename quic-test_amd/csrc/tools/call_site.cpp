@@ -205,7 +205,7 @@ int batcher(int S, double seconds, int r) {
         // stream came back for it (a thread descheduled while 2 * slabs * max_groups newer groups
         // were encoded) is counted as expired, any other failure as an error.
         if (!e.ok()) {
-          if (e.msg.find("expired") != std::string::npos) ++expired; else ++errors;
+          if (e.code == FEC_ERR_RANGE) ++expired; else ++errors;
           if (head < sub.size()) ++head;
         }
       };

@@ -654,7 +654,11 @@ Error BatchedFECEncoder::collect(const Ticket& t, int64_t timeoutUs, std::vector
   const int rc = fec_batcher_wait(b_->raw(), t.ticket, rowbuf_.data(), static_cast<uint32_t>(b_->slot()), timeoutUs);
   *ready = rc != FEC_ERR_AGAIN;
   if (rc == FEC_ERR_AGAIN) return {};
-  if (rc < 0) return errorf("C++ encoding failed: %s", fec_batcher_last_error());
+  if (rc < 0) {
+    Error e = errorf("C++ encoding failed: %s", fec_batcher_last_error());
+    e.code = rc;  // FEC_ERR_RANGE: the result expired (a ticket of this encoder is always issued once)
+    return e;
+  }
   const size_t len = static_cast<size_t>(rc);
   for (int row = 0; row < r; ++row) {
     RSRepairHeader h;

@@ -38,6 +38,8 @@ using Bytes = std::vector<uint8_t>;
 // Go's `error`: empty = nil.
 struct Error {
   std::string msg;
+  int code = 0;  // the library's FEC_ERR_* when a library call failed (e.g. a batcher result
+                 // that expired: FEC_ERR_RANGE from fec_batcher_wait), else 0
   bool ok() const { return msg.empty(); }
   explicit operator bool() const { return !msg.empty(); }
 };

@@ -24,6 +24,7 @@ package fec
 import "C"
 
 import (
+	"errors"
 	"fmt"
 	"runtime"
 	"sync"
@@ -40,6 +41,11 @@ type SharedBatcher struct {
 }
 
 func batcherLastError() *C.char { return C.fec_batcher_last_error() }
+
+// ErrResultExpired: an async group's repair rows were overwritten in the batcher's ring before
+// its stream collected them (2 * slabs * maxGroups newer groups were encoded meanwhile).  Poll
+// returns it wrapped (errors.Is) after dropping that group.
+var ErrResultExpired = errors.New("fec: batcher result expired before it was collected")
 
 // NewSharedBatcher: groups of k packets of at most slotBytes, r repair packets per group,
 // up to maxGroups per launch, flushed `deadline` after the oldest pending group (0: as soon
@@ -174,6 +180,9 @@ func (s *SharedBatcher) wait(ticket int64, rows []byte, timeout time.Duration) (
 	switch {
 	case rc == C.FEC_ERR_AGAIN:
 		return 0, false, nil
+	case rc == C.FEC_ERR_RANGE:
+		// every ticket of a BatchedFECEncoder is issued and collected once: out of range = expired
+		return 0, true, fmt.Errorf("%w: %s", ErrResultExpired, C.GoString(C.fec_batcher_last_error()))
 	case rc < 0:
 		return 0, true, fmt.Errorf("C++ encoding failed: %s", C.GoString(C.fec_batcher_last_error()))
 	}

@@ -603,6 +603,37 @@ static void TestBatchedEncoderRSAsync() {
 }
 
 // Many streams, one batcher: every repair exact, groups of different streams share launches.
+// A result the ring overwrote before its stream came back for it: stream A submits a group,
+// stream B pushes 20 more through a batcher of 2-group slabs (1 asked, 2 the minimum: results
+// stay collectable for 8 newer groups and the ring slot is reused 12 groups on), then A polls.  A's Poll drops that group with the library's FEC_ERR_RANGE in
+// Error::code and no rows, and A's next group is collected whole (the Poll continues after it).
+static void TestBatchedEncoderExpiredPoll() {
+  const int k = 10;
+  auto sb = SharedFECBatcher::New(k, 1, 256, 2, 0, -1, 1);
+  CHECK(sb != nullptr);
+  if (!sb) return;
+  BatchedFECEncoder a(sb), b(sb);
+  std::vector<Bytes> first, second, out;
+  for (int i = 0; i < k; ++i) {
+    first.push_back(rnd(200, 7000 + i));
+    CHECK(a.AddPacketAsync(first.back().data(), first.back().size(), i).ok());
+  }
+  for (int g = 0; g < 20; ++g)
+    for (int i = 0; i < k; ++i) {
+      const auto res = b.AddPacket(rnd(100, 8000 + g * k + i), uint64_t(g * k + i));
+      CHECK(res.err.ok() && res.needsRedundancy == (i == k - 1));
+    }
+  for (int i = 0; i < k; ++i) {
+    second.push_back(rnd(150, 9000 + i));
+    CHECK(a.AddPacketAsync(second.back().data(), second.back().size(), k + i).ok());
+  }
+  CHECK(a.FlushAsync().ok());
+  const Error e = a.Poll(&out, -1);
+  CHECK(!e.ok() && e.code == FEC_ERR_RANGE && out.empty() && a.outstanding() == 1);
+  CHECK(a.Poll(&out, -1).ok() && a.outstanding() == 0 && out.size() == 1);
+  CHECK(out.size() == 1 && out[0] == go_redundancy(second, 1));
+}
+
 static void TestBatcherManyStreams() {
   const int S = 32, G = 30, k = 10;
   auto sb = SharedFECBatcher::New(k, 1, 1200, 16, 300);
@@ -862,6 +893,7 @@ int main() {
   TestRSDecoderPartialAndShort();
   TestBatchedEncoderMatchesHybrid();
   TestBatchedEncoderRSAsync();
+  TestBatchedEncoderExpiredPoll();
   TestBatcherManyStreams();
   TestBatcherDeadline();
   TestBatcherReservationStress();
